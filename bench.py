@@ -1,0 +1,334 @@
+#!/usr/bin/env python3
+"""Benchmark: BASELINE.json's metric on its 1-GPU config.
+
+Default workload (configs[1]): one step = one batched TAS filter + prioritize pass of
+4096 pending pods x 100k nodes x 16 rules (15 dontschedule + 1 scheduleonmetric) over
+a 64-metric node snapshot, every input resident in HBM.  value = pod-node evaluations
+per second over the whole job.  With N GPUs every rank evaluates its own 4096-pod
+batch against the same (replicated) snapshot — pending pods are independent, so the
+path shards by pod with no data-path collective ("scaling": "weak").
+
+Also: --workload gas (configs[2], 10k pods x 50k nodes x 8 cards) and
+--workload deschedule (configs[3] per-GPU sweep, 1M nodes x 64 rules).
+
+Prints ONE JSON line on rank 0.  See DESIGN.md §Measurement for the byte model.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
+
+import pas_amd  # noqa: E402
+from pas_amd import _lib  # noqa: E402
+from pas_amd import workload as wl  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "pod-node evals/sec (filter+prioritize), 4k pods×100k nodes; % of HBM peak"
+
+
+def dist_setup(n_gpus):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed_steps(step, steps, warmup, world):
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    return max_over_ranks(t1 - t0, world)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def load_traffic(name):
+    """Per-launch HBM bytes for `name` from the committed rocprofv3 PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+# ------------------------------------------------------------------------------- TAS
+
+def bench_tas(args, world, rank):
+    P, N, M, R = args.pods, args.nodes, args.metrics, args.rules - 1
+    ctx = pas_amd.Context(torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+    snap = wl.make_tas_snapshot(N, M, seed=0xC2)
+    batch = wl.make_tas_batch(snap, P, R, seed=0xC2 + 7919 * rank)
+    v_t, p_t = dev(snap.v_milli), dev(snap.present.view(np.int64))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.tas_snapshot_set_device(1, N, M, v_t, p_t, stream)
+    torch.cuda.synchronize()
+    snapshot_ms = (time.perf_counter() - t0) * 1e3
+    rules_t = dev(batch.rules.view(np.uint8))
+    off_t = dev(batch.rule_off)
+    prio_t = dev(batch.prio.view(np.uint8))
+    pass_t = torch.empty((P, pas_amd.w64(N)), dtype=torch.int64, device="cuda")
+    order_t = torch.empty((P, N), dtype=torch.int32, device="cuda")
+    len_t = torch.empty(P, dtype=torch.int32, device="cuda")
+    n_rules = len(batch.rules)
+    flags = pas_amd.PAS_TAS_FILTER | pas_amd.PAS_TAS_PRIORITIZE
+
+    def step():
+        ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pass_t, order_t,
+                            len_t, stream)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    elapsed = timed_steps(step, args.steps, 0, world)
+    ctx.set_timing(False)
+    k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_EVAL)
+    r_ms, r_n = ctx.kernel_time(_lib.PAS_K_TAS_RANGES)
+    sum_len = int(len_t.sum().item())
+    # algorithmic bytes per launch: columns + presence + pass bitmaps +
+    # ordered lists + lengths; rule tables included
+    w = pas_amd.w64(N)
+    alg_bytes = 8 * M * N + 8 * M * w + 8 * P * w + 4 * sum_len + 4 * P + 16 * (n_rules + P)
+    kernel_s = (k_ms / max(k_n, 1)) / 1e3
+    achieved = alg_bytes / kernel_s / 1e9
+    evals = P * N * world
+    value = evals * args.steps / elapsed
+    traffic = load_traffic("tas_eval_kernel")
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "pod-node evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic (seeded cluster snapshot + pod batch, SURVEY.md §8(d) distributions)",
+        "config": {
+            "workload": "tas_filter_prioritize (BASELINE configs[1])",
+            "pods_per_gpu": P, "nodes": N, "metrics": M, "rules_per_pod": R + 1,
+            "parallelism": f"pod-sharded x{world} (independent batches, replicated snapshot)",
+            "prioritize_entries_per_step": sum_len * world,
+            "snapshot_build_ms": snapshot_ms,
+            "ranges_kernel_ms": r_ms / max(r_n, 1),
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "tas_eval_kernel",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes": alg_bytes,
+            "kernel_ms": kernel_s * 1e3,
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline_tas(snap, batch, args.cpu_seconds)
+    ctx.close()
+    return out
+
+
+def cpu_baseline_tas(snap, batch, budget_s):
+    """The C restatement of the reference (oracle/, 1 thread) on a bounded pod sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+    N = snap.v_milli.shape[1]
+
+    def run(pods):
+        off = batch.rule_off[: pods + 1]
+        t0 = time.perf_counter()
+        oracle.tas_eval(snap.v_milli, snap.present, batch.rules[: off[-1]], off,
+                        batch.prio[:pods], None, 3)
+        return time.perf_counter() - t0
+
+    one = run(1)
+    pods = int(max(1, min(len(batch.prio), budget_s / max(one, 1e-6))))
+    t = run(pods)
+    return {"value": pods * N / t, "unit": "pod-node evals/s", "cores": 1, "kind": "port",
+            "sample": f"{pods} pods x {N} nodes x 16 rules (first pods of the rank-0 batch), "
+                      f"{t:.1f} s, oracle/pas_oracle.c single thread"}
+
+
+# ------------------------------------------------------------------------------- GAS
+
+def bench_gas(args, world, rank):
+    P, N = args.pods, args.nodes
+    ctx = pas_amd.Context(torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+    snap = wl.make_gas_snapshot(N, seed=0xC3)
+    batch = wl.make_gas_batch(P, seed=0xC3 + 7919 * rank)
+    K, Q = snap.used.shape[1], snap.used.shape[2]
+    C = batch.req.shape[1]
+    ctx.gas_snapshot_set_device(1, N, K, Q, dev(snap.n_cards), dev(snap.cap), dev(snap.used),
+                                stream)
+    req_t, mask_t = dev(batch.req), dev(batch.req_mask.view(np.int32))
+    nc_t = dev(batch.n_containers)
+    res_t = torch.empty((P, N), dtype=torch.int32, device="cuda")
+
+    def step():
+        ctx.gas_fit_device(1, P, C, wl.I915, req_t, mask_t, nc_t, res_t, stream)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    elapsed = timed_steps(step, args.steps, 0, world)
+    ctx.set_timing(False)
+    k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
+    alg_bytes = N * (8 * Q + 8 * K * Q + 4) + P * (8 * C * Q + 4 * C + 4) + 4 * P * N
+    kernel_s = (k_ms / max(k_n, 1)) / 1e3
+    achieved = alg_bytes / kernel_s / 1e9
+    out = {
+        "metric": "GAS per-card fit evals/sec (pod-node fits), 10k pods×50k nodes×8 cards",
+        "value": P * N * world * args.steps / elapsed, "unit": "pod-node fits/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C3)",
+        "config": {"workload": "gas_fit (BASELINE configs[2])", "pods_per_gpu": P, "nodes": N,
+                   "cards": K, "resources": Q,
+                   "fit_fraction": float((res_t.cpu().numpy().view(np.uint32) >> 31).mean())},
+        "roofline": {"bound": "hbm", "kernel": "gas_fit_kernel", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic("gas_fit_kernel"), "algorithmic_bytes": alg_bytes,
+                     "kernel_ms": kernel_s * 1e3},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle
+        t0 = time.perf_counter()
+        oracle.gas_fit(snap.n_cards, snap.cap, snap.used, batch.req[:1], batch.req_mask[:1],
+                       batch.n_containers[:1], wl.I915)
+        one = time.perf_counter() - t0
+        pods = int(max(1, min(P, args.cpu_seconds / max(one, 1e-6))))
+        t0 = time.perf_counter()
+        oracle.gas_fit(snap.n_cards, snap.cap, snap.used, batch.req[:pods],
+                       batch.req_mask[:pods], batch.n_containers[:pods], wl.I915)
+        t = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": pods * N / t, "unit": "pod-node fits/s", "cores": 1,
+                               "kind": "port", "sample": f"{pods} pods x {N} nodes, {t:.1f} s"}
+    ctx.close()
+    return out
+
+
+# ------------------------------------------------------------------------ deschedule
+
+def bench_deschedule(args, world, rank):
+    N, M, S = args.nodes, args.metrics, 16
+    ctx = pas_amd.Context(torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+    snap = wl.make_tas_snapshot(N, M, seed=0xC4 + rank)
+    rules, off = wl.make_deschedule_rules(snap, S, 4, seed=0xC4)
+    ctx.tas_snapshot_set_device(1, N, M, dev(snap.v_milli), dev(snap.present.view(np.int64)),
+                                stream)
+    rules_t, off_t = dev(rules.view(np.uint8)), dev(off)
+    viol_t = torch.empty((S, pas_amd.w64(N)), dtype=torch.int64, device="cuda")
+
+    def step():
+        ctx.tas_violations_device(1, S, len(rules), rules_t, off_t, viol_t, stream)
+
+    for _ in range(args.warmup):
+        step()
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    elapsed = timed_steps(step, args.steps, 0, world)
+    ctx.set_timing(False)
+    k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_VIOLATIONS)
+    w = pas_amd.w64(N)
+    alg_bytes = 8 * M * N + 8 * M * w + 8 * S * w
+    kernel_s = (k_ms / max(k_n, 1)) / 1e3
+    achieved = alg_bytes / kernel_s / 1e9
+    out = {
+        "metric": "TAS deschedule sweep node-rule evals/sec, 1M nodes×64 rules per GPU",
+        "value": N * len(rules) * world * args.steps / elapsed, "unit": "node-rule evals/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C4)",
+        "config": {"workload": "tas_deschedule_sweep (BASELINE configs[3], node-sharded)",
+                   "nodes_per_gpu": N, "metrics": M, "strategies": S, "rules": len(rules)},
+        "roofline": {"bound": "hbm", "kernel": "tas_violations_kernel", "achieved": achieved,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": load_traffic("tas_violations_kernel"),
+                     "algorithmic_bytes": alg_bytes, "kernel_ms": kernel_s * 1e3},
+    }
+    ctx.close()
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["tas", "gas", "deschedule"], default="tas")
+    ap.add_argument("--pods", type=int, default=None)
+    ap.add_argument("--nodes", type=int, default=None)
+    ap.add_argument("--metrics", type=int, default=64)
+    ap.add_argument("--rules", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    defaults = {"tas": (4096, 100_000), "gas": (10_000, 50_000), "deschedule": (0, 1_000_000)}
+    dp, dn = defaults[args.workload]
+    args.pods = args.pods or dp
+    args.nodes = args.nodes or dn
+    world, rank, _ = dist_setup(args.gpus)
+    fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule}[args.workload]
+    out = fn(args, world, rank)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

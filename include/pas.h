@@ -1,0 +1,240 @@
+/*
+ * pas.h — C-ABI of the MI355X-native Platform Aware Scheduling evaluator.
+ *
+ * This is the drop-in boundary beneath the reference's extender.Scheduler
+ * HTTP verbs (extender/types.go:11-15; registered at extender/scheduler.go:86-91).
+ * The Go handlers keep decoding extender.Args and encoding FilterResult /
+ * HostPriorityList; the compute they do per request is replaced by the batched
+ * entry points below (cgo binding shown in INTEGRATION.md).
+ *
+ * Conventions
+ *   - Plain C types only; no exceptions or aborts cross this boundary.
+ *   - Every function returns a pas_status (0 = OK, negative = error) and leaves a
+ *     message retrievable with pas_last_error(ctx).
+ *   - Host-pointer entry points copy their inputs in and results out and return
+ *     when the results are in host memory.  *_device entry points take device
+ *     pointers and a hipStream_t (as void*) and return once the work is enqueued.
+ *   - A pas_ctx is NOT thread safe: callers serialise calls per context (the GAS
+ *     extender already holds GASExtender.rwmutex around filter/bind,
+ *     gpu-aware-scheduling/pkg/gpuscheduler/scheduler.go:463-465).
+ *   - Bitmaps are little-endian uint64 words, node n at bit (n & 63) of word n >> 6;
+ *     W64(n) = (n + 63) / 64 words per row, bits >= n_nodes are zero.
+ *   - Metric values are int64 "milli" units: value * 1000 of the reference's
+ *     resource.Quantity (telemetry-aware-scheduling/pkg/metrics/client.go:25-29).
+ *     pas_quantity_to_milli() converts a Quantity string and reports
+ *     non-milli-exact values (PAS_ENOTEXACT) — those must not reach the device.
+ */
+#ifndef PAS_H_
+#define PAS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PAS_ABI_VERSION 1
+
+typedef enum pas_status {
+  PAS_OK = 0,
+  PAS_EINVAL = -1,     /* bad argument (shape, operator, null pointer) */
+  PAS_ESTALE = -2,     /* generation mismatch between call and resident snapshot */
+  PAS_ENOTEXACT = -3,  /* a value is not representable as exact int64 milli */
+  PAS_EDEVICE = -4,    /* HIP runtime error */
+  PAS_ENOMEM = -5,     /* device or host allocation failed */
+  PAS_ENOSNAP = -6,    /* no snapshot uploaded yet */
+  PAS_ECAPACITY = -7   /* shape exceeds a documented kernel limit */
+} pas_status;
+
+/* TASPolicyRule.Operator (telemetrypolicy/api/v1alpha1/types.go:31-35), evaluated as
+ * in core.EvaluateRule (strategies/core/operator.go:13-26).  Any other string panics
+ * in the reference (operator.go:25: nil map entry); here it is PAS_EINVAL. */
+typedef enum pas_op {
+  PAS_OP_LESS_THAN = 0,
+  PAS_OP_GREATER_THAN = 1,
+  PAS_OP_EQUALS = 2
+} pas_op;
+
+/* One TASPolicyRule with the metric name resolved to a snapshot column.
+ * metric < 0 or >= n_metrics means "metric not in the cache": the rule is skipped,
+ * as dontschedule.Violated does on a ReadMetric error (dontschedule/strategy.go:28-32). */
+typedef struct pas_rule {
+  int32_t metric;
+  int32_t op;      /* pas_op */
+  int64_t target;  /* TASPolicyRule.Target, integer units (NOT milli) */
+} pas_rule;
+
+typedef struct pas_config {
+  int32_t device;    /* HIP device ordinal; -1 = current device */
+  int32_t reserved;  /* must be 0 */
+} pas_config;
+
+typedef struct pas_ctx pas_ctx;
+
+int pas_abi_version(void);
+
+/* Context: owns one HIP stream (replaceable with pas_set_stream), the resident
+ * snapshots and scratch. */
+int pas_create(const pas_config* cfg, pas_ctx** out);
+void pas_destroy(pas_ctx* ctx);
+const char* pas_last_error(const pas_ctx* ctx);
+int pas_set_stream(pas_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+int pas_synchronize(pas_ctx* ctx);
+
+/* Operator string -> pas_op ("LessThan", "GreaterThan", "Equals"), else PAS_EINVAL.
+ * Replaces the map lookup in core.EvaluateRule (operator.go:14-25). */
+int pas_parse_operator(const char* op);
+
+/* resource.Quantity string (k8s.io/apimachinery v0.22.2 grammar: sign, digits,
+ * optional fraction, optional suffix n u m k M G T P E Ki Mi Gi Ti Pi Ei or
+ * e/E exponent) -> exact int64 value*1000.  PAS_ENOTEXACT if the value has
+ * sub-milli precision or is outside int64 milli range; PAS_EINVAL if unparsable. */
+int pas_quantity_to_milli(const char* quantity, int64_t* milli_out);
+
+/* resource.Quantity.AsInt64 as the reference uses it, ignoring `ok`
+ * (gpuscheduler/utils.go:23, scheduler.go:155): the integer value, or 0 when the
+ * quantity is non-integral or out of int64 range.  PAS_EINVAL if unparsable. */
+int pas_quantity_as_int64(const char* quantity, int64_t* out);
+
+/* ------------------------------------------------------------------------- */
+/* Telemetry Aware Scheduling                                                */
+/* ------------------------------------------------------------------------- */
+
+/* Upload a node-metric snapshot: the content of AutoUpdatingCache's
+ * "metrics/<name>" entries (cache/autoupdating.go:76-85) as SoA columns.
+ *   v_milli [n_metrics][n_nodes]      value * 1000 (ignored where not present)
+ *   present [n_metrics][W64(n_nodes)] node has this metric (NodeMetricsInfo key set)
+ * The device builds per-metric sorted orders once here, so that per-request
+ * evaluation never sorts (core.OrderedList, operator.go:30-42, sorts per request).
+ * gen is an opaque generation id checked by the eval calls (PAS_ESTALE). */
+int pas_tas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t n_metrics,
+                         const int64_t* v_milli, const uint64_t* present);
+int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t n_metrics,
+                                const int64_t* d_v_milli, const uint64_t* d_present,
+                                void* hip_stream);
+int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
+                          int32_t* n_metrics);
+
+#define PAS_TAS_FILTER 1u      /* produce pass_out (MetricsExtender.filterNodes) */
+#define PAS_TAS_PRIORITIZE 2u  /* produce order_out/order_len (prioritizeNodesForRule) */
+
+/* Batched TAS filter + prioritize for n_pods pending pods against the resident
+ * snapshot.  Replaces, per pod:
+ *   filter:     dontschedule.Strategy.Violated (dontschedule/strategy.go:25-44) and the
+ *               candidate loop of MetricsExtender.filterNodes (telemetryscheduler.go:204-211)
+ *   prioritize: prioritizeNodesForRule (telemetryscheduler.go:128-149) with
+ *               core.OrderedList (operator.go:30-42).
+ * Inputs
+ *   rules, rule_off  CSR of each pod's dontschedule rules: pod p owns
+ *                    rules[rule_off[p] .. rule_off[p+1])
+ *   prio             [n_pods] scheduleonmetric Rules[0] (getSchedulingRule,
+ *                    telemetryscheduler.go:115-124); metric < 0 = no rule / missing metric
+ *   cand             [n_pods][W64] candidate bitmaps (args.Nodes), or NULL = every node
+ * Outputs
+ *   pass_out   [n_pods][W64]  cand AND NOT violated            (flag PAS_TAS_FILTER)
+ *   order_out  [n_pods][n_nodes], order_len [n_pods]           (flag PAS_TAS_PRIORITIZE)
+ *              node indices of prioritize candidates that have the metric, best first;
+ *              HostPriority.Score of entry i is 10 - i (telemetryscheduler.go:145).
+ *              Candidates are pass_out when PAS_TAS_FILTER is also set (kube-scheduler
+ *              prioritizes the filter-feasible nodes), else cand.
+ * Order (the reference's is Go-map order + unstable sort.Slice, i.e. unspecified for
+ * ties and for operators other than LessThan/GreaterThan): GreaterThan = value
+ * descending, LessThan = value ascending, ties by ascending node index; any other
+ * operator = ascending node index.  The oracle uses the same rule. */
+int pas_tas_eval(pas_ctx* ctx, uint64_t gen, int32_t n_pods, const pas_rule* rules,
+                 const int32_t* rule_off, const pas_rule* prio, const uint64_t* cand,
+                 uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len);
+int pas_tas_eval_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_rules,
+                        const pas_rule* d_rules, const int32_t* d_rule_off,
+                        const pas_rule* d_prio, const uint64_t* d_cand, uint32_t flags,
+                        uint64_t* d_pass_out, int32_t* d_order_out, int32_t* d_order_len,
+                        void* hip_stream);
+
+/* Deschedule sweep: for each registered deschedule strategy s (rules
+ * rules[rule_off[s] .. rule_off[s+1])), the node set of deschedule.Strategy.Violated
+ * (deschedule/strategy.go:31-50), as the bitmap viol_out[s][W64].  The per-node
+ * policy lists of nodeStatusForStrategy (deschedule/enforce.go:154-164) are the
+ * columns of this matrix. */
+int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const pas_rule* rules,
+                       const int32_t* rule_off, uint64_t* viol_out);
+int pas_tas_violations_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
+                              int32_t n_rules, const pas_rule* d_rules,
+                              const int32_t* d_rule_off, uint64_t* d_viol_out,
+                              void* hip_stream);
+
+/* ------------------------------------------------------------------------- */
+/* GPU Aware Scheduling                                                      */
+/* ------------------------------------------------------------------------- */
+
+#define PAS_GAS_MAX_CARDS 8      /* cards per node held in registers */
+#define PAS_GAS_MAX_RES 4        /* gpu.intel.com/ resource kinds per batch */
+#define PAS_GAS_MAX_SELECTIONS 8 /* sum over containers of i915 count per pod */
+
+/* Frozen allocation snapshot (Cache.getNodeResourceStatus,
+ * gpuscheduler/node_resource_cache.go:474-491) in node-major SoA:
+ *   n_cards     [n_nodes]  unique card names of label gpu.intel.com/cards; 0 = label
+ *                          missing (getNodeGPUList -> nil, scheduler.go:132-148,
+ *                          errWontFit at :294-298); -1 = node not in the lister
+ *                          (FetchNode error, :282-288)
+ *   cap_per_gpu [n_nodes][n_res]        AsInt64(allocatable) / len(label split),
+ *                                       truncating (getPerGPUResourceCapacity :164-178);
+ *                                       0 where the node lacks the resource
+ *   used        [n_nodes][max_cards][n_res] usage of the node's cards in lexicographic
+ *                                       (sort.Strings, :216-224) order of card name;
+ *                                       cards in the usage map but not in the label are
+ *                                       left out (skipped at :230-234)
+ * max_cards <= PAS_GAS_MAX_CARDS, n_res <= PAS_GAS_MAX_RES. */
+int pas_gas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
+                         int32_t n_res, const int32_t* n_cards, const int64_t* cap_per_gpu,
+                         const int64_t* used);
+int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
+                                int32_t n_res, const int32_t* d_n_cards,
+                                const int64_t* d_cap_per_gpu, const int64_t* d_used,
+                                void* hip_stream);
+
+/* GAS filter for a batch of pods over every node of the snapshot: one
+ * runSchedulingLogic (scheduler.go:280-338) per (pod, node), first-fit over cards
+ * with checkResourceCapacity (:341-383).
+ *   req       [n_pods][max_containers][n_res] AsInt64 container requests
+ *             (containerRequests, utils.go:14-32); res_index i915 identifies
+ *             gpu.intel.com/i915 among the n_res kinds (or -1 if absent)
+ *   req_mask  [n_pods][max_containers] bit q set = container requests kind q
+ *             (the key exists in its resourceMap, even with value 0)
+ *   n_containers [n_pods]
+ * Output res_out[n_pods][n_nodes], one word per (pod, node):
+ *   bit 31     the pod fits (node passes GASExtender.filterNodes, :467-473)
+ *   bits 24-27 number of card selections S (= sum of per-container i915 counts)
+ *   bits 0-23  S 3-bit card ranks (lexicographic index into the node's cards),
+ *              selection j at bits 3j..3j+2, containers in order, i.e. the
+ *              "gas-container-cards" annotation (:317-335) in packed form.
+ * PAS_ECAPACITY if a pod needs more than PAS_GAS_MAX_SELECTIONS selections. */
+int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                const int32_t* n_containers, uint32_t* res_out);
+int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                       int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
+                       const int32_t* d_n_containers, uint32_t* d_res_out, void* hip_stream);
+
+/* ------------------------------------------------------------------------- */
+/* Instrumentation                                                           */
+/* ------------------------------------------------------------------------- */
+
+/* Kernel timing with HIP events on the stream each kernel is launched on.
+ * Kernel ids: */
+#define PAS_K_TAS_RANGES 0
+#define PAS_K_TAS_EVAL 1
+#define PAS_K_TAS_VIOLATIONS 2
+#define PAS_K_GAS_PREP 3
+#define PAS_K_GAS_FIT 4
+#define PAS_K_COUNT 5
+int pas_set_timing(pas_ctx* ctx, int enable);
+/* Sum of elapsed ms and number of launches recorded for a kernel since the last reset. */
+int pas_kernel_time(pas_ctx* ctx, int32_t kernel_id, double* total_ms, int64_t* launches);
+int pas_reset_timing(pas_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PAS_H_ */

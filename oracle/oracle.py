@@ -1,0 +1,145 @@
+"""ctypes wrapper of oracle/build/liboracle.so — the CPU restatement of the reference.
+
+TEST INFRASTRUCTURE ONLY.  Used by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg as the checker / baseline; never by the product package.
+Parity status: pinned against the reference's own test vectors and e2e fixtures
+(tests/golden/); the Go reference cannot be built in this image.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import POINTER, c_int, c_int32, c_int64, c_uint32, c_void_p
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+RULE_DTYPE = np.dtype([("metric", "<i4"), ("op", "<i4"), ("target", "<i8")], align=True)
+RM_MAX_KEYS = 8
+
+
+class OrRm(ctypes.Structure):
+    _fields_ = [("has", ctypes.c_uint8 * RM_MAX_KEYS), ("val", c_int64 * RM_MAX_KEYS)]
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        build()
+    lib = ctypes.CDLL(LIB_PATH)
+    P = c_void_p
+    sigs = {
+        "or_evaluate_rule": (c_int, [c_int64, c_int32, c_int64]),
+        "or_violated": (c_int, [c_int32, c_int32, P, P, P, c_int32, P]),
+        "or_ordered_list": (c_int32, [c_int32, c_int32, P, P, P, P, P]),
+        "or_tas_eval": (c_int, [c_int32, c_int32, P, P, c_int32, P, P, P, P, c_uint32, P, P, P]),
+        "or_tas_violations": (c_int, [c_int32, c_int32, P, P, c_int32, P, P, P]),
+        "or_rm_add": (c_int, [POINTER(OrRm), c_int32, c_int64]),
+        "or_rm_subtract": (c_int, [POINTER(OrRm), c_int32, c_int64]),
+        "or_rm_add_rm": (c_int, [POINTER(OrRm), POINTER(OrRm)]),
+        "or_rm_subtract_rm": (c_int, [POINTER(OrRm), POINTER(OrRm)]),
+        "or_rm_divide": (c_int, [POINTER(OrRm), c_int32]),
+        "or_check_resource_capacity": (c_int, [POINTER(OrRm), POINTER(OrRm), POINTER(OrRm)]),
+        "or_gas_fit": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
+                               P, P, P, P]),
+    }
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _p(a):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(c_void_p)
+
+
+def w64(n):
+    return (n + 63) // 64
+
+
+def evaluate_rule(v_milli: int, op: int, target: int) -> int:
+    return load().or_evaluate_rule(v_milli, op, target)
+
+
+def tas_eval(v_milli, present, rules, rule_off, prio, cand=None, flags=3):
+    v = np.ascontiguousarray(v_milli, np.int64)
+    m, n = v.shape
+    p = np.ascontiguousarray(present, np.uint64)
+    rules = np.ascontiguousarray(rules, RULE_DTYPE)
+    rule_off = np.ascontiguousarray(rule_off, np.int32)
+    prio = np.ascontiguousarray(prio, RULE_DTYPE)
+    n_pods = rule_off.shape[0] - 1
+    if cand is not None:
+        cand = np.ascontiguousarray(cand, np.uint64)
+    pass_out = np.zeros((n_pods, w64(n)), np.uint64) if flags & 1 else None
+    order = np.zeros((n_pods, max(n, 1)), np.int32) if flags & 2 else None
+    lens = np.zeros(n_pods, np.int32) if flags & 2 else None
+    rc = load().or_tas_eval(n, m, _p(v), _p(p), n_pods, _p(rules) if rules.size else None,
+                            _p(rule_off), _p(prio), _p(cand), flags, _p(pass_out), _p(order),
+                            _p(lens))
+    if rc != 0:
+        raise ValueError("oracle: invalid operator (the reference panics)")
+    return pass_out, order, lens
+
+
+def tas_violations(v_milli, present, rules, rule_off):
+    v = np.ascontiguousarray(v_milli, np.int64)
+    m, n = v.shape
+    p = np.ascontiguousarray(present, np.uint64)
+    rules = np.ascontiguousarray(rules, RULE_DTYPE)
+    rule_off = np.ascontiguousarray(rule_off, np.int32)
+    s = rule_off.shape[0] - 1
+    out = np.zeros((s, w64(n)), np.uint64)
+    rc = load().or_tas_violations(n, m, _p(v), _p(p), s, _p(rules) if rules.size else None,
+                                  _p(rule_off), _p(out))
+    if rc != 0:
+        raise ValueError("oracle: invalid operator (the reference panics)")
+    return out
+
+
+def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index):
+    n_cards = np.ascontiguousarray(n_cards, np.int32)
+    cap = np.ascontiguousarray(cap, np.int64)
+    used = np.ascontiguousarray(used, np.int64)
+    req = np.ascontiguousarray(req, np.int64)
+    req_mask = np.ascontiguousarray(req_mask, np.uint32)
+    n_containers = np.ascontiguousarray(n_containers, np.int32)
+    n, k, q = used.shape
+    p, c, _ = req.shape
+    out = np.zeros((p, n), np.uint32)
+    rc = load().or_gas_fit(n, k, q, _p(n_cards), _p(cap), _p(used), p, c, i915_index, _p(req),
+                           _p(req_mask), _p(n_containers), _p(out))
+    if rc != 0:
+        raise ValueError(f"oracle gas_fit failed: {rc}")
+    return out
+
+
+def rm(d: dict, keys: list) -> OrRm:
+    """Build an or_rm from {name: value} with key ids from `keys`."""
+    r = OrRm()
+    for name, v in d.items():
+        i = keys.index(name)
+        r.has[i] = 1
+        r.val[i] = v
+    return r
+
+
+def rm_dict(r: OrRm, keys: list) -> dict:
+    return {keys[i]: r.val[i] for i in range(len(keys)) if r.has[i]}

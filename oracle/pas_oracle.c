@@ -1,0 +1,342 @@
+/*
+ * pas_oracle.c — CPU restatement of the reference semantics (see pas_oracle.h).
+ * TEST INFRASTRUCTURE ONLY; never linked into the product library.
+ *
+ * Reference root: tejasshahintel/platform-aware-scheduling @ 2025-02-20.
+ *   TAS: telemetry-aware-scheduling/pkg/{strategies,telemetryscheduler}
+ *   GAS: gpu-aware-scheduling/pkg/gpuscheduler
+ */
+#include "pas_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+static inline int has_bit(const uint64_t* bits, int64_t i) {
+  return (int)((bits[i >> 6] >> (i & 63)) & 1u);
+}
+
+static inline int64_t w64(int32_t n) { return ((int64_t)n + 63) / 64; }
+
+/* Metric column m "exists in the cache" when it has at least one node: the cache never
+ * stores an empty NodeMetricsInfo (nilPayloadCheck, cache/autoupdating.go:138-145), so
+ * ReadMetric errors exactly when the column is empty (autoupdating.go:76-85). */
+static int metric_in_cache(int32_t n_nodes, int32_t n_metrics, const uint64_t* present,
+                           int32_t m) {
+  if (m < 0 || m >= n_metrics) return 0;
+  const uint64_t* row = present + (int64_t)m * w64(n_nodes);
+  for (int64_t w = 0; w < w64(n_nodes); ++w)
+    if (row[w]) return 1;
+  return 0;
+}
+
+/* operator.go:13-26.  The reference compares the exact decimal Quantity with the int64
+ * target; here value = v_milli / 1000 exactly, so the comparison is v_milli against
+ * target * 1000 in 128-bit arithmetic (no saturation needed). */
+int or_evaluate_rule(int64_t v_milli, int32_t op, int64_t target) {
+  const __int128 v = (__int128)v_milli;
+  const __int128 t = (__int128)target * 1000;
+  const int cmp = v < t ? -1 : (v > t ? 1 : 0); /* Quantity.CmpInt64 */
+  switch (op) {
+    case 0: return cmp == -1; /* "LessThan"    operator.go:15-17 */
+    case 1: return cmp == 1;  /* "GreaterThan" operator.go:18-20 */
+    case 2: return cmp == 0;  /* "Equals"      operator.go:21-23 */
+    default: return -1;       /* nil map entry -> panic at operator.go:25 */
+  }
+}
+
+/* dontschedule/strategy.go:25-44 (deschedule/strategy.go:31-50 is the same loop). */
+int or_violated(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                const uint64_t* present, const or_rule* rules, int32_t n_rules,
+                uint8_t* violating) {
+  memset(violating, 0, (size_t)n_nodes);
+  for (int32_t r = 0; r < n_rules; ++r) {            /* for _, rule := range d.Rules */
+    const or_rule* rule = &rules[r];
+    if (rule->op < 0 || rule->op > 2) return -1;
+    if (!metric_in_cache(n_nodes, n_metrics, present, rule->metric))
+      continue;                                      /* ReadMetric err -> continue :28-32 */
+    const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
+    const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
+    for (int32_t n = 0; n < n_nodes; ++n) {          /* for nodeName, nodeMetric := range */
+      if (!has_bit(pres, n)) continue;
+      if (or_evaluate_rule(col[n], rule->op, rule->target))
+        violating[n] = 1;                            /* violatingNodes[nodeName] = nil */
+    }
+  }
+  return 0;
+}
+
+/* ---- OrderedList ---------------------------------------------------------- */
+
+typedef struct sortable {
+  int32_t node;
+  int64_t value;
+} sortable;
+
+/* Stable merge sort; `desc` selects the GreaterThan comparator (operator.go:37),
+ * otherwise LessThan (operator.go:39).  Stability over input in node-index order is
+ * the documented tie-break. */
+static void merge_sort(sortable* a, sortable* tmp, int32_t n, int desc) {
+  if (n < 2) return;
+  if (n <= 16) { /* insertion sort, stable */
+    for (int32_t i = 1; i < n; ++i) {
+      sortable x = a[i];
+      int32_t j = i - 1;
+      while (j >= 0 && (desc ? (x.value > a[j].value) : (x.value < a[j].value))) {
+        a[j + 1] = a[j];
+        --j;
+      }
+      a[j + 1] = x;
+    }
+    return;
+  }
+  const int32_t h = n / 2;
+  merge_sort(a, tmp, h, desc);
+  merge_sort(a + h, tmp, n - h, desc);
+  int32_t i = 0, j = h, k = 0;
+  while (i < h && j < n) {
+    const int take_right = desc ? (a[j].value > a[i].value) : (a[j].value < a[i].value);
+    tmp[k++] = take_right ? a[j++] : a[i++];
+  }
+  while (i < h) tmp[k++] = a[i++];
+  while (j < n) tmp[k++] = a[j++];
+  memcpy(a, tmp, (size_t)n * sizeof(sortable));
+}
+
+int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                        const uint64_t* present, const or_rule* rule, const uint8_t* cand,
+                        int32_t* out) {
+  /* getSchedulingRule (telemetryscheduler.go:115-124) already rejected rules without a
+   * metric name; a metric missing from the cache makes prioritizeNodesForRule fail
+   * (:130-133) and prioritizeNodes answer with an empty list (:92-96). */
+  if (!metric_in_cache(n_nodes, n_metrics, present, rule->metric)) return 0;
+  const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
+  const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
+  sortable* items = (sortable*)malloc(sizeof(sortable) * (size_t)(n_nodes > 0 ? n_nodes : 1));
+  sortable* tmp = (sortable*)malloc(sizeof(sortable) * (size_t)(n_nodes > 0 ? n_nodes : 1));
+  int32_t cnt = 0;
+  /* filteredNodeData: candidates that have the metric (telemetryscheduler.go:135-139) */
+  for (int32_t n = 0; n < n_nodes; ++n) {
+    if (!cand[n] || !has_bit(pres, n)) continue;
+    items[cnt].node = n;
+    items[cnt].value = col[n];
+    ++cnt;
+  }
+  if (rule->op == 1) merge_sort(items, tmp, cnt, 1);       /* "GreaterThan" :36-37 */
+  else if (rule->op == 0) merge_sort(items, tmp, cnt, 0);  /* "LessThan"    :38-39 */
+  /* any other operator: no sort (switch without default, :35-40) */
+  for (int32_t i = 0; i < cnt; ++i) out[i] = items[i].node; /* Score: 10 - i, :145 */
+  free(items);
+  free(tmp);
+  return cnt;
+}
+
+int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                const uint64_t* present, int32_t n_pods, const or_rule* rules,
+                const int32_t* rule_off, const or_rule* prio, const uint64_t* cand,
+                uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len) {
+  const int64_t W = w64(n_nodes);
+  uint8_t* viol = (uint8_t*)malloc((size_t)(n_nodes > 0 ? n_nodes : 1));
+  uint8_t* cset = (uint8_t*)malloc((size_t)(n_nodes > 0 ? n_nodes : 1));
+  int rc = 0;
+  for (int32_t p = 0; p < n_pods && rc == 0; ++p) {
+    /* candidate set (args.Nodes.Items) */
+    for (int32_t n = 0; n < n_nodes; ++n)
+      cset[n] = cand ? (uint8_t)has_bit(cand + (int64_t)p * W, n) : 1;
+    if (flags & 1u) {
+      /* filterNodes: violatingNodes := dontscheduleStrategy.Violated(m.cache) (:199) */
+      if (or_violated(n_nodes, n_metrics, v_milli, present, rules + rule_off[p],
+                      rule_off[p + 1] - rule_off[p], viol) != 0) {
+        rc = -1;
+        break;
+      }
+      uint64_t* row = pass_out + (int64_t)p * W;
+      memset(row, 0, (size_t)W * sizeof(uint64_t));
+      for (int32_t n = 0; n < n_nodes; ++n) { /* for _, node := range args.Nodes.Items */
+        if (!cset[n]) continue;
+        if (viol[n]) {
+          cset[n] = 0;                        /* failedNodes[node.Name] = "Node violates" */
+        } else {
+          row[n >> 6] |= 1ull << (n & 63);    /* filteredNodes = append(...) */
+        }
+      }
+    }
+    if (flags & 2u) {
+      /* prioritize over the filter-feasible set (kube-scheduler passes only those) */
+      const or_rule* r = &prio[p];
+      int32_t len = 0;
+      if (r->metric >= 0) {
+        /* an unknown operator is not an error here: OrderedList's switch has no default
+         * (operator.go:35-40), the list is just left unsorted */
+        len = or_ordered_list(n_nodes, n_metrics, v_milli, present, r, cset,
+                              order_out + (int64_t)p * n_nodes);
+      }
+      order_len[p] = len;
+    }
+  }
+  free(viol);
+  free(cset);
+  return rc;
+}
+
+int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                      const uint64_t* present, int32_t n_strategies, const or_rule* rules,
+                      const int32_t* rule_off, uint64_t* viol_out) {
+  const int64_t W = w64(n_nodes);
+  uint8_t* viol = (uint8_t*)malloc((size_t)(n_nodes > 0 ? n_nodes : 1));
+  int rc = 0;
+  /* for strat := range enforcer.RegisteredStrategies[StrategyType] (enforce.go:156) */
+  for (int32_t s = 0; s < n_strategies; ++s) {
+    if (or_violated(n_nodes, n_metrics, v_milli, present, rules + rule_off[s],
+                    rule_off[s + 1] - rule_off[s], viol) != 0) {
+      rc = -1;
+      break;
+    }
+    uint64_t* row = viol_out + (int64_t)s * W;
+    memset(row, 0, (size_t)W * sizeof(uint64_t));
+    for (int32_t n = 0; n < n_nodes; ++n) /* violations[node] = append(..., policy) */
+      if (viol[n]) row[n >> 6] |= 1ull << (n & 63);
+  }
+  free(viol);
+  return rc;
+}
+
+/* ---- GAS resourceMap ------------------------------------------------------ */
+
+int or_rm_add(or_rm* rm, int32_t key, int64_t value) {
+  if (value < 0) return OR_RM_ERR_INPUT;               /* minAllowedInput, :78-82 */
+  if (rm->has[key]) {
+    value = (int64_t)((uint64_t)value + (uint64_t)rm->val[key]); /* Go wraps */
+    if (value < 0) return OR_RM_ERR_OVERFLOW;          /* :88-92 */
+  }
+  rm->has[key] = 1;
+  rm->val[key] = value;
+  return OR_RM_OK;
+}
+
+int or_rm_subtract(or_rm* rm, int32_t key, int64_t value) {
+  if (value < 0) return OR_RM_ERR_INPUT;               /* :104-108 */
+  if (!rm->has[key]) return OR_RM_ERR_INPUT;           /* non-existing key, :120-124 */
+  rm->val[key] = (int64_t)((uint64_t)rm->val[key] - (uint64_t)value);
+  if (rm->val[key] < 0) rm->val[key] = 0;              /* capped to zero, :114-119 */
+  return OR_RM_OK;
+}
+
+int or_rm_add_rm(or_rm* rm, const or_rm* src) {
+  or_rm copy = *rm;                                    /* mapCopy := rm.newCopy() */
+  for (int32_t k = 0; k < OR_RM_MAX_KEYS; ++k) {
+    if (!src->has[k]) continue;
+    const int err = or_rm_add(&copy, k, src->val[k]);
+    if (err) return err;                               /* nothing added on error */
+  }
+  *rm = copy;                                          /* rm.copyFrom(mapCopy) */
+  return OR_RM_OK;
+}
+
+int or_rm_subtract_rm(or_rm* rm, const or_rm* src) {
+  or_rm copy = *rm;
+  for (int32_t k = 0; k < OR_RM_MAX_KEYS; ++k) {
+    if (!src->has[k]) continue;
+    const int err = or_rm_subtract(&copy, k, src->val[k]);
+    if (err) return err;
+  }
+  *rm = copy;
+  return OR_RM_OK;
+}
+
+int or_rm_divide(or_rm* rm, int32_t divider) {
+  if (divider < 1) return OR_RM_ERR_INPUT;             /* :130-134 */
+  if (divider == 1) return OR_RM_OK;
+  for (int32_t k = 0; k < OR_RM_MAX_KEYS; ++k)
+    if (rm->has[k]) rm->val[k] = rm->val[k] / divider; /* truncating, :140-142 */
+  return OR_RM_OK;
+}
+
+int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const or_rm* used) {
+  for (int32_t k = 0; k < OR_RM_MAX_KEYS; ++k) {       /* for resName, resNeed := range */
+    if (!need->has[k]) continue;
+    const int64_t res_need = need->val[k];
+    if (res_need < 0) return 0;                                  /* :343-347 */
+    if (!capacity->has[k] || capacity->val[k] <= 0) return 0;    /* :349-354 */
+    const int64_t res_cap = capacity->val[k];
+    const int64_t res_used = used->has[k] ? used->val[k] : 0;    /* missing = 0, :356 */
+    if (res_used < 0) return 0;                                  /* :358-362 */
+    const int64_t sum = (int64_t)((uint64_t)res_used + (uint64_t)res_need);
+    if (sum < 0) return 0;                                       /* overflow, :367-371 */
+    if (res_cap < sum) return 0;                                 /* :373-377 */
+  }
+  return 1;
+}
+
+/* ---- GAS runSchedulingLogic over the packed snapshot ---------------------- */
+
+/* Builds the reference's maps from the packed layout: capacity has every resource kind
+ * with a positive per-GPU value... careful: a kind whose per-GPU capacity is 0 may
+ * still be a key of the capacity map, but checkResourceCapacity treats "missing" and
+ * "<= 0" identically (:349-354), so has = 1 with the stored value is equivalent. */
+int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+               const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
+               int32_t max_containers, int32_t i915_index, const int64_t* req,
+               const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out) {
+  if (max_cards > 8 || n_res > OR_RM_MAX_KEYS) return -1;
+  or_rm node_used[8];
+  for (int32_t p = 0; p < n_pods; ++p) {
+    for (int32_t n = 0; n < n_nodes; ++n) {
+      uint32_t word = 0;
+      int fits = 1;
+      int32_t nsel = 0;
+      /* iCache.FetchNode error (:282-288) / no cards label -> errWontFit (:290-298) */
+      if (n_cards[n] <= 0) fits = 0;
+      or_rm capacity;
+      memset(&capacity, 0, sizeof capacity);
+      if (fits) {
+        for (int32_t q = 0; q < n_res; ++q) {         /* getPerGPUResourceCapacity */
+          capacity.has[q] = 1;
+          capacity.val[q] = cap_per_gpu[(int64_t)n * n_res + q];
+        }
+        /* readNodeResources deep copy (node_resource_cache.go:474-491) +
+         * addEmptyResourceMaps (:269-275): a fresh copy per (pod, node) */
+        for (int32_t k = 0; k < n_cards[n]; ++k) {
+          memset(&node_used[k], 0, sizeof(or_rm));
+          for (int32_t q = 0; q < n_res; ++q) {
+            const int64_t u = used[((int64_t)n * max_cards + k) * n_res + q];
+            node_used[k].has[q] = 1;
+            node_used[k].val[q] = u;
+          }
+        }
+      }
+      for (int32_t c = 0; fits && c < n_containers[p]; ++c) {   /* for i, containerRequest */
+        const int64_t base = ((int64_t)p * max_containers + c);
+        const uint32_t mask = req_mask[base];
+        if (mask == 0) continue;                /* len(containerRequest) == 0 -> [] :206-208 */
+        or_rm per_gpu;                          /* getPerGPUResourceRequest :180-190 */
+        memset(&per_gpu, 0, sizeof per_gpu);
+        for (int32_t q = 0; q < n_res; ++q)
+          if (mask & (1u << q)) { per_gpu.has[q] = 1; per_gpu.val[q] = req[base * n_res + q]; }
+        int64_t num_i915 = 0;                   /* getNumI915 :192-198 */
+        if (i915_index >= 0 && per_gpu.has[i915_index] && per_gpu.val[i915_index] > 0)
+          num_i915 = per_gpu.val[i915_index];
+        if (num_i915 > 1) or_rm_divide(&per_gpu, (int32_t)num_i915);
+        for (int64_t g = 0; g < num_i915; ++g) {  /* for gpuNum := 0; gpuNum < numI915 */
+          int fitted = 0;
+          /* cards in sort.Strings order; stale cards are absent from the packed snapshot,
+           * which equals skipping them (!gpuMap[gpuName] -> continue, :230-234) */
+          for (int32_t k = 0; k < n_cards[n]; ++k) {
+            if (or_check_resource_capacity(&per_gpu, &capacity, &node_used[k])) {
+              if (or_rm_add_rm(&node_used[k], &per_gpu) == OR_RM_OK) {
+                fitted = 1;
+                if (nsel < 8) word |= (uint32_t)k << (3 * nsel);
+                ++nsel;                         /* cards = append(cards, gpuName) */
+              }
+              break;
+            }
+          }
+          if (!fitted) { fits = 0; break; }    /* errWontFit :249-253 */
+        }
+      }
+      if (nsel > 8) return -2;                  /* beyond the packed encoding */
+      res_out[(int64_t)p * n_nodes + n] =
+          fits ? (0x80000000u | ((uint32_t)nsel << 24) | word) : 0u;
+    }
+  }
+  return 0;
+}

@@ -1,0 +1,98 @@
+/*
+ * pas_oracle.h — CPU restatement of the reference's filter/prioritize/deschedule and
+ * GAS fit semantics.  TEST INFRASTRUCTURE ONLY: imported by tests/, by
+ * __graft_entry__.smoke() and by bench.py's cpu_baseline leg, and only as the
+ * checker.  The product (platform-aware-scheduling_amd/) never links or calls it.
+ *
+ * Parity is pinned by the reference's own table-driven test vectors and e2e
+ * fixtures, transcribed under tests/golden/ (SURVEY.md Appendix B, G1-G11); the
+ * reference itself (Go 1.16 + k8s.io/apimachinery v0.22.2) cannot be built here.
+ *
+ * Every function names the reference lines it restates.  It deliberately uses the
+ * reference's loop structure (rule -> node map -> EvaluateRule; sort per request;
+ * per (pod, node) sequential container/card loop) and exact 128-bit arithmetic, not
+ * the device's sorted-range / saturating formulation.
+ */
+#ifndef PAS_ORACLE_H_
+#define PAS_ORACLE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_rule {
+  int32_t metric;  /* column, or <0 = metric not in cache */
+  int32_t op;      /* 0 LessThan, 1 GreaterThan, 2 Equals, other = invalid */
+  int64_t target;  /* integer units */
+} or_rule;
+
+/* core.EvaluateRule (telemetry-aware-scheduling/pkg/strategies/core/operator.go:13-26):
+ * Quantity.CmpInt64(target) == -1 / 1 / 0, restated on an exact milli value.
+ * Returns 1/0, or -1 for an operator the reference would panic on (operator.go:25). */
+int or_evaluate_rule(int64_t v_milli, int32_t op, int64_t target);
+
+/* Strategy.Violated for dontschedule (dontschedule/strategy.go:25-44) and deschedule
+ * (deschedule/strategy.go:31-50) — identical loops.  violating[n] set to 1 for every
+ * node of the union.  Returns 0, or -1 on an invalid operator. */
+int or_violated(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                const uint64_t* present, const or_rule* rules, int32_t n_rules,
+                uint8_t* violating);
+
+/* prioritizeNodesForRule (telemetryscheduler/telemetryscheduler.go:128-149) with
+ * core.OrderedList (operator.go:30-42): candidates (cand[n] != 0) that have the metric,
+ * GreaterThan = descending, LessThan = ascending, other = unsorted; ties and the
+ * unsorted case follow the documented rule "ascending node index" (the reference's
+ * order there is Go-map order, i.e. unspecified).  Writes node indices best-first to
+ * out and returns the count. */
+int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                        const uint64_t* present, const or_rule* rule, const uint8_t* cand,
+                        int32_t* out);
+
+/* Batched equivalent of pas_tas_eval (include/pas.h): per pod, filterNodes
+ * (telemetryscheduler.go:184-225) and/or prioritizeNodesForRule.  Same argument
+ * layout as the C-ABI host entry point.  Returns 0 or -1 (invalid operator). */
+int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                const uint64_t* present, int32_t n_pods, const or_rule* rules,
+                const int32_t* rule_off, const or_rule* prio, const uint64_t* cand,
+                uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len);
+
+/* nodeStatusForStrategy (deschedule/enforce.go:154-164): per strategy, Violated as a
+ * bitmap viol_out[s][W64]. */
+int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                      const uint64_t* present, int32_t n_strategies, const or_rule* rules,
+                      const int32_t* rule_off, uint64_t* viol_out);
+
+/* ---- GAS ---------------------------------------------------------------- */
+
+/* A resourceMap (gpuscheduler/resource_map.go:20) restated over small integer key
+ * ids: has[k] says the key exists, val[k] its int64 amount. */
+#define OR_RM_MAX_KEYS 8
+typedef struct or_rm {
+  uint8_t has[OR_RM_MAX_KEYS];
+  int64_t val[OR_RM_MAX_KEYS];
+} or_rm;
+
+enum { OR_RM_OK = 0, OR_RM_ERR_INPUT = 1, OR_RM_ERR_OVERFLOW = 2 };
+
+int or_rm_add(or_rm* rm, int32_t key, int64_t value);         /* resource_map.go:77-98 */
+int or_rm_subtract(or_rm* rm, int32_t key, int64_t value);    /* resource_map.go:103-127 */
+int or_rm_add_rm(or_rm* rm, const or_rm* src);                /* resource_map.go:38-53 */
+int or_rm_subtract_rm(or_rm* rm, const or_rm* src);           /* resource_map.go:58-73 */
+int or_rm_divide(or_rm* rm, int32_t divider);                 /* resource_map.go:129-145 */
+/* checkResourceCapacity (gpuscheduler/scheduler.go:341-383). */
+int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const or_rm* used);
+
+/* GAS filter over every (pod, node) of a packed snapshot, one runSchedulingLogic
+ * (scheduler.go:280-338) each; same layouts and result encoding as pas_gas_fit. */
+int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+               const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
+               int32_t max_containers, int32_t i915_index, const int64_t* req,
+               const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PAS_ORACLE_H_ */

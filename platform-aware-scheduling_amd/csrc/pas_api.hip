@@ -1,0 +1,695 @@
+// pas_api.hip — the C-ABI surface (include/pas.h): context, errors, timing, quantity
+// parsing and the host-pointer wrappers around the device launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+
+#include "pas.h"
+#include "pas_internal.h"
+
+namespace pas {
+
+int set_error(pas_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+int check_hip(pas_ctx* ctx, hipError_t e, const char* what) {
+  std::string m = std::string(what) + ": " + hipGetErrorString(e);
+  return set_error(ctx, e == hipErrorOutOfMemory ? PAS_ENOMEM : PAS_EDEVICE, m);
+}
+
+int activate(pas_ctx* ctx) {
+  PAS_HIP(ctx, hipSetDevice(ctx->device));
+  return PAS_OK;
+}
+
+hipStream_t pick_stream(pas_ctx* ctx, void* s) {
+  return s ? reinterpret_cast<hipStream_t>(s) : ctx->stream;
+}
+
+int ensure_scratch(pas_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return PAS_OK;
+  if (ctx->scratch) {
+    PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PAS_HIP(ctx, hipFree(ctx->scratch));
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+  }
+  size_t want = std::max(bytes, size_t(1) << 20);
+  PAS_HIP(ctx, hipMalloc(&ctx->scratch, want));
+  ctx->scratch_bytes = want;
+  return PAS_OK;
+}
+
+static hipEvent_t take_event(pas_ctx* ctx) {
+  if (!ctx->event_pool.empty()) {
+    hipEvent_t e = ctx->event_pool.back();
+    ctx->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+void timing_begin(pas_ctx* ctx, hipStream_t s, int kernel, TimedLaunch* tl) {
+  tl->kernel = -1;
+  if (!ctx->timing) return;
+  tl->start = take_event(ctx);
+  tl->stop = take_event(ctx);
+  if (!tl->start || !tl->stop) return;
+  tl->kernel = kernel;
+  (void)hipEventRecord(tl->start, s);
+}
+
+void timing_end(pas_ctx* ctx, hipStream_t s, TimedLaunch* tl) {
+  if (tl->kernel < 0) return;
+  (void)hipEventRecord(tl->stop, s);
+  ctx->pending.push_back(*tl);
+}
+
+static void resolve_timing(pas_ctx* ctx) {
+  for (auto& tl : ctx->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(tl.stop) == hipSuccess &&
+        hipEventElapsedTime(&ms, tl.start, tl.stop) == hipSuccess) {
+      ctx->total_ms[tl.kernel] += ms;
+      ctx->launches[tl.kernel] += 1;
+    }
+    ctx->event_pool.push_back(tl.start);
+    ctx->event_pool.push_back(tl.stop);
+  }
+  ctx->pending.clear();
+}
+
+static void free_ptr(void*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+
+void free_tas(pas_ctx* ctx) {
+  TasSnapshot& t = ctx->tas;
+  free_ptr(reinterpret_cast<void*&>(t.vals));
+  free_ptr(reinterpret_cast<void*&>(t.present));
+  free_ptr(reinterpret_cast<void*&>(t.cnt));
+  free_ptr(reinterpret_cast<void*&>(t.sorted));
+  free_ptr(reinterpret_cast<void*&>(t.perm));
+  free_ptr(reinterpret_cast<void*&>(t.rank));
+  free_ptr(reinterpret_cast<void*&>(t.vals_c));
+  free_ptr(reinterpret_cast<void*&>(t.word_scan));
+  free_ptr(reinterpret_cast<void*&>(t.seg_begin));
+  free_ptr(reinterpret_cast<void*&>(t.seg_end));
+  free_ptr(t.sort_tmp);
+  free_ptr(t.scan_tmp);
+  t = TasSnapshot{};
+}
+
+void free_gas(pas_ctx* ctx) {
+  GasSnapshot& g = ctx->gas;
+  free_ptr(reinterpret_cast<void*&>(g.n_cards));
+  free_ptr(reinterpret_cast<void*&>(g.cap));
+  free_ptr(reinterpret_cast<void*&>(g.used));
+  g = GasSnapshot{};
+}
+
+// ---------------------------------------------------------------------------
+// resource.Quantity -> exact scaled integer
+// ---------------------------------------------------------------------------
+
+// Parses the k8s.io/apimachinery v0.22.2 quantity grammar
+// (<signedNumber><suffix>, suffix in {"" n u m k M G T P E Ki..Ei, e<int>, E<int>})
+// into mantissa * 10^exp10 * 2^exp2 and scales it by 10^extra10 exactly.
+// Returns PAS_OK with *out set, PAS_ENOTEXACT if non-integral after scaling or out of
+// int64 range, PAS_EINVAL if unparsable.
+static int quantity_scaled(const char* s, int extra10, int64_t* out) {
+  if (!s) return PAS_EINVAL;
+  const char* p = s;
+  bool neg = false;
+  if (*p == '+' || *p == '-') { neg = (*p == '-'); ++p; }
+  __int128 mant = 0;
+  int ndigits = 0, nfrac = 0, sig = 0;
+  bool seen_dot = false, overflow = false;
+  for (;; ++p) {
+    if (*p >= '0' && *p <= '9') {
+      ++ndigits;
+      if (seen_dot) ++nfrac;
+      if (mant != 0 || *p != '0') {
+        if (++sig > 36) { overflow = true; }
+        else mant = mant * 10 + (*p - '0');
+      }
+    } else if (*p == '.' && !seen_dot) {
+      seen_dot = true;
+    } else {
+      break;
+    }
+  }
+  if (ndigits == 0) return PAS_EINVAL;
+  int exp10 = 0, exp2 = 0;
+  const std::string suf(p);
+  if (suf.empty()) {
+  } else if (suf == "n") { exp10 = -9;
+  } else if (suf == "u") { exp10 = -6;
+  } else if (suf == "m") { exp10 = -3;
+  } else if (suf == "k") { exp10 = 3;
+  } else if (suf == "M") { exp10 = 6;
+  } else if (suf == "G") { exp10 = 9;
+  } else if (suf == "T") { exp10 = 12;
+  } else if (suf == "P") { exp10 = 15;
+  } else if (suf == "E") { exp10 = 18;
+  } else if (suf == "Ki") { exp2 = 10;
+  } else if (suf == "Mi") { exp2 = 20;
+  } else if (suf == "Gi") { exp2 = 30;
+  } else if (suf == "Ti") { exp2 = 40;
+  } else if (suf == "Pi") { exp2 = 50;
+  } else if (suf == "Ei") { exp2 = 60;
+  } else if ((suf[0] == 'e' || suf[0] == 'E') && suf.size() > 1) {
+    const char* q = suf.c_str() + 1;
+    bool eneg = false;
+    if (*q == '+' || *q == '-') { eneg = (*q == '-'); ++q; }
+    if (!*q) return PAS_EINVAL;
+    long e = 0;
+    for (; *q; ++q) {
+      if (*q < '0' || *q > '9') return PAS_EINVAL;
+      e = e * 10 + (*q - '0');
+      if (e > 100000) return PAS_ENOTEXACT;
+    }
+    exp10 = (int)(eneg ? -e : e);
+  } else {
+    return PAS_EINVAL;
+  }
+  if (overflow) return PAS_ENOTEXACT;
+  const __int128 lim = ((__int128)1) << 120;
+  for (int i = 0; i < exp2; ++i) {
+    mant *= 2;
+    if (mant > lim) return PAS_ENOTEXACT;
+  }
+  int e = exp10 + extra10 - nfrac;
+  if (mant == 0) { *out = 0; return PAS_OK; }
+  while (e > 0) {
+    mant *= 10;
+    --e;
+    if (mant > lim) return PAS_ENOTEXACT;
+  }
+  while (e < 0) {
+    if (mant % 10 != 0) return PAS_ENOTEXACT;
+    mant /= 10;
+    ++e;
+  }
+  const __int128 v = neg ? -mant : mant;
+  if (v > (__int128)INT64_MAX || v < (__int128)INT64_MIN) return PAS_ENOTEXACT;
+  *out = (int64_t)v;
+  return PAS_OK;
+}
+
+struct Carve {
+  char* base;
+  size_t off = 0;
+  template <typename T>
+  T* take(size_t count) {
+    T* p = reinterpret_cast<T*>(base + off);
+    off += (count * sizeof(T) + 255) & ~size_t(255);
+    return p;
+  }
+};
+
+static size_t carve_size(std::initializer_list<size_t> sizes) {
+  size_t s = 0;
+  for (size_t b : sizes) s += (b + 255) & ~size_t(255);
+  return s;
+}
+
+}  // namespace pas
+
+using namespace pas;
+
+extern "C" {
+
+int pas_abi_version(void) { return PAS_ABI_VERSION; }
+
+int pas_create(const pas_config* cfg, pas_ctx** out) {
+  if (!out) return PAS_EINVAL;
+  *out = nullptr;
+  pas_ctx* ctx = new (std::nothrow) pas_ctx();
+  if (!ctx) return PAS_ENOMEM;
+  int dev = cfg ? cfg->device : -1;
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) {
+      delete ctx;
+      return PAS_EDEVICE;
+    }
+  }
+  ctx->device = dev;
+  if (hipSetDevice(dev) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return PAS_EDEVICE;
+  }
+  ctx->stream = ctx->own_stream;
+  *out = ctx;
+  return PAS_OK;
+}
+
+void pas_destroy(pas_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  resolve_timing(ctx);
+  for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
+  free_tas(ctx);
+  free_gas(ctx);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->aux) (void)hipFree(ctx->aux);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
+  delete ctx;
+}
+
+const char* pas_last_error(const pas_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int pas_set_stream(pas_ctx* ctx, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  return PAS_OK;
+}
+
+int pas_synchronize(pas_ctx* ctx) {
+  if (!ctx) return PAS_EINVAL;
+  PAS_HIP(ctx, hipSetDevice(ctx->device));
+  PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return PAS_OK;
+}
+
+int pas_parse_operator(const char* op) {
+  if (!op) return PAS_EINVAL;
+  if (std::strcmp(op, "LessThan") == 0) return PAS_OP_LESS_THAN;
+  if (std::strcmp(op, "GreaterThan") == 0) return PAS_OP_GREATER_THAN;
+  if (std::strcmp(op, "Equals") == 0) return PAS_OP_EQUALS;
+  return PAS_EINVAL;
+}
+
+int pas_quantity_to_milli(const char* quantity, int64_t* milli_out) {
+  if (!milli_out) return PAS_EINVAL;
+  return quantity_scaled(quantity, 3, milli_out);
+}
+
+int pas_quantity_as_int64(const char* quantity, int64_t* out) {
+  if (!out) return PAS_EINVAL;
+  int64_t v = 0;
+  const int rc = quantity_scaled(quantity, 0, &v);
+  if (rc == PAS_EINVAL) return rc;
+  *out = (rc == PAS_OK) ? v : 0;  // AsInt64 `ok` ignored by the reference -> 0
+  return PAS_OK;
+}
+
+// --------------------------------------------------------------------------- TAS
+
+int pas_tas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t n_metrics,
+                         const int64_t* v_milli, const uint64_t* present) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_nodes < 0 || n_metrics < 0 || (n_nodes > 0 && n_metrics > 0 && (!v_milli || !present)))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_snapshot_set: bad shape or null input");
+  int rc = activate(ctx);
+  if (rc) return rc;
+  const size_t vb = sizeof(int64_t) * (size_t)n_nodes * (size_t)n_metrics;
+  const size_t pb = sizeof(uint64_t) * (size_t)w64(n_nodes) * (size_t)n_metrics;
+  rc = ensure_scratch(ctx, vb + pb + 256);
+  if (rc) return rc;
+  char* base = static_cast<char*>(ctx->scratch);
+  int64_t* d_v = reinterpret_cast<int64_t*>(base);
+  uint64_t* d_p = reinterpret_cast<uint64_t*>(base + ((vb + 255) & ~size_t(255)));
+  if (vb) PAS_HIP(ctx, hipMemcpyAsync(d_v, v_milli, vb, hipMemcpyHostToDevice, ctx->stream));
+  if (pb) PAS_HIP(ctx, hipMemcpyAsync(d_p, present, pb, hipMemcpyHostToDevice, ctx->stream));
+  rc = tas_snapshot_build(ctx, gen, n_nodes, n_metrics, d_v, d_p, ctx->stream);
+  if (rc) return rc;
+  PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return PAS_OK;
+}
+
+int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t n_metrics,
+                                const int64_t* d_v_milli, const uint64_t* d_present,
+                                void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_nodes < 0 || n_metrics < 0) return set_error(ctx, PAS_EINVAL, "bad snapshot shape");
+  int rc = activate(ctx);
+  if (rc) return rc;
+  return tas_snapshot_build(ctx, gen, n_nodes, n_metrics, d_v_milli, d_present,
+                            pick_stream(ctx, hip_stream));
+}
+
+int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
+                          int32_t* n_metrics) {
+  if (!ctx) return PAS_EINVAL;
+  if (!ctx->tas.valid) return PAS_ENOSNAP;
+  if (gen) *gen = ctx->tas.gen;
+  if (n_nodes) *n_nodes = ctx->tas.n_nodes;
+  if (n_metrics) *n_metrics = ctx->tas.n_metrics;
+  return PAS_OK;
+}
+
+static int check_tas_gen(pas_ctx* ctx, uint64_t gen) {
+  if (!ctx->tas.valid) return set_error(ctx, PAS_ENOSNAP, "no TAS snapshot uploaded");
+  if (ctx->tas.gen != gen)
+    return set_error(ctx, PAS_ESTALE, "TAS snapshot generation mismatch: resident " +
+                                          std::to_string(ctx->tas.gen) + ", requested " +
+                                          std::to_string(gen));
+  return PAS_OK;
+}
+
+// Host-side rule validation: an unknown operator string panics in core.EvaluateRule
+// (operator.go:25) only when the rule is evaluated, i.e. when its metric is cached
+// (dontschedule/strategy.go:28-32 skips missing metrics first).  Here: PAS_EINVAL.
+static int validate_rules(pas_ctx* ctx, int32_t n, const pas_rule* rules) {
+  for (int32_t i = 0; i < n; ++i) {
+    const pas_rule& r = rules[i];
+    if (r.op >= 0 && r.op <= 2) continue;
+    if (r.metric < 0 || r.metric >= ctx->tas.n_metrics) continue;  // never evaluated
+    return set_error(ctx, PAS_EINVAL, "rule " + std::to_string(i) + ": unknown operator " +
+                                          std::to_string(r.op) +
+                                          " (the reference panics in EvaluateRule)");
+  }
+  return PAS_OK;
+}
+
+static int validate_csr(pas_ctx* ctx, int32_t n, const int32_t* off, const char* what) {
+  if (off[0] != 0) return set_error(ctx, PAS_EINVAL, std::string(what) + ": offsets[0] != 0");
+  for (int32_t i = 0; i < n; ++i)
+    if (off[i + 1] < off[i])
+      return set_error(ctx, PAS_EINVAL, std::string(what) + ": offsets not monotone");
+  return PAS_OK;
+}
+
+int pas_tas_eval(pas_ctx* ctx, uint64_t gen, int32_t n_pods, const pas_rule* rules,
+                 const int32_t* rule_off, const pas_rule* prio, const uint64_t* cand,
+                 uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_pods < 0 || (n_pods > 0 && (!rule_off || !prio)))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_eval: null rule_off/prio");
+  if ((flags & PAS_TAS_FILTER) && n_pods > 0 && !pass_out)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_eval: FILTER without pass_out");
+  if ((flags & PAS_TAS_PRIORITIZE) && n_pods > 0 && (!order_out || !order_len))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_eval: PRIORITIZE without order outputs");
+  if (n_pods == 0) return PAS_OK;
+  if ((rc = validate_csr(ctx, n_pods, rule_off, "rule_off"))) return rc;
+  const int32_t n_rules = rule_off[n_pods];
+  if (n_rules > 0 && !rules) return set_error(ctx, PAS_EINVAL, "pas_tas_eval: null rules");
+  if ((rc = validate_rules(ctx, n_rules, rules))) return rc;
+  if ((rc = activate(ctx))) return rc;
+  const int64_t N = ctx->tas.n_nodes, W = w64(N);
+  const size_t b_rules = sizeof(pas_rule) * (size_t)std::max(n_rules, 1);
+  const size_t b_off = sizeof(int32_t) * (size_t)(n_pods + 1);
+  const size_t b_prio = sizeof(pas_rule) * (size_t)n_pods;
+  const size_t b_cand = cand ? sizeof(uint64_t) * (size_t)(W * n_pods) : 0;
+  const size_t b_pass = (flags & PAS_TAS_FILTER) ? sizeof(uint64_t) * (size_t)(W * n_pods) : 0;
+  const size_t b_order =
+      (flags & PAS_TAS_PRIORITIZE) ? sizeof(int32_t) * (size_t)(N * n_pods) : 0;
+  const size_t b_len = sizeof(int32_t) * (size_t)n_pods;
+  if ((rc = ensure_scratch(ctx, carve_size({b_rules, b_off, b_prio, b_cand, b_pass, b_order,
+                                            b_len}))))
+    return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  pas_rule* d_rules = cv.take<pas_rule>(std::max(n_rules, 1));
+  int32_t* d_off = cv.take<int32_t>(n_pods + 1);
+  pas_rule* d_prio = cv.take<pas_rule>(n_pods);
+  uint64_t* d_cand = cand ? cv.take<uint64_t>(W * n_pods) : nullptr;
+  uint64_t* d_pass = b_pass ? cv.take<uint64_t>(W * n_pods) : nullptr;
+  int32_t* d_order = b_order ? cv.take<int32_t>(N * n_pods) : nullptr;
+  int32_t* d_len = cv.take<int32_t>(n_pods);
+  hipStream_t s = ctx->stream;
+  if (n_rules) PAS_HIP(ctx, hipMemcpyAsync(d_rules, rules, b_rules, hipMemcpyHostToDevice, s));
+  PAS_HIP(ctx, hipMemcpyAsync(d_off, rule_off, b_off, hipMemcpyHostToDevice, s));
+  PAS_HIP(ctx, hipMemcpyAsync(d_prio, prio, b_prio, hipMemcpyHostToDevice, s));
+  if (d_cand) PAS_HIP(ctx, hipMemcpyAsync(d_cand, cand, b_cand, hipMemcpyHostToDevice, s));
+  rc = tas_eval_launch(ctx, n_pods, n_rules, d_rules, d_off, d_prio, d_cand, flags, d_pass,
+                       d_order, d_len, s);
+  if (rc) return rc;
+  if (d_pass) PAS_HIP(ctx, hipMemcpyAsync(pass_out, d_pass, b_pass, hipMemcpyDeviceToHost, s));
+  if (flags & PAS_TAS_PRIORITIZE) {
+    PAS_HIP(ctx, hipMemcpyAsync(order_len, d_len, b_len, hipMemcpyDeviceToHost, s));
+    PAS_HIP(ctx, hipMemcpyAsync(order_out, d_order, b_order, hipMemcpyDeviceToHost, s));
+  }
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  return PAS_OK;
+}
+
+int pas_tas_eval_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_rules,
+                        const pas_rule* d_rules, const int32_t* d_rule_off,
+                        const pas_rule* d_prio, const uint64_t* d_cand, uint32_t flags,
+                        uint64_t* d_pass_out, int32_t* d_order_out, int32_t* d_order_len,
+                        void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_pods < 0 || n_rules < 0) return set_error(ctx, PAS_EINVAL, "negative count");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_rule_off || !d_prio || (n_rules > 0 && !d_rules))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_eval_device: null input");
+  if ((flags & PAS_TAS_FILTER) && !d_pass_out)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_eval_device: FILTER without pass_out");
+  if ((flags & PAS_TAS_PRIORITIZE) && (!d_order_out || !d_order_len))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_eval_device: PRIORITIZE without outputs");
+  if ((rc = activate(ctx))) return rc;
+  return tas_eval_launch(ctx, n_pods, n_rules, d_rules, d_rule_off, d_prio, d_cand, flags,
+                         d_pass_out, d_order_out, d_order_len, pick_stream(ctx, hip_stream));
+}
+
+int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const pas_rule* rules,
+                       const int32_t* rule_off, uint64_t* viol_out) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_strategies < 0) return set_error(ctx, PAS_EINVAL, "negative strategy count");
+  if (n_strategies == 0) return PAS_OK;
+  if (!rule_off || !viol_out) return set_error(ctx, PAS_EINVAL, "null rule_off/viol_out");
+  if ((rc = validate_csr(ctx, n_strategies, rule_off, "rule_off"))) return rc;
+  const int32_t n_rules = rule_off[n_strategies];
+  if (n_rules > 0 && !rules) return set_error(ctx, PAS_EINVAL, "null rules");
+  if ((rc = validate_rules(ctx, n_rules, rules))) return rc;
+  if ((rc = activate(ctx))) return rc;
+  const int64_t W = w64(ctx->tas.n_nodes);
+  const size_t b_rules = sizeof(pas_rule) * (size_t)std::max(n_rules, 1);
+  const size_t b_off = sizeof(int32_t) * (size_t)(n_strategies + 1);
+  const size_t b_viol = sizeof(uint64_t) * (size_t)(W * n_strategies);
+  if ((rc = ensure_scratch(ctx, carve_size({b_rules, b_off, b_viol})))) return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  pas_rule* d_rules = cv.take<pas_rule>(std::max(n_rules, 1));
+  int32_t* d_off = cv.take<int32_t>(n_strategies + 1);
+  uint64_t* d_viol = cv.take<uint64_t>(W * n_strategies);
+  hipStream_t s = ctx->stream;
+  if (n_rules) PAS_HIP(ctx, hipMemcpyAsync(d_rules, rules, b_rules, hipMemcpyHostToDevice, s));
+  PAS_HIP(ctx, hipMemcpyAsync(d_off, rule_off, b_off, hipMemcpyHostToDevice, s));
+  rc = tas_violations_launch(ctx, n_strategies, d_rules, d_off, d_viol, s);
+  if (rc) return rc;
+  PAS_HIP(ctx, hipMemcpyAsync(viol_out, d_viol, b_viol, hipMemcpyDeviceToHost, s));
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  return PAS_OK;
+}
+
+int pas_tas_violations_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
+                              int32_t n_rules, const pas_rule* d_rules,
+                              const int32_t* d_rule_off, uint64_t* d_viol_out,
+                              void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_strategies < 0 || n_rules < 0) return set_error(ctx, PAS_EINVAL, "negative count");
+  if (n_strategies == 0) return PAS_OK;
+  if (!d_rule_off || !d_viol_out || (n_rules > 0 && !d_rules))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_violations_device: null input");
+  if ((rc = activate(ctx))) return rc;
+  return tas_violations_launch(ctx, n_strategies, d_rules, d_rule_off, d_viol_out,
+                               pick_stream(ctx, hip_stream));
+}
+
+// --------------------------------------------------------------------------- GAS
+
+static int gas_alloc(pas_ctx* ctx, int32_t n_nodes, int32_t max_cards, int32_t n_res) {
+  GasSnapshot& g = ctx->gas;
+  if (g.n_nodes != n_nodes || g.max_cards != max_cards || g.n_res != n_res || !g.n_cards) {
+    PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    free_gas(ctx);
+    const size_t nn = (size_t)std::max(n_nodes, 1);
+    PAS_HIP(ctx, hipMalloc(&g.n_cards, sizeof(int32_t) * nn));
+    PAS_HIP(ctx, hipMalloc(&g.cap, sizeof(int64_t) * nn * (size_t)std::max(n_res, 1)));
+    PAS_HIP(ctx, hipMalloc(&g.used, sizeof(int64_t) * nn * (size_t)std::max(max_cards, 1) *
+                                        (size_t)std::max(n_res, 1)));
+    g.n_nodes = n_nodes;
+    g.max_cards = max_cards;
+    g.n_res = n_res;
+  }
+  return PAS_OK;
+}
+
+static int gas_shape_ok(pas_ctx* ctx, int32_t n_nodes, int32_t max_cards, int32_t n_res) {
+  if (n_nodes < 0 || max_cards < 1 || n_res < 1)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_snapshot_set: bad shape");
+  if (max_cards > PAS_GAS_MAX_CARDS || n_res > PAS_GAS_MAX_RES)
+    return set_error(ctx, PAS_ECAPACITY,
+                     "pas_gas_snapshot_set: max_cards <= 8 and n_res <= 4 supported");
+  return PAS_OK;
+}
+
+int pas_gas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
+                         int32_t n_res, const int32_t* n_cards, const int64_t* cap_per_gpu,
+                         const int64_t* used) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = gas_shape_ok(ctx, n_nodes, max_cards, n_res);
+  if (rc) return rc;
+  if (n_nodes > 0 && (!n_cards || !cap_per_gpu || !used))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_snapshot_set: null input");
+  for (int32_t n = 0; n < n_nodes; ++n)
+    if (n_cards[n] > max_cards)
+      return set_error(ctx, PAS_EINVAL, "pas_gas_snapshot_set: n_cards > max_cards");
+  if ((rc = activate(ctx))) return rc;
+  if ((rc = gas_alloc(ctx, n_nodes, max_cards, n_res))) return rc;
+  GasSnapshot& g = ctx->gas;
+  hipStream_t s = ctx->stream;
+  if (n_nodes > 0) {
+    PAS_HIP(ctx, hipMemcpyAsync(g.n_cards, n_cards, sizeof(int32_t) * n_nodes,
+                                hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(g.cap, cap_per_gpu, sizeof(int64_t) * n_nodes * n_res,
+                                hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(g.used, used,
+                                sizeof(int64_t) * (size_t)n_nodes * max_cards * n_res,
+                                hipMemcpyHostToDevice, s));
+  }
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  g.gen = gen;
+  g.valid = true;
+  return PAS_OK;
+}
+
+int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
+                                int32_t n_res, const int32_t* d_n_cards,
+                                const int64_t* d_cap_per_gpu, const int64_t* d_used,
+                                void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = gas_shape_ok(ctx, n_nodes, max_cards, n_res);
+  if (rc) return rc;
+  if (n_nodes > 0 && (!d_n_cards || !d_cap_per_gpu || !d_used))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_snapshot_set_device: null input");
+  if ((rc = activate(ctx))) return rc;
+  if ((rc = gas_alloc(ctx, n_nodes, max_cards, n_res))) return rc;
+  GasSnapshot& g = ctx->gas;
+  hipStream_t s = pick_stream(ctx, hip_stream);
+  if (n_nodes > 0) {
+    PAS_HIP(ctx, hipMemcpyAsync(g.n_cards, d_n_cards, sizeof(int32_t) * n_nodes,
+                                hipMemcpyDeviceToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(g.cap, d_cap_per_gpu, sizeof(int64_t) * n_nodes * n_res,
+                                hipMemcpyDeviceToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(g.used, d_used,
+                                sizeof(int64_t) * (size_t)n_nodes * max_cards * n_res,
+                                hipMemcpyDeviceToDevice, s));
+  }
+  g.gen = gen;
+  g.valid = true;
+  return PAS_OK;
+}
+
+static int check_gas_gen(pas_ctx* ctx, uint64_t gen) {
+  if (!ctx->gas.valid) return set_error(ctx, PAS_ENOSNAP, "no GAS snapshot uploaded");
+  if (ctx->gas.gen != gen) return set_error(ctx, PAS_ESTALE, "GAS snapshot generation mismatch");
+  return PAS_OK;
+}
+
+int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                const int32_t* n_containers, uint32_t* res_out) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_gas_gen(ctx, gen);
+  if (rc) return rc;
+  const int32_t Q = ctx->gas.n_res;
+  if (n_pods < 0 || max_containers < 0 || i915_index >= Q || i915_index < -1)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit: bad shape");
+  if (n_pods == 0) return PAS_OK;
+  if (!n_containers || !res_out || (max_containers > 0 && (!req || !req_mask)))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit: null input");
+  // Validate the packed-annotation capacity (sum of i915 counts per pod).
+  for (int32_t p = 0; p < n_pods; ++p) {
+    if (n_containers[p] < 0 || n_containers[p] > max_containers)
+      return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_containers out of range");
+    int64_t sel = 0;
+    for (int32_t c = 0; c < n_containers[p]; ++c) {
+      const int64_t b = (int64_t)p * max_containers + c;
+      if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, "pas_gas_fit: mask bit >= n_res");
+      if (i915_index >= 0 && (req_mask[b] >> i915_index & 1u)) {
+        const int64_t v = req[b * Q + i915_index];
+        if (v > 0) sel += v;
+      }
+    }
+    if (sel > PAS_GAS_MAX_SELECTIONS)
+      return set_error(ctx, PAS_ECAPACITY, "pod " + std::to_string(p) +
+                                               " needs more than 8 card selections");
+  }
+  if ((rc = activate(ctx))) return rc;
+  const int64_t N = ctx->gas.n_nodes;
+  const size_t C = (size_t)std::max(max_containers, 1);
+  const size_t b_req = sizeof(int64_t) * (size_t)n_pods * C * Q;
+  const size_t b_mask = sizeof(uint32_t) * (size_t)n_pods * C;
+  const size_t b_nc = sizeof(int32_t) * (size_t)n_pods;
+  const size_t b_res = sizeof(uint32_t) * (size_t)n_pods * (size_t)N;
+  if ((rc = ensure_scratch(ctx, carve_size({b_req, b_mask, b_nc, b_res})))) return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  int64_t* d_req = cv.take<int64_t>((size_t)n_pods * C * Q);
+  uint32_t* d_mask = cv.take<uint32_t>((size_t)n_pods * C);
+  int32_t* d_nc = cv.take<int32_t>(n_pods);
+  uint32_t* d_res = cv.take<uint32_t>((size_t)n_pods * N);
+  hipStream_t s = ctx->stream;
+  if (max_containers > 0) {
+    PAS_HIP(ctx, hipMemcpyAsync(d_req, req, b_req, hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(d_mask, req_mask, b_mask, hipMemcpyHostToDevice, s));
+  }
+  PAS_HIP(ctx, hipMemcpyAsync(d_nc, n_containers, b_nc, hipMemcpyHostToDevice, s));
+  rc = gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_mask, d_nc, d_res, s);
+  if (rc) return rc;
+  if (b_res) PAS_HIP(ctx, hipMemcpyAsync(res_out, d_res, b_res, hipMemcpyDeviceToHost, s));
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  return PAS_OK;
+}
+
+int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                       int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
+                       const int32_t* d_n_containers, uint32_t* d_res_out, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_gas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_pods < 0 || max_containers < 0 || i915_index >= ctx->gas.n_res || i915_index < -1)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_device: bad shape");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_n_containers || !d_res_out || (max_containers > 0 && (!d_req || !d_req_mask)))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_device: null input");
+  if ((rc = activate(ctx))) return rc;
+  return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                        d_n_containers, d_res_out, pick_stream(ctx, hip_stream));
+}
+
+// --------------------------------------------------------------------------- timing
+
+int pas_set_timing(pas_ctx* ctx, int enable) {
+  if (!ctx) return PAS_EINVAL;
+  ctx->timing = enable != 0;
+  return PAS_OK;
+}
+
+int pas_kernel_time(pas_ctx* ctx, int32_t kernel_id, double* total_ms, int64_t* launches) {
+  if (!ctx || kernel_id < 0 || kernel_id >= PAS_K_COUNT) return PAS_EINVAL;
+  resolve_timing(ctx);
+  if (total_ms) *total_ms = ctx->total_ms[kernel_id];
+  if (launches) *launches = ctx->launches[kernel_id];
+  return PAS_OK;
+}
+
+int pas_reset_timing(pas_ctx* ctx) {
+  if (!ctx) return PAS_EINVAL;
+  resolve_timing(ctx);
+  for (int i = 0; i < PAS_K_COUNT; ++i) {
+    ctx->total_ms[i] = 0;
+    ctx->launches[i] = 0;
+  }
+  return PAS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,127 @@
+// pas_internal.h — context and snapshot state shared by the HIP translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "pas.h"
+
+namespace pas {
+
+constexpr uint32_t kNoRank = 0xFFFFFFFFu;
+constexpr int kOrderAsc = 0;   // LessThan   (operator.go:38-39)
+constexpr int kOrderDesc = 1;  // GreaterThan (operator.go:36-37)
+constexpr int kOrderIndex = 2; // any other operator: no sort
+constexpr int kNumOrders = 3;
+
+inline int64_t w64(int64_t n) { return (n + 63) / 64; }
+inline int64_t w32(int64_t n) { return (n + 31) / 32; }
+
+// Device-resident TAS snapshot.  Layout in HBM (M metrics, N nodes):
+//   vals     int64 [M][N]      raw v_milli (deschedule sweep reads it directly)
+//   present  uint64 [M][W64]
+//   cnt      int32 [M]         nodes that have metric m
+//   sorted   int64 [M][N]      ascending values of the present nodes (first cnt[m])
+//   perm     int32 [3][M][N]   node ids in asc / desc / index order (first cnt[m])
+//   rank     uint32 [3][M][N]  position of node n in each order, kNoRank if absent
+struct TasSnapshot {
+  bool valid = false;
+  uint64_t gen = 0;
+  int32_t n_nodes = 0;
+  int32_t n_metrics = 0;
+  int64_t* vals = nullptr;
+  uint64_t* present = nullptr;
+  int32_t* cnt = nullptr;
+  int64_t* sorted = nullptr;
+  int32_t* perm = nullptr;
+  uint32_t* rank = nullptr;
+  // build scratch
+  int64_t* vals_c = nullptr;       // compacted values in index order
+  uint32_t* word_scan = nullptr;   // [M*W64 + 1]
+  int32_t* seg_begin = nullptr;    // [M]
+  int32_t* seg_end = nullptr;      // [M]
+  void* sort_tmp = nullptr;
+  size_t sort_tmp_bytes = 0;
+  void* scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+};
+
+// Device-resident GAS snapshot (node-major):
+//   n_cards int32 [N], cap int64 [N][Q], used int64 [N][K][Q]
+struct GasSnapshot {
+  bool valid = false;
+  uint64_t gen = 0;
+  int32_t n_nodes = 0;
+  int32_t max_cards = 0;
+  int32_t n_res = 0;
+  int32_t* n_cards = nullptr;
+  int64_t* cap = nullptr;
+  int64_t* used = nullptr;
+};
+
+struct TimedLaunch {
+  hipEvent_t start;
+  hipEvent_t stop;
+  int32_t kernel;
+};
+
+}  // namespace pas
+
+struct pas_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  std::string err;
+  pas::TasSnapshot tas;
+  pas::GasSnapshot gas;
+  // per-call scratch (grown on demand, never freed inside a launch function)
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  void* aux = nullptr;  // per-call device table: TAS rule ranges / GAS container steps
+  size_t aux_bytes = 0;
+  // timing
+  bool timing = false;
+  std::vector<pas::TimedLaunch> pending;
+  std::vector<hipEvent_t> event_pool;
+  double total_ms[PAS_K_COUNT] = {};
+  int64_t launches[PAS_K_COUNT] = {};
+};
+
+namespace pas {
+
+int set_error(pas_ctx* ctx, int code, const std::string& msg);
+int check_hip(pas_ctx* ctx, hipError_t e, const char* what);
+#define PAS_HIP(ctx, expr)                                       \
+  do {                                                           \
+    hipError_t _e = (expr);                                      \
+    if (_e != hipSuccess) return ::pas::check_hip(ctx, _e, #expr); \
+  } while (0)
+
+int ensure_scratch(pas_ctx* ctx, size_t bytes);
+int activate(pas_ctx* ctx);  // hipSetDevice(ctx->device)
+hipStream_t pick_stream(pas_ctx* ctx, void* s);
+
+// Bracket a launch with timing events when ctx->timing is on.
+void timing_begin(pas_ctx* ctx, hipStream_t s, int kernel, TimedLaunch* tl);
+void timing_end(pas_ctx* ctx, hipStream_t s, TimedLaunch* tl);
+
+void free_tas(pas_ctx* ctx);
+void free_gas(pas_ctx* ctx);
+
+// Per-translation-unit entry points used by the C-ABI layer.
+int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t n_metrics,
+                       const int64_t* d_vals, const uint64_t* d_present, hipStream_t s);
+int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
+                    const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
+                    uint32_t flags, uint64_t* d_pass, int32_t* d_order, int32_t* d_len,
+                    hipStream_t s);
+int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
+                          const int32_t* d_rule_off, uint64_t* d_viol, hipStream_t s);
+int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
+                   const int64_t* d_req, const uint32_t* d_req_mask,
+                   const int32_t* d_n_containers, uint32_t* d_res, hipStream_t s);
+
+}  // namespace pas

@@ -1,0 +1,137 @@
+"""ctypes binding of lib/libpas.so (the C-ABI declared in include/pas.h).
+
+The library is the product: HIP kernels for gfx950 behind a plain C ABI.  This module
+only loads it and declares the signatures.  There is no fallback: if the shared
+object is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
+
+_PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpas.so")
+HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG_DIR)), "include", "pas.h")
+
+PAS_OK = 0
+PAS_EINVAL = -1
+PAS_ESTALE = -2
+PAS_ENOTEXACT = -3
+PAS_EDEVICE = -4
+PAS_ENOMEM = -5
+PAS_ENOSNAP = -6
+PAS_ECAPACITY = -7
+
+STATUS_NAMES = {
+    PAS_OK: "PAS_OK",
+    PAS_EINVAL: "PAS_EINVAL",
+    PAS_ESTALE: "PAS_ESTALE",
+    PAS_ENOTEXACT: "PAS_ENOTEXACT",
+    PAS_EDEVICE: "PAS_EDEVICE",
+    PAS_ENOMEM: "PAS_ENOMEM",
+    PAS_ENOSNAP: "PAS_ENOSNAP",
+    PAS_ECAPACITY: "PAS_ECAPACITY",
+}
+
+PAS_OP_LESS_THAN = 0
+PAS_OP_GREATER_THAN = 1
+PAS_OP_EQUALS = 2
+
+PAS_TAS_FILTER = 1
+PAS_TAS_PRIORITIZE = 2
+
+PAS_GAS_MAX_CARDS = 8
+PAS_GAS_MAX_RES = 4
+PAS_GAS_MAX_SELECTIONS = 8
+
+PAS_K_TAS_RANGES = 0
+PAS_K_TAS_EVAL = 1
+PAS_K_TAS_VIOLATIONS = 2
+PAS_K_GAS_PREP = 3
+PAS_K_GAS_FIT = 4
+KERNEL_NAMES = {
+    PAS_K_TAS_RANGES: "tas_ranges_kernel",
+    PAS_K_TAS_EVAL: "tas_eval_kernel",
+    PAS_K_TAS_VIOLATIONS: "tas_violations_kernel",
+    PAS_K_GAS_PREP: "gas_prep_kernel",
+    PAS_K_GAS_FIT: "gas_fit_kernel",
+}
+
+
+class PasError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{STATUS_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+class PasConfig(ctypes.Structure):
+    _fields_ = [("device", c_int32), ("reserved", c_int32)]
+
+
+# Every exported symbol with (restype, argtypes); tests check this list against pas.h.
+_P = c_void_p
+SIGNATURES = {
+    "pas_abi_version": (c_int, []),
+    "pas_create": (c_int, [POINTER(PasConfig), POINTER(c_void_p)]),
+    "pas_destroy": (None, [_P]),
+    "pas_last_error": (c_char_p, [_P]),
+    "pas_set_stream": (c_int, [_P, _P]),
+    "pas_synchronize": (c_int, [_P]),
+    "pas_parse_operator": (c_int, [c_char_p]),
+    "pas_quantity_to_milli": (c_int, [c_char_p, POINTER(c_int64)]),
+    "pas_quantity_as_int64": (c_int, [c_char_p, POINTER(c_int64)]),
+    "pas_tas_snapshot_set": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P]),
+    "pas_tas_snapshot_set_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P]),
+    "pas_tas_snapshot_info": (c_int, [_P, POINTER(c_uint64), POINTER(c_int32), POINTER(c_int32)]),
+    "pas_tas_eval": (c_int, [_P, c_uint64, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P]),
+    "pas_tas_eval_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P],
+    ),
+    "pas_tas_violations": (c_int, [_P, c_uint64, c_int32, _P, _P, _P]),
+    "pas_tas_violations_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P]),
+    "pas_gas_snapshot_set": (c_int, [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P]),
+    "pas_gas_snapshot_set_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P],
+    ),
+    "pas_gas_fit": (c_int, [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P]),
+    "pas_gas_fit_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
+    ),
+    "pas_set_timing": (c_int, [_P, c_int]),
+    "pas_kernel_time": (c_int, [_P, c_int32, POINTER(c_double), POINTER(c_int64)]),
+    "pas_reset_timing": (c_int, [_P]),
+}
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libpas.so once; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not found: build it with `make -C platform-aware-scheduling_amd` "
+            "(or __graft_entry__.build()); there is no CPU fallback"
+        )
+    # One HIP runtime per process: torch's wheel ships its own libamdhip64.so with the
+    # same soname (libamdhip64.so.7).  Loading torch first makes libpas.so bind to that
+    # instance, so device pointers from torch allocations and torch streams are valid in
+    # both; loading libpas.so first would leave torch a second runtime that cannot
+    # initialise the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (restype, argtypes) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    _lib = lib
+    return lib

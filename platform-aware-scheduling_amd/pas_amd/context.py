@@ -1,0 +1,253 @@
+"""Thin Python handle over a pas_ctx (include/pas.h).
+
+Host entry points take/return numpy arrays; *_device entry points take objects with a
+``data_ptr()`` (torch tensors on the GPU) and a HIP stream handle, so benchmarks can run
+with every input already resident in HBM.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_double, c_int32, c_int64, c_uint64, c_void_p
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import PasError
+
+# pas_rule {int32 metric; int32 op; int64 target}
+RULE_DTYPE = np.dtype([("metric", "<i4"), ("op", "<i4"), ("target", "<i8")], align=True)
+assert RULE_DTYPE.itemsize == 16
+
+
+def w64(n: int) -> int:
+    return (n + 63) // 64
+
+
+def make_rules(metric, op, target) -> np.ndarray:
+    metric = np.asarray(metric, dtype=np.int32)
+    r = np.zeros(metric.shape[0], dtype=RULE_DTYPE)
+    r["metric"] = metric
+    r["op"] = np.asarray(op, dtype=np.int32)
+    r["target"] = np.asarray(target, dtype=np.int64)
+    return r
+
+
+def _ptr(a: Optional[np.ndarray]):
+    if a is None:
+        return None
+    assert a.flags["C_CONTIGUOUS"], "arrays passed to libpas must be C-contiguous"
+    return a.ctypes.data_as(c_void_p)
+
+
+def _dptr(t):
+    if t is None:
+        return None
+    return c_void_p(t.data_ptr())
+
+
+def _stream(s):
+    if s is None:
+        return None
+    if isinstance(s, int):
+        return c_void_p(s)
+    return c_void_p(s.cuda_stream)  # torch.cuda.Stream
+
+
+def parse_operator(op: str) -> int:
+    """core.EvaluateRule's operator lookup (operator.go:14-25) via the C-ABI."""
+    return _lib.load().pas_parse_operator(op.encode())
+
+
+def quantity_to_milli(q: str) -> int:
+    """Exact value*1000 of a resource.Quantity string; PasError(PAS_ENOTEXACT) otherwise."""
+    out = c_int64()
+    rc = _lib.load().pas_quantity_to_milli(q.encode(), byref(out))
+    if rc != _lib.PAS_OK:
+        raise PasError(rc, f"quantity {q!r}")
+    return out.value
+
+
+def quantity_as_int64(q: str) -> int:
+    """resource.Quantity.AsInt64 with `ok` ignored (gpuscheduler/utils.go:23)."""
+    out = c_int64()
+    rc = _lib.load().pas_quantity_as_int64(q.encode(), byref(out))
+    if rc != _lib.PAS_OK:
+        raise PasError(rc, f"quantity {q!r}")
+    return out.value
+
+
+class Context:
+    """One pas_ctx bound to a HIP device."""
+
+    def __init__(self, device: int = -1):
+        self._l = _lib.load()
+        h = c_void_p()
+        cfg = _lib.PasConfig(device, 0)
+        rc = self._l.pas_create(byref(cfg), byref(h))
+        if rc != _lib.PAS_OK:
+            raise PasError(rc, "pas_create failed (no usable HIP device?)")
+        self._h = h
+        self.n_nodes = 0
+        self.n_metrics = 0
+        self.gas_shape = (0, 0, 0)
+
+    # ------------------------------------------------------------------ plumbing
+    def close(self):
+        if getattr(self, "_h", None):
+            self._l.pas_destroy(self._h)
+            self._h = None
+
+    def __del__(self):  # pragma: no cover - best effort
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, rc: int, what: str):
+        if rc != _lib.PAS_OK:
+            msg = self._l.pas_last_error(self._h)
+            raise PasError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def last_error(self) -> str:
+        return self._l.pas_last_error(self._h).decode()
+
+    def set_stream(self, stream):
+        self._check(self._l.pas_set_stream(self._h, _stream(stream)), "pas_set_stream")
+
+    def synchronize(self):
+        self._check(self._l.pas_synchronize(self._h), "pas_synchronize")
+
+    # ------------------------------------------------------------------ timing
+    def set_timing(self, enable: bool):
+        self._check(self._l.pas_set_timing(self._h, 1 if enable else 0), "pas_set_timing")
+
+    def kernel_time(self, kernel_id: int) -> Tuple[float, int]:
+        ms = c_double()
+        n = c_int64()
+        self._check(self._l.pas_kernel_time(self._h, kernel_id, byref(ms), byref(n)),
+                    "pas_kernel_time")
+        return ms.value, n.value
+
+    def reset_timing(self):
+        self._check(self._l.pas_reset_timing(self._h), "pas_reset_timing")
+
+    # ------------------------------------------------------------------ TAS
+    def tas_snapshot_set(self, gen: int, v_milli: np.ndarray, present: np.ndarray):
+        v = np.ascontiguousarray(v_milli, dtype=np.int64)
+        m, n = v.shape
+        p = np.ascontiguousarray(present, dtype=np.uint64)
+        assert p.shape == (m, w64(n)), (p.shape, (m, w64(n)))
+        self._check(self._l.pas_tas_snapshot_set(self._h, gen, n, m, _ptr(v), _ptr(p)),
+                    "pas_tas_snapshot_set")
+        self.n_nodes, self.n_metrics = n, m
+
+    def tas_snapshot_set_device(self, gen: int, n_nodes: int, n_metrics: int, v_t, p_t,
+                                stream=None):
+        self._check(self._l.pas_tas_snapshot_set_device(self._h, gen, n_nodes, n_metrics,
+                                                        _dptr(v_t), _dptr(p_t),
+                                                        _stream(stream)),
+                    "pas_tas_snapshot_set_device")
+        self.n_nodes, self.n_metrics = n_nodes, n_metrics
+
+    def tas_snapshot_info(self):
+        g = c_uint64()
+        n = c_int32()
+        m = c_int32()
+        self._check(self._l.pas_tas_snapshot_info(self._h, byref(g), byref(n), byref(m)),
+                    "pas_tas_snapshot_info")
+        return g.value, n.value, m.value
+
+    def tas_eval(self, gen: int, rules: np.ndarray, rule_off: np.ndarray, prio: np.ndarray,
+                 cand: Optional[np.ndarray] = None,
+                 flags: int = _lib.PAS_TAS_FILTER | _lib.PAS_TAS_PRIORITIZE):
+        """Returns (pass[P, W64] uint64 or None, order[P, N] int32 or None, len[P] or None)."""
+        rule_off = np.ascontiguousarray(rule_off, dtype=np.int32)
+        n_pods = rule_off.shape[0] - 1
+        rules = np.ascontiguousarray(rules, dtype=RULE_DTYPE)
+        prio = np.ascontiguousarray(prio, dtype=RULE_DTYPE)
+        assert prio.shape[0] == n_pods
+        n = self.n_nodes
+        if cand is not None:
+            cand = np.ascontiguousarray(cand, dtype=np.uint64)
+            assert cand.shape == (n_pods, w64(n))
+        pass_out = np.zeros((n_pods, w64(n)), np.uint64) if flags & _lib.PAS_TAS_FILTER else None
+        order = np.zeros((n_pods, n), np.int32) if flags & _lib.PAS_TAS_PRIORITIZE else None
+        lens = np.zeros(n_pods, np.int32) if flags & _lib.PAS_TAS_PRIORITIZE else None
+        rc = self._l.pas_tas_eval(self._h, gen, n_pods, _ptr(rules) if rules.size else None,
+                                  _ptr(rule_off), _ptr(prio), _ptr(cand), flags, _ptr(pass_out),
+                                  _ptr(order), _ptr(lens))
+        self._check(rc, "pas_tas_eval")
+        return pass_out, order, lens
+
+    def tas_eval_device(self, gen: int, n_pods: int, n_rules: int, rules_t, rule_off_t, prio_t,
+                        cand_t, flags: int, pass_t, order_t, len_t, stream=None):
+        rc = self._l.pas_tas_eval_device(self._h, gen, n_pods, n_rules, _dptr(rules_t),
+                                         _dptr(rule_off_t), _dptr(prio_t), _dptr(cand_t), flags,
+                                         _dptr(pass_t), _dptr(order_t), _dptr(len_t),
+                                         _stream(stream))
+        self._check(rc, "pas_tas_eval_device")
+
+    def tas_violations(self, gen: int, rules: np.ndarray, rule_off: np.ndarray) -> np.ndarray:
+        rule_off = np.ascontiguousarray(rule_off, dtype=np.int32)
+        s = rule_off.shape[0] - 1
+        rules = np.ascontiguousarray(rules, dtype=RULE_DTYPE)
+        out = np.zeros((s, w64(self.n_nodes)), np.uint64)
+        rc = self._l.pas_tas_violations(self._h, gen, s, _ptr(rules) if rules.size else None,
+                                        _ptr(rule_off), _ptr(out))
+        self._check(rc, "pas_tas_violations")
+        return out
+
+    def tas_violations_device(self, gen: int, n_strat: int, n_rules: int, rules_t, rule_off_t,
+                              viol_t, stream=None):
+        rc = self._l.pas_tas_violations_device(self._h, gen, n_strat, n_rules, _dptr(rules_t),
+                                               _dptr(rule_off_t), _dptr(viol_t),
+                                               _stream(stream))
+        self._check(rc, "pas_tas_violations_device")
+
+    # ------------------------------------------------------------------ GAS
+    def gas_snapshot_set(self, gen: int, n_cards: np.ndarray, cap_per_gpu: np.ndarray,
+                         used: np.ndarray):
+        n_cards = np.ascontiguousarray(n_cards, dtype=np.int32)
+        cap = np.ascontiguousarray(cap_per_gpu, dtype=np.int64)
+        used = np.ascontiguousarray(used, dtype=np.int64)
+        n, k, q = used.shape
+        assert cap.shape == (n, q) and n_cards.shape == (n,)
+        self._check(self._l.pas_gas_snapshot_set(self._h, gen, n, k, q, _ptr(n_cards),
+                                                 _ptr(cap), _ptr(used)),
+                    "pas_gas_snapshot_set")
+        self.gas_shape = (n, k, q)
+
+    def gas_snapshot_set_device(self, gen: int, n_nodes: int, max_cards: int, n_res: int,
+                                n_cards_t, cap_t, used_t, stream=None):
+        self._check(self._l.pas_gas_snapshot_set_device(self._h, gen, n_nodes, max_cards, n_res,
+                                                        _dptr(n_cards_t), _dptr(cap_t),
+                                                        _dptr(used_t), _stream(stream)),
+                    "pas_gas_snapshot_set_device")
+        self.gas_shape = (n_nodes, max_cards, n_res)
+
+    def gas_fit(self, gen: int, req: np.ndarray, req_mask: np.ndarray, n_containers: np.ndarray,
+                i915_index: int) -> np.ndarray:
+        req = np.ascontiguousarray(req, dtype=np.int64)
+        p, c, q = req.shape
+        req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
+        n_containers = np.ascontiguousarray(n_containers, dtype=np.int32)
+        assert req_mask.shape == (p, c) and n_containers.shape == (p,)
+        out = np.zeros((p, self.gas_shape[0]), np.uint32)
+        rc = self._l.pas_gas_fit(self._h, gen, p, c, i915_index, _ptr(req), _ptr(req_mask),
+                                 _ptr(n_containers), _ptr(out))
+        self._check(rc, "pas_gas_fit")
+        return out
+
+    def gas_fit_device(self, gen: int, n_pods: int, max_containers: int, i915_index: int, req_t,
+                       mask_t, ncont_t, res_t, stream=None):
+        rc = self._l.pas_gas_fit_device(self._h, gen, n_pods, max_containers, i915_index,
+                                        _dptr(req_t), _dptr(mask_t), _dptr(ncont_t),
+                                        _dptr(res_t), _stream(stream))
+        self._check(rc, "pas_gas_fit_device")

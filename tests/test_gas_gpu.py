@@ -1,0 +1,118 @@
+"""GAS per-card first fit through libpas.so's HIP kernel, bit-exact against the oracle
+(card selections included) and the reference's golden vectors.  Marked gpu."""
+import numpy as np
+import pytest
+
+import pas_amd
+from pas_amd import workload as wl
+from helpers import decode_gas_word, golden
+from test_oracle_golden import commit_pod, gas_readme_case
+
+pytestmark = pytest.mark.gpu
+G = golden()
+_gen = [5000]
+
+
+def gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, i915):
+    _gen[0] += 1
+    ctx.gas_snapshot_set(_gen[0], n_cards, cap, used)
+    return ctx.gas_fit(_gen[0], req, mask, ncont, i915)
+
+
+def test_golden_g10_no_label(ctx):
+    res = gpu_fit(ctx, np.array([0, -1], np.int32), np.zeros((2, 1), np.int64),
+                  np.zeros((2, 1, 1), np.int64), np.zeros((1, 1, 1), np.int64),
+                  np.zeros((1, 1), np.uint32), np.array([1], np.int32), 0)
+    assert not decode_gas_word(res[0, 0])[0] and not decode_gas_word(res[0, 1])[0]
+    # checkResourceCapacity(need {foo:1}, capacity {}, used {}) == false (scheduler_test.go:122-131)
+    res = gpu_fit(ctx, np.array([1], np.int32), np.zeros((1, 1), np.int64),
+                  np.zeros((1, 1, 1), np.int64), np.ones((1, 1, 1), np.int64),
+                  np.array([[1]], np.uint32), np.array([1], np.int32), 0)
+    assert not decode_gas_word(res[0, 0])[0]
+
+
+def test_golden_g11_readme(ctx):
+    g = G["G11_gas_readme"]
+    for ex in (g["memory_example"], g["millicores_example"]):
+        kinds, cards, n_cards, cap, used, req, mask = gas_readme_case(ex)
+        for want in ex["want"]:
+            res = gpu_fit(ctx, n_cards, cap, used, req, mask, np.array([1], np.int32), 0)
+            fits, sel = decode_gas_word(res[0, 0])
+            assert fits == want["fits"]
+            if fits:
+                assert ",".join(cards[k] for k in sel) == want["annotation"]
+                commit_pod(used[0], req[0], mask[0], [sel])
+
+
+def random_gas(rng, n, k, q, p, c, extreme=False, i915=0):
+    n_cards = rng.integers(-1, k + 1, size=n).astype(np.int32)
+    cap = rng.integers(0, 1000, size=(n, q)).astype(np.int64)
+    cap[rng.random((n, q)) < 0.05] = 0
+    used = rng.integers(0, 1000, size=(n, k, q)).astype(np.int64)
+    req = rng.integers(0, 600, size=(p, c, q)).astype(np.int64)
+    col = max(i915, 0)
+    req[:, :, col] = rng.integers(0, 4, size=(p, c))
+    mask = rng.integers(0, 1 << q, size=(p, c)).astype(np.uint32)
+    ncont = rng.integers(0, c + 1, size=p).astype(np.int32)
+    if extreme:
+        big = np.int64(2**63 - 1)
+        used[rng.random((n, k, q)) < 0.05] = -5
+        used[rng.random((n, k, q)) < 0.05] = big - 3
+        cap[rng.random((n, q)) < 0.05] = big
+        req[rng.random((p, c, q)) < 0.05] = -2
+        req[rng.random((p, c, q)) < 0.03] = big
+    # keep within the packed 8-selection budget per pod
+    for pi in range(p):
+        while i915 >= 0 and sum(int(req[pi, ci, col]) for ci in range(ncont[pi])
+                                if (mask[pi, ci] >> col & 1) and req[pi, ci, col] > 0) > 8:
+            req[pi, rng.integers(0, c), col] = 0
+    return n_cards, cap, used, req, mask, ncont
+
+
+@pytest.mark.parametrize("q", [1, 2, 3, 4])
+@pytest.mark.parametrize("k", [1, 3, 8])
+def test_random_parity(ctx, oracle, q, k):
+    rng = np.random.default_rng(q * 100 + k)
+    for extreme in (False, True):
+        i915 = -1 if (extreme and q == 2) else (q - 1 if k == 3 else 0)
+        args = random_gas(rng, 777, k, q, 23, 4, extreme, i915)
+        got = gpu_fit(ctx, *args, i915)
+        want = oracle.gas_fit(*args, i915)
+        np.testing.assert_array_equal(got, want)
+
+
+def test_c3_shape_pod_sample(ctx, oracle):
+    # configs[2] node shape: 50k nodes x 8 cards x 3 kinds, on 64 pods (full oracle check)
+    snap = wl.make_gas_snapshot(50_000, seed=0xC3)
+    batch = wl.make_gas_batch(64, seed=0xC3)
+    got = gpu_fit(ctx, snap.n_cards, snap.cap, snap.used, batch.req, batch.req_mask,
+                  batch.n_containers, wl.I915)
+    want = oracle.gas_fit(snap.n_cards, snap.cap, snap.used, batch.req, batch.req_mask,
+                          batch.n_containers, wl.I915)
+    np.testing.assert_array_equal(got, want)
+    fit_frac = (got >> 31).mean()
+    assert 0.3 < fit_frac < 0.99
+
+
+def test_selection_capacity_error(ctx):
+    req = np.zeros((1, 2, 1), np.int64)
+    req[0, :, 0] = 5  # 10 selections
+    with pytest.raises(pas_amd.PasError) as e:
+        gpu_fit(ctx, np.array([8], np.int32), np.full((1, 1), 100, np.int64),
+                np.zeros((1, 8, 1), np.int64), req, np.ones((1, 2), np.uint32),
+                np.array([2], np.int32), 0)
+    assert e.value.code == -7  # PAS_ECAPACITY
+
+
+def test_same_card_reuse_and_container_accumulation(ctx, oracle):
+    # per-GPU i915 capacity 300 (shared-dev-num), so one card can take every selection;
+    # a second container sees the first one's usage (scheduler.go:317-319)
+    n_cards = np.array([2], np.int32)
+    cap = np.array([[300, 1000]], np.int64)
+    used = np.zeros((1, 2, 2), np.int64)
+    req = np.array([[[2, 800], [1, 300]]], np.int64)  # per GPU: [1, 400] x2, then [1, 300]
+    mask = np.array([[3, 3]], np.uint32)
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, np.array([2], np.int32), 0)
+    assert decode_gas_word(got[0, 0]) == (True, [0, 0, 1])
+    np.testing.assert_array_equal(got, oracle.gas_fit(n_cards, cap, used, req, mask,
+                                                      np.array([2], np.int32), 0))
