@@ -8,25 +8,27 @@
 //   prioritizeNodesForRule (:128-149) -> core.OrderedList (strategies/core/operator.go:30-42)
 //                                        over the candidates that have the metric
 //
-// Device formulation (snapshot orders built by tas_snapshot.hip):
-//   * rule -> range.  With the present values of metric m sorted ascending, the nodes
-//     satisfying EvaluateRule (operator.go:13-26) form one contiguous range:
-//       LessThan  t: [0, lower_bound(t*1000))     GreaterThan t: [upper_bound(t*1000), cnt)
-//       Equals    t: [lower_bound, upper_bound)
-//     (t*1000 saturates: above int64 every present value is LessThan, none is greater
-//     or equal; symmetric below).  tas_ranges_kernel computes them for the batch.
-//   * filter.  One workgroup per pod keeps a node-space pass bitmap in LDS (N bits),
-//     initialised from the candidates, and clears the bit of every node listed in any
-//     of the pod's rule ranges (perm_asc entries, read coalesced).  The bitmap is the
-//     FilterResult (pass = candidate AND NOT violated).
-//   * prioritize.  The order for the pod's scheduleonmetric rule (asc / desc / index) is
-//     a fixed permutation of the metric's present nodes.  Every non-passing node is
-//     mapped through that order's rank array into a "drop" bitmap over sorted positions
-//     (LDS), the per-wave drop counts give each wave its output offset, and each wave
-//     streams its slice of the permutation, writing kept entries with mbcnt compaction.
-//     HBM traffic per pod: N/8 B of pass bitmap + 4 B per listed node written, the
-//     permutation read (L2/MALL-resident, shared by all pods with the same metric/order).
+// Device formulation (snapshot orders built once per snapshot by tas_snapshot.hip):
+//   K ranges  rule -> range.  With the present values of metric m sorted ascending, the
+//             nodes satisfying EvaluateRule (operator.go:13-26) form one contiguous range:
+//               LessThan t: [0, lower_bound(t*1000))   GreaterThan t: [upper_bound(t*1000), cnt)
+//               Equals   t: [lower_bound, upper_bound)
+//             (t*1000 saturates: above int64 every present value is LessThan, none is
+//             greater or equal; symmetric below).
+//   K group   pods are bucketed by their prioritize order (metric, asc/desc/index), so
+//             pods sharing a permutation / rank array run back to back (L2 locality).
+//   K filter  one workgroup per pod, XCD-aware over the bucketed pod list: a node-space
+//             pass bitmap in LDS (candidates, then every node of every rule range cleared;
+//             this is the FilterResult), then every non-passing node mapped through the
+//             order's rank array into a "drop" bitmap over order positions, written to HBM
+//             with the output base of each 1024-position segment.
+//   K emit    row-major over the bucketed pods: each wave compacts one 1024-position
+//             segment of the pod's permutation by its drop bits (mbcnt) and writes it with
+//             16-byte stores; concurrent waves cover contiguous row spans, so the path is
+//             bound by HBM writes of the ordered lists.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 
 #include "pas_internal.h"
 
@@ -36,29 +38,14 @@ namespace {
 constexpr int kTpb = 256;
 constexpr int kWaves = kTpb / 64;
 constexpr int kRuleChunk = 64;
-// LDS words reserved in front of the two bitmaps (rule chunk tables + wave counts),
-// a multiple of 4 so the bitmaps stay 16-byte aligned (cdna_hip_programming G17).
+constexpr int kSegWords = 16;               // 64-bit drop words per emit segment
+constexpr int kSegPos = kSegWords * 64;     // 1024 order positions per emit segment
+constexpr int kGroupTpb = 1024;
+constexpr int kMaxGroupMetrics = 4096;      // 3 * M + 1 buckets in LDS for K group
+// LDS words reserved in front of the two bitmaps (rule chunk tables, scan partials), a
+// multiple of 4 so the bitmaps stay 16-byte aligned (cdna_hip_programming G17).
 constexpr int kMiscWords = 4 * kRuleChunk + 16;
-
-struct EvalParams {
-  int32_t N;
-  int32_t M;
-  int32_t W32;   // ceil(N / 32)
-  int32_t W32p;  // 2 * W64: words per LDS bitmap
-  int32_t W64;
-  uint32_t flags;
-  const int32_t* rule_off;
-  const int2* ranges;
-  const pas_rule* rules;
-  const pas_rule* prio;
-  const uint64_t* cand;
-  const int32_t* perm;   // [3][M][N]
-  const uint32_t* rank;  // [3][M][N]
-  const int32_t* cnt;    // [M]
-  uint64_t* pass_out;
-  int32_t* order_out;
-  int32_t* order_len;
-};
+static_assert(kMiscWords >= kTpb, "scan partials live in the misc words");
 
 __device__ __forceinline__ uint32_t tail_mask32(int32_t w, int32_t n) {
   const int32_t lo = w * 32;
@@ -74,7 +61,6 @@ __device__ __forceinline__ uint64_t tail_mask64(int32_t c, int32_t n) {
   return (1ull << (n - lo)) - 1ull;
 }
 
-// Binary search bounds over ascending sorted values.
 __device__ __forceinline__ int32_t lower_bound_i64(const int64_t* __restrict__ a, int32_t n,
                                                    int64_t x) {
   int32_t lo = 0, hi = n;
@@ -95,8 +81,8 @@ __device__ __forceinline__ int32_t upper_bound_i64(const int64_t* __restrict__ a
   return lo;
 }
 
-// target * 1000 with saturation: sat = +1 (above every int64 milli value), -1 (below
-// every value) or 0 with *tm exact.
+// target * 1000 with saturation: +1 (above every int64 milli value), -1 (below every
+// value) or 0 with *tm exact.
 __device__ __forceinline__ int target_milli(int64_t t, int64_t* tm) {
   constexpr int64_t kMax = INT64_MAX / 1000;
   constexpr int64_t kMin = INT64_MIN / 1000;
@@ -106,7 +92,39 @@ __device__ __forceinline__ int target_milli(int64_t t, int64_t* tm) {
   return 0;
 }
 
-// One thread per rule: its violating range in the metric's ascending order.
+__device__ __forceinline__ int order_of(int32_t op) {
+  return op == PAS_OP_GREATER_THAN ? kOrderDesc : op == PAS_OP_LESS_THAN ? kOrderAsc : kOrderIndex;
+}
+
+// Exclusive scan of a[0..n) in LDS by the whole block; returns the total.
+// `partial` holds blockDim.x ints of LDS.
+__device__ int32_t block_exclusive_scan(int32_t* a, int32_t n, int32_t* partial) {
+  const int T = blockDim.x, tid = threadIdx.x;
+  const int32_t per = (n + T - 1) / T;
+  const int32_t lo = min(n, tid * per), hi = min(n, lo + per);
+  int32_t s = 0;
+  for (int32_t i = lo; i < hi; ++i) s += a[i];
+  partial[tid] = s;
+  __syncthreads();
+  for (int off = 1; off < T; off <<= 1) {
+    const int32_t v = tid >= off ? partial[tid - off] : 0;
+    __syncthreads();
+    partial[tid] += v;
+    __syncthreads();
+  }
+  int32_t run = partial[tid] - s;
+  const int32_t total = partial[T - 1];
+  for (int32_t i = lo; i < hi; ++i) {
+    const int32_t t = a[i];
+    a[i] = run;
+    run += t;
+  }
+  __syncthreads();
+  return total;
+}
+
+// ---------------------------------------------------------------------------- ranges
+
 __global__ void tas_ranges_kernel(int32_t n_rules, const pas_rule* __restrict__ rules,
                                   const int32_t* __restrict__ cnt,
                                   const int64_t* __restrict__ sorted, int32_t N, int32_t M,
@@ -131,19 +149,88 @@ __global__ void tas_ranges_kernel(int32_t n_rules, const pas_rule* __restrict__ 
   ranges[r] = out;
 }
 
-__global__ __launch_bounds__(kTpb) void tas_eval_kernel(EvalParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  int32_t* s_pref = reinterpret_cast<int32_t*>(lds);          // [kRuleChunk + 1]
-  int32_t* s_lo = s_pref + (kRuleChunk + 4);                  // [kRuleChunk]
-  int32_t* s_m = s_lo + kRuleChunk;                           // [kRuleChunk]
-  int32_t* s_wdrop = s_m + kRuleChunk;                        // [kWaves]
-  uint32_t* pass = lds + kMiscWords;                          // [W32p]
-  uint32_t* drop = pass + P.W32p;                             // [W32p]
+// ---------------------------------------------------------------------------- group
 
-  const int32_t pod = blockIdx.x;
+struct GroupParams {
+  int32_t P, M, N;
+  uint32_t flags;
+  const pas_rule* prio;
+  const int32_t* cnt;
+  int32_t* pod_list;     // [P]   pods bucketed by key, bucket G (no list) last
+  int32_t* group_start;  // [G+2]
+};
+
+__device__ __forceinline__ int32_t pod_key(const GroupParams& g, int32_t p) {
+  const int32_t G = 3 * g.M;
+  if (!(g.flags & PAS_TAS_PRIORITIZE)) return G;
+  const pas_rule r = g.prio[p];
+  if (r.metric < 0 || r.metric >= g.M || g.cnt[r.metric] == 0) return G;
+  return order_of(r.op) * g.M + r.metric;
+}
+
+// One block: counting sort of the pods by bucket.
+__global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
+  extern __shared__ __attribute__((aligned(16))) int32_t sh[];
+  const int32_t G = 3 * g.M;
+  int32_t* partial = sh;                  // [kGroupTpb]
+  int32_t* hist = sh + kGroupTpb;         // [G + 1]
   const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
+  for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
+  __syncthreads();
+  for (int32_t p = tid; p < g.P; p += kGroupTpb) atomicAdd(&hist[pod_key(g, p)], 1);
+  __syncthreads();
+  block_exclusive_scan(hist, G + 1, partial);
+  for (int32_t i = tid; i <= G; i += kGroupTpb) g.group_start[i] = hist[i];
+  if (tid == 0) g.group_start[G + 1] = g.P;
+  __syncthreads();
+  for (int32_t p = tid; p < g.P; p += kGroupTpb) {
+    const int32_t pos = atomicAdd(&hist[pod_key(g, p)], 1);  // order inside a bucket is free
+    g.pod_list[pos] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------- filter
+
+struct FilterParams {
+  int32_t N, M, P;
+  int32_t W32;   // ceil(N / 32)
+  int32_t W32p;  // 2 * W64: words per LDS bitmap
+  int32_t W64;
+  int32_t D64;   // drop row stride in 64-bit words (multiple of kSegWords)
+  int32_t S;     // seg_base row stride (= D64 / kSegWords)
+  uint32_t flags;
+  const int32_t* rule_off;
+  const int2* ranges;
+  const pas_rule* rules;
+  const pas_rule* prio;
+  const uint64_t* cand;
+  const int32_t* perm;   // [3][M][N]
+  const uint32_t* rank;  // [3][M][N]
+  const int32_t* cnt;    // [M]
+  const int32_t* pod_list;
+  uint64_t* pass_out;    // [P][W64]
+  uint64_t* drop;        // [P][D64]
+  int32_t* seg_base;     // [P][S]
+  int32_t* order_len;    // [P]
+};
+
+__global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  int32_t* s_pref = reinterpret_cast<int32_t*>(lds);  // [kRuleChunk + 1]
+  int32_t* s_lo = s_pref + (kRuleChunk + 4);          // [kRuleChunk]
+  int32_t* s_m = s_lo + kRuleChunk;                   // [kRuleChunk]
+  int32_t* s_partial = reinterpret_cast<int32_t*>(lds);  // [kTpb], after the rule phase
+  uint32_t* pass = lds + kMiscWords;                  // [W32p]
+  uint32_t* drop = pass + P.W32p;                     // [W32p]
+
+  // XCD-aware placement: blocks b and b+8 share an XCD (MI355X_MICROARCH.md, Workgroup
+  // dispatch), so give each XCD a contiguous run of the bucketed pod list; pods of a
+  // bucket then hit the same rank array in that XCD's L2.  Speed only, never correctness.
+  const int32_t nb = gridDim.x, b = blockIdx.x;
+  const int32_t xcd = b & 7, per_xcd = nb >> 3, rem = nb & 7;
+  const int32_t pos = xcd * per_xcd + min(xcd, rem) + (b >> 3);
+  const int32_t pod = P.pod_list[pos];
+  const int tid = threadIdx.x;
   const int32_t N = P.N;
 
   // ---- candidates -> pass bitmap (args.Nodes.Items, telemetryscheduler.go:204) ----
@@ -155,7 +242,7 @@ __global__ __launch_bounds__(kTpb) void tas_eval_kernel(EvalParams P) {
   }
   __syncthreads();
 
-  // ---- dontschedule.Violated: clear every node in any rule range ----
+  // ---- dontschedule.Violated: clear every node of every rule range ----
   if (P.flags & PAS_TAS_FILTER) {
     const int32_t r0 = P.rule_off[pod], r1 = P.rule_off[pod + 1];
     const int32_t* perm_asc = P.perm + (int64_t)kOrderAsc * P.M * N;
@@ -201,7 +288,7 @@ __global__ __launch_bounds__(kTpb) void tas_eval_kernel(EvalParams P) {
 
   if (!(P.flags & PAS_TAS_PRIORITIZE)) return;
 
-  // ---- prioritizeNodesForRule over the candidates that passed ----
+  // ---- prioritizeNodesForRule: drop bitmap over the order's positions ----
   const pas_rule pr = P.prio[pod];
   const int32_t m0 = pr.metric;
   const int32_t cnt0 = (m0 >= 0 && m0 < P.M) ? P.cnt[m0] : 0;
@@ -209,20 +296,16 @@ __global__ __launch_bounds__(kTpb) void tas_eval_kernel(EvalParams P) {
     if (tid == 0) P.order_len[pod] = 0;
     return;
   }
-  const int order = pr.op == PAS_OP_GREATER_THAN ? kOrderDesc
-                    : pr.op == PAS_OP_LESS_THAN  ? kOrderAsc
-                                                 : kOrderIndex;
-  const int64_t col = ((int64_t)order * P.M + m0) * N;
-  const int32_t* __restrict__ pm = P.perm + col;
+  const int64_t col = ((int64_t)order_of(pr.op) * P.M + m0) * N;
   const uint32_t* __restrict__ rk = P.rank + col;
-  const int32_t C64 = (cnt0 + 63) / 64;
-  for (int32_t w = tid; w < 2 * C64; w += kTpb) drop[w] = 0u;
+  const int32_t n_seg = (cnt0 + kSegPos - 1) / kSegPos;
+  const int32_t DW = n_seg * kSegWords * 2;  // 32-bit drop words written
+  for (int32_t w = tid; w < DW; w += kTpb) drop[w] = 0u;
   __syncthreads();
 
-  // Map every non-passing node to its position in the order (4 gathers in flight).
   for (int32_t w = tid; w < P.W32; w += kTpb) {
     uint32_t z = ~pass[w] & tail_mask32(w, N);
-    while (z) {
+    while (z) {  // 4 rank gathers in flight per thread
       int32_t n0 = -1, n1 = -1, n2 = -1, n3 = -1;
       n0 = w * 32 + __ffs(z) - 1; z &= z - 1;
       if (z) { n1 = w * 32 + __ffs(z) - 1; z &= z - 1; }
@@ -240,42 +323,113 @@ __global__ __launch_bounds__(kTpb) void tas_eval_kernel(EvalParams P) {
   }
   __syncthreads();
 
-  // Each wave owns a contiguous run of 64-position chunks of the order.
-  const int32_t per = (C64 + kWaves - 1) / kWaves;
-  const int32_t c_begin = min(C64, wave * per);
-  const int32_t c_end = min(C64, c_begin + per);
+  // drop row -> HBM; kept count per segment -> output base of each segment
   const uint64_t* drop64 = reinterpret_cast<const uint64_t*>(drop);
-  int32_t dropped = 0;
-  for (int32_t c = c_begin + lane; c < c_end; c += 64)
-    dropped += __popcll(drop64[c] & tail_mask64(c, cnt0));
+  uint64_t* drow = P.drop + (int64_t)pod * P.D64;
+  for (int32_t w = tid; w < n_seg * kSegWords; w += kTpb) drow[w] = drop64[w];
+  int32_t* segk = reinterpret_cast<int32_t*>(pass);  // pass is dead now
+  for (int32_t sgi = tid; sgi < n_seg; sgi += kTpb) {
+    int32_t kept = 0;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) dropped += __shfl_xor(dropped, off, 64);
-  if (lane == 0) s_wdrop[wave] = dropped;
+    for (int j = 0; j < kSegWords; ++j) {
+      const int32_t c = sgi * kSegWords + j;
+      kept += __popcll(~drop64[c] & tail_mask64(c, cnt0));
+    }
+    segk[sgi] = kept;
+  }
   __syncthreads();
-  int32_t drops_before = 0, drops_total = 0;
-#pragma unroll
-  for (int i = 0; i < kWaves; ++i) {
-    drops_total += s_wdrop[i];
-    if (i < wave) drops_before += s_wdrop[i];
-  }
-  int32_t* __restrict__ out = P.order_out + (int64_t)pod * N;
-  int32_t base = c_begin * 64 - drops_before;
-#pragma unroll 4
-  for (int32_t c = c_begin; c < c_end; ++c) {
-    const int32_t k = c * 64 + lane;
-    const uint64_t keep = ~drop64[c] & tail_mask64(c, cnt0);
-    const int32_t node = k < cnt0 ? pm[k] : 0;
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-        (uint32_t)(keep >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
-    if ((keep >> lane) & 1ull) out[base + (int32_t)below] = node;
-    base += __popcll(keep);
-  }
-  if (tid == 0) P.order_len[pod] = cnt0 - drops_total;
+  const int32_t total = block_exclusive_scan(segk, n_seg, s_partial);
+  int32_t* sb = P.seg_base + (int64_t)pod * P.S;
+  for (int32_t sgi = tid; sgi < n_seg; sgi += kTpb) sb[sgi] = segk[sgi];
+  if (tid == 0) P.order_len[pod] = total;
 }
 
-// Deschedule sweep: one wave per 64-node word, strategies x rules in the wave loop.
-// deschedule.Strategy.Violated (deschedule/strategy.go:31-50) per registered strategy,
-// as nodeStatusForStrategy does (deschedule/enforce.go:154-164).
+// ---------------------------------------------------------------------------- emit
+
+constexpr int kEmitSegsPerBlock = kWaves;                       // 4 x 1024 positions
+constexpr int kStageWords = ((kSegPos + 3 + 255) / 256) * 256;  // 5 x 256 (unrolled reads)
+
+// Row-major emit: block b covers 4 consecutive 1024-position segments of one pod row, pods
+// in bucket order.  Concurrent blocks therefore write a few contiguous row spans (the
+// DRAM-friendly pattern a linear fill has), and the pods of a bucket, which share one
+// permutation, run back to back so the permutation segments are L2 hits.  Each wave does
+// one load round (its permutation segment, the pod's 16 drop words, the segment base),
+// compacts the kept entries into an LDS stage aligned to the destination's 16-byte grid and
+// writes them with dwordx4 stores (dword stores for the two partial end chunks).
+// kAblate (diagnostic timing builds only, PAS_EMIT_ABLATE; outputs wrong): 1 = no stores.
+template <int kAblate>
+__global__ __launch_bounds__(kTpb) void tas_emit_kernel(
+    int32_t N, int32_t M, int32_t D64, int32_t S, int32_t blocks_per_pod,
+    const int32_t* __restrict__ perm, const int32_t* __restrict__ cnt,
+    const pas_rule* __restrict__ prio, const int32_t* __restrict__ pod_list,
+    const int32_t* __restrict__ group_start, int32_t G, const uint64_t* __restrict__ drop,
+    const int32_t* __restrict__ seg_base, int32_t* __restrict__ order_out) {
+  __shared__ __attribute__((aligned(16))) int32_t stage_all[kWaves][kStageWords];
+  const int wave = threadIdx.x >> 6;
+  int32_t* stage = stage_all[wave];
+  const int lane = threadIdx.x & 63;
+  const int32_t pidx = blockIdx.x / blocks_per_pod;
+  if (pidx >= group_start[G]) return;  // pods without a list sit after the buckets
+  const int32_t s = (blockIdx.x % blocks_per_pod) * kEmitSegsPerBlock + wave;
+  const int32_t pod = pod_list[pidx];
+  const pas_rule pr = prio[pod];
+  const int32_t m0 = pr.metric;
+  const int32_t cnt0 = cnt[m0];
+  if (s * kSegPos >= cnt0) return;
+  const int32_t order = order_of(pr.op);
+  const int32_t* __restrict__ pm = perm + ((int64_t)order * M + m0) * N;
+  const int32_t k0 = s * kSegPos + lane;
+  int32_t node[kSegWords];
+#pragma unroll
+  for (int j = 0; j < kSegWords; ++j) {
+    const int32_t kk = k0 + j * 64;
+    node[j] = kk < cnt0 ? pm[kk] : 0;
+  }
+  const uint64_t* __restrict__ dw = drop + (int64_t)pod * D64 + s * kSegWords;
+  uint64_t d[kSegWords];
+#pragma unroll
+  for (int j = 0; j < kSegWords; ++j) d[j] = dw[j];
+  const int32_t base = seg_base[(int64_t)pod * S + s];
+  const bool full = (s + 1) * kSegPos <= cnt0;
+  const int64_t gdst = (int64_t)pod * N + base;  // element index of the first entry
+  const int32_t a = (int32_t)(gdst & 3);
+  int32_t k = a;
+#pragma unroll
+  for (int j = 0; j < kSegWords; ++j) {
+    const uint64_t keep = ~d[j] & (full ? ~0ull : tail_mask64(s * kSegWords + j, cnt0));
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+        (uint32_t)(keep >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
+    if ((keep >> lane) & 1ull) stage[k + (int32_t)below] = node[j];
+    k += __popcll(keep);
+  }
+  __builtin_amdgcn_wave_barrier();
+  int32_t* __restrict__ out = order_out + (gdst - a);  // 16-byte aligned
+  constexpr int kChunkIters = kStageWords / 256;
+  int4 v[kChunkIters];
+#pragma unroll
+  for (int it = 0; it < kChunkIters; ++it)
+    v[it] = *reinterpret_cast<const int4*>(stage + (lane + it * 64) * 4);
+#pragma unroll
+  for (int it = 0; it < kChunkIters; ++it) {
+    const int32_t e0 = (lane + it * 64) * 4;
+    if (kAblate == 1 && gdst >= 0) {
+      asm volatile("" ::"v"(v[it].x), "v"(v[it].y), "v"(v[it].z), "v"(v[it].w));
+    } else if (e0 >= a && e0 + 4 <= k) {
+      *reinterpret_cast<int4*>(out + e0) = v[it];
+    } else if (e0 < k && e0 + 4 > a) {  // one of the two partial end chunks
+      if (e0 + 0 >= a && e0 + 0 < k) out[e0 + 0] = v[it].x;
+      if (e0 + 1 >= a && e0 + 1 < k) out[e0 + 1] = v[it].y;
+      if (e0 + 2 >= a && e0 + 2 < k) out[e0 + 2] = v[it].z;
+      if (e0 + 3 >= a && e0 + 3 < k) out[e0 + 3] = v[it].w;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- deschedule
+
+// One wave per 64-node word, strategies x rules in the wave loop: deschedule.Strategy.
+// Violated (deschedule/strategy.go:31-50) per registered strategy, as
+// nodeStatusForStrategy does (deschedule/enforce.go:154-164).
 __global__ __launch_bounds__(kTpb) void tas_violations_kernel(
     int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
     const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
@@ -305,6 +459,8 @@ __global__ __launch_bounds__(kTpb) void tas_violations_kernel(
   }
 }
 
+size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
+
 }  // namespace
 
 int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
@@ -314,12 +470,28 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   const TasSnapshot& t = ctx->tas;
   const int32_t N = t.n_nodes, M = t.n_metrics;
   const int32_t W64 = (int32_t)w64(N);
-  const size_t lds_bytes = sizeof(uint32_t) * ((size_t)kMiscWords + 4 * (size_t)W64);
-  if (lds_bytes > 160 * 1024)
+  const int32_t S = (int32_t)((N + kSegPos - 1) / kSegPos);
+  const int32_t D64 = S * kSegWords;
+  const int32_t G = 3 * M;
+  // LDS: misc | pass bitmap (2*W64 words) | drop bitmap (S segments x 32 words)
+  const size_t filter_lds =
+      sizeof(uint32_t) * ((size_t)kMiscWords + 2 * (size_t)W64 + (size_t)S * kSegWords * 2);
+  if (filter_lds > 160 * 1024)
     return set_error(ctx, PAS_ECAPACITY,
                      "pas_tas_eval: n_nodes too large for the LDS bitmaps (max ~620k nodes)");
-  // rule ranges live in a context-owned buffer that grows with the rule count
-  const size_t need = sizeof(int2) * (size_t)std::max(n_rules, 1);
+  if (M > kMaxGroupMetrics)
+    return set_error(ctx, PAS_ECAPACITY, "pas_tas_eval: more than 4096 metric columns");
+  const bool prio = (flags & PAS_TAS_PRIORITIZE) != 0;
+
+  // scratch: ranges | pod_list | group_start | seg_base | drop
+  const size_t sizes[5] = {
+      align256(sizeof(int2) * (size_t)std::max(n_rules, 1)),
+      align256(sizeof(int32_t) * (size_t)n_pods),
+      align256(sizeof(int32_t) * (size_t)(G + 2)),
+      prio ? align256(sizeof(int32_t) * (size_t)n_pods * S) : 0,
+      prio ? align256(sizeof(uint64_t) * (size_t)n_pods * D64) : 0};
+  size_t need = 0;
+  for (size_t b : sizes) need += b;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -327,10 +499,21 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
       ctx->aux = nullptr;
       ctx->aux_bytes = 0;
     }
-    PAS_HIP(ctx, hipMalloc(&ctx->aux, need * 2));
-    ctx->aux_bytes = need * 2;
+    PAS_HIP(ctx, hipMalloc(&ctx->aux, need));
+    ctx->aux_bytes = need;
   }
-  int2* d_ranges = static_cast<int2*>(ctx->aux);
+  char* cur = static_cast<char*>(ctx->aux);
+  char* parts[5];
+  for (int i = 0; i < 5; ++i) {
+    parts[i] = cur;
+    cur += sizes[i];
+  }
+  int2* d_ranges = reinterpret_cast<int2*>(parts[0]);
+  int32_t* d_list = reinterpret_cast<int32_t*>(parts[1]);
+  int32_t* d_gs = reinterpret_cast<int32_t*>(parts[2]);
+  int32_t* d_sb = reinterpret_cast<int32_t*>(parts[3]);
+  uint64_t* d_drop = reinterpret_cast<uint64_t*>(parts[4]);
+
   TimedLaunch tl;
   if ((flags & PAS_TAS_FILTER) && n_rules > 0) {
     timing_begin(ctx, s, PAS_K_TAS_RANGES, &tl);
@@ -339,32 +522,70 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     timing_end(ctx, s, &tl);
     PAS_HIP(ctx, hipGetLastError());
   }
-  EvalParams p;
-  p.N = N;
-  p.M = M;
-  p.W32 = (int32_t)w32(N);
-  p.W32p = 2 * W64;
-  p.W64 = W64;
-  p.flags = flags;
-  p.rule_off = d_rule_off;
-  p.ranges = d_ranges;
-  p.rules = d_rules;
-  p.prio = d_prio;
-  p.cand = d_cand;
-  p.perm = t.perm;
-  p.rank = t.rank;
-  p.cnt = t.cnt;
-  p.pass_out = d_pass;
-  p.order_out = d_order;
-  p.order_len = d_len;
-  if (lds_bytes > 64 * 1024)
-    PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_eval_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds_bytes));
-  timing_begin(ctx, s, PAS_K_TAS_EVAL, &tl);
-  tas_eval_kernel<<<n_pods, kTpb, lds_bytes, s>>>(p);
+
+  GroupParams gp{n_pods, M, N, flags, d_prio, t.cnt, d_list, d_gs};
+  const size_t group_lds = sizeof(int32_t) * ((size_t)kGroupTpb + G + 1);
+  if (group_lds > 64 * 1024)
+    PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_group_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_lds));
+  timing_begin(ctx, s, PAS_K_TAS_GROUP, &tl);
+  tas_group_kernel<<<1, kGroupTpb, group_lds, s>>>(gp);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
+
+  FilterParams fp;
+  fp.N = N;
+  fp.M = M;
+  fp.P = n_pods;
+  fp.W32 = (int32_t)w32(N);
+  fp.W32p = 2 * W64;
+  fp.W64 = W64;
+  fp.D64 = D64;
+  fp.S = S;
+  fp.flags = flags;
+  fp.rule_off = d_rule_off;
+  fp.ranges = d_ranges;
+  fp.rules = d_rules;
+  fp.prio = d_prio;
+  fp.cand = d_cand;
+  fp.perm = t.perm;
+  fp.rank = t.rank;
+  fp.cnt = t.cnt;
+  fp.pod_list = d_list;
+  fp.pass_out = d_pass;
+  fp.drop = d_drop;
+  fp.seg_base = d_sb;
+  fp.order_len = d_len;
+  if (filter_lds > 64 * 1024)
+    PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_filter_kernel),
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)filter_lds));
+  timing_begin(ctx, s, PAS_K_TAS_FILTER, &tl);
+  tas_filter_kernel<<<n_pods, kTpb, filter_lds, s>>>(fp);
+  timing_end(ctx, s, &tl);
+  PAS_HIP(ctx, hipGetLastError());
+
+  if (prio) {
+    const int32_t bpp = (S + kEmitSegsPerBlock - 1) / kEmitSegsPerBlock;
+    const int64_t blocks = (int64_t)n_pods * bpp;
+    if (blocks > 0) {
+      timing_begin(ctx, s, PAS_K_TAS_EMIT, &tl);
+      static const int ablate = [] {
+        const char* e = std::getenv("PAS_EMIT_ABLATE");
+        return e ? std::atoi(e) : 0;
+      }();
+      if (ablate == 1)
+        tas_emit_kernel<1><<<(unsigned)blocks, kTpb, 0, s>>>(N, M, D64, S, bpp, t.perm, t.cnt,
+                                                             d_prio, d_list, d_gs, G, d_drop,
+                                                             d_sb, d_order);
+      else
+        tas_emit_kernel<0><<<(unsigned)blocks, kTpb, 0, s>>>(N, M, D64, S, bpp, t.perm, t.cnt,
+                                                             d_prio, d_list, d_gs, G, d_drop,
+                                                             d_sb, d_order);
+      timing_end(ctx, s, &tl);
+      PAS_HIP(ctx, hipGetLastError());
+    }
+  }
   return PAS_OK;
 }
 

@@ -46,16 +46,20 @@ PAS_GAS_MAX_RES = 4
 PAS_GAS_MAX_SELECTIONS = 8
 
 PAS_K_TAS_RANGES = 0
-PAS_K_TAS_EVAL = 1
+PAS_K_TAS_FILTER = 1
 PAS_K_TAS_VIOLATIONS = 2
 PAS_K_GAS_PREP = 3
 PAS_K_GAS_FIT = 4
+PAS_K_TAS_GROUP = 5
+PAS_K_TAS_EMIT = 6
 KERNEL_NAMES = {
     PAS_K_TAS_RANGES: "tas_ranges_kernel",
-    PAS_K_TAS_EVAL: "tas_eval_kernel",
+    PAS_K_TAS_FILTER: "tas_filter_kernel",
     PAS_K_TAS_VIOLATIONS: "tas_violations_kernel",
     PAS_K_GAS_PREP: "gas_prep_kernel",
     PAS_K_GAS_FIT: "gas_fit_kernel",
+    PAS_K_TAS_GROUP: "tas_group_kernel",
+    PAS_K_TAS_EMIT: "tas_emit_kernel",
 }
 
 
