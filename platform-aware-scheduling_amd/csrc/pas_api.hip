@@ -248,6 +248,10 @@ int pas_create(const pas_config* cfg, pas_ctx** out) {
     return PAS_EDEVICE;
   }
   ctx->stream = ctx->own_stream;
+  int n_cu = 0;
+  if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+      n_cu > 0)
+    ctx->n_cu = n_cu;
   *out = ctx;
   return PAS_OK;
 }

@@ -72,6 +72,7 @@ struct TimedLaunch {
 
 struct pas_ctx {
   int device = 0;
+  int n_cu = 256;  // compute units of the device (persistent grids)
   hipStream_t own_stream = nullptr;
   hipStream_t stream = nullptr;
   std::string err;

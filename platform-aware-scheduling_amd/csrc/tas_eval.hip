@@ -22,10 +22,10 @@
 //             this is the FilterResult), then every non-passing node mapped through the
 //             order's rank array into a "drop" bitmap over order positions, written to HBM
 //             with the output base of each 1024-position segment.
-//   K emit    row-major over the bucketed pods: each wave compacts one 1024-position
-//             segment of the pod's permutation by its drop bits (mbcnt) and writes it with
-//             16-byte stores; concurrent waves cover contiguous row spans, so the path is
-//             bound by HBM writes of the ordered lists.
+//   K emit    one wave per (bucket, 1024-position segment): the permutation segment is
+//             read ONCE into registers and written, compacted by each pod's drop bits
+//             (mbcnt), for every pod of the bucket, with 16-byte non-temporal stores.  The
+//             path is therefore bound by the HBM writes of the ordered lists (§8(d)).
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
@@ -158,6 +158,9 @@ struct GroupParams {
   const int32_t* cnt;
   int32_t* pod_list;     // [P]   pods bucketed by key, bucket G (no list) last
   int32_t* group_start;  // [G+2]
+  int32_t* seg_start;    // [G+1] first emit segment of each bucket
+  int32_t* seg_group;    // [max_segs] bucket of each emit segment, -1 past the last
+  int32_t max_segs;
 };
 
 __device__ __forceinline__ int32_t pod_key(const GroupParams& g, int32_t p) {
@@ -168,7 +171,7 @@ __device__ __forceinline__ int32_t pod_key(const GroupParams& g, int32_t p) {
   return order_of(r.op) * g.M + r.metric;
 }
 
-// One block: counting sort of the pods by bucket.
+// One block: counting sort of the pods by bucket + emit-segment table per bucket.
 __global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
   extern __shared__ __attribute__((aligned(16))) int32_t sh[];
   const int32_t G = 3 * g.M;
@@ -187,6 +190,22 @@ __global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
     const int32_t pos = atomicAdd(&hist[pod_key(g, p)], 1);  // order inside a bucket is free
     g.pod_list[pos] = p;
   }
+  __syncthreads();
+  // hist[i] now holds the end of bucket i: emit segments per non-empty bucket
+  for (int32_t i = tid; i < G; i += kGroupTpb) {
+    const int32_t begin = g.group_start[i];
+    const int32_t c = g.cnt[i % g.M];
+    hist[i] = hist[i] > begin ? (c + kSegPos - 1) / kSegPos : 0;
+  }
+  __syncthreads();
+  const int32_t total = block_exclusive_scan(hist, G, partial);
+  for (int32_t i = tid; i < G; i += kGroupTpb) g.seg_start[i] = hist[i];
+  if (tid == 0) g.seg_start[G] = total;
+  for (int32_t i = tid; i < G; i += kGroupTpb) {
+    const int32_t end = i + 1 < G ? hist[i + 1] : total;
+    for (int32_t k = hist[i]; k < end; ++k) g.seg_group[k] = i;
+  }
+  for (int32_t k = total + tid; k < g.max_segs; k += kGroupTpb) g.seg_group[k] = -1;
 }
 
 // ---------------------------------------------------------------------------- filter
@@ -212,6 +231,7 @@ struct FilterParams {
   uint64_t* drop;        // [P][D64]
   int32_t* seg_base;     // [P][S]
   int32_t* order_len;    // [P]
+  int4* desc;            // [P] per bucketed position: {pod, order*M + m0, cnt0, n_seg}
 };
 
 __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
@@ -242,7 +262,28 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
   }
   __syncthreads();
 
-  // ---- dontschedule.Violated: clear every node of every rule range ----
+  // ---- prioritize setup: the order whose positions the drop bitmap indexes ----
+  int32_t cnt0 = 0, n_seg = 0;
+  const uint32_t* __restrict__ rk = nullptr;
+  if (P.flags & PAS_TAS_PRIORITIZE) {
+    const pas_rule pr = P.prio[pod];
+    const int32_t m0 = pr.metric;
+    cnt0 = (m0 >= 0 && m0 < P.M) ? P.cnt[m0] : 0;
+    if (cnt0 > 0) {
+      const int32_t ocol = order_of(pr.op) * P.M + m0;
+      rk = P.rank + (int64_t)ocol * N;
+      n_seg = (cnt0 + kSegPos - 1) / kSegPos;
+      if (tid == 0) P.desc[pos] = make_int4(pod, ocol, cnt0, n_seg);
+      for (int32_t w = tid; w < n_seg * kSegWords * 2; w += kTpb) drop[w] = 0u;
+    } else if (tid == 0) {
+      P.order_len[pod] = 0;  // no rule / ReadMetric error -> empty HostPriorityList (:92-96)
+    }
+    __syncthreads();
+  }
+  const bool has_list = rk != nullptr;
+
+  // ---- dontschedule.Violated: every node of every rule range fails the filter and, when
+  //      the pod has a prioritize list, is dropped at its rank in that order ----
   if (P.flags & PAS_TAS_FILTER) {
     const int32_t r0 = P.rule_off[pod], r1 = P.rule_off[pod + 1];
     const int32_t* perm_asc = P.perm + (int64_t)kOrderAsc * P.M * N;
@@ -263,7 +304,7 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
       __syncthreads();
       const int32_t total = s_pref[nr];
       int32_t r = 0;
-      constexpr int U = 8;
+      constexpr int U = 8;  // 8 range reads, then 8 rank gathers in flight per thread
       for (int32_t base = tid; base < total; base += kTpb * U) {
         int32_t v[U];
 #pragma unroll
@@ -275,9 +316,14 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
             v[u] = perm_asc[(int64_t)s_m[r] * N + s_lo[r] + (f - s_pref[r])];
           }
         }
+        uint32_t q[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) q[u] = (has_list && v[u] >= 0) ? rk[v[u]] : kNoRank;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
           if (v[u] >= 0) atomicAnd(&pass[v[u] >> 5], ~(1u << (v[u] & 31)));
+          if (q[u] != kNoRank) atomicOr(&drop[q[u] >> 5], 1u << (q[u] & 31));
+        }
       }
       __syncthreads();
     }
@@ -285,40 +331,27 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
     for (int32_t w = tid; w < P.W64; w += kTpb)
       out[w] = (uint64_t)pass[2 * w] | ((uint64_t)pass[2 * w + 1] << 32);
   }
+  if (!has_list) return;
 
-  if (!(P.flags & PAS_TAS_PRIORITIZE)) return;
-
-  // ---- prioritizeNodesForRule: drop bitmap over the order's positions ----
-  const pas_rule pr = P.prio[pod];
-  const int32_t m0 = pr.metric;
-  const int32_t cnt0 = (m0 >= 0 && m0 < P.M) ? P.cnt[m0] : 0;
-  if (cnt0 == 0) {  // no rule / ReadMetric error -> empty HostPriorityList (:92-96)
-    if (tid == 0) P.order_len[pod] = 0;
-    return;
-  }
-  const int64_t col = ((int64_t)order_of(pr.op) * P.M + m0) * N;
-  const uint32_t* __restrict__ rk = P.rank + col;
-  const int32_t n_seg = (cnt0 + kSegPos - 1) / kSegPos;
-  const int32_t DW = n_seg * kSegWords * 2;  // 32-bit drop words written
-  for (int32_t w = tid; w < DW; w += kTpb) drop[w] = 0u;
-  __syncthreads();
-
-  for (int32_t w = tid; w < P.W32; w += kTpb) {
-    uint32_t z = ~pass[w] & tail_mask32(w, N);
-    while (z) {  // 4 rank gathers in flight per thread
-      int32_t n0 = -1, n1 = -1, n2 = -1, n3 = -1;
-      n0 = w * 32 + __ffs(z) - 1; z &= z - 1;
-      if (z) { n1 = w * 32 + __ffs(z) - 1; z &= z - 1; }
-      if (z) { n2 = w * 32 + __ffs(z) - 1; z &= z - 1; }
-      if (z) { n3 = w * 32 + __ffs(z) - 1; z &= z - 1; }
-      const uint32_t q0 = rk[n0];
-      const uint32_t q1 = n1 >= 0 ? rk[n1] : kNoRank;
-      const uint32_t q2 = n2 >= 0 ? rk[n2] : kNoRank;
-      const uint32_t q3 = n3 >= 0 ? rk[n3] : kNoRank;
-      if (q0 != kNoRank) atomicOr(&drop[q0 >> 5], 1u << (q0 & 31));
-      if (q1 != kNoRank) atomicOr(&drop[q1 >> 5], 1u << (q1 & 31));
-      if (q2 != kNoRank) atomicOr(&drop[q2 >> 5], 1u << (q2 & 31));
-      if (q3 != kNoRank) atomicOr(&drop[q3 >> 5], 1u << (q3 & 31));
+  // ---- nodes outside the candidate set are dropped too (4 rank gathers in flight) ----
+  if (cand32) {
+    for (int32_t w = tid; w < P.W32; w += kTpb) {
+      uint32_t z = ~cand32[w] & tail_mask32(w, N);
+      while (z) {
+        int32_t n0 = -1, n1 = -1, n2 = -1, n3 = -1;
+        n0 = w * 32 + __ffs(z) - 1; z &= z - 1;
+        if (z) { n1 = w * 32 + __ffs(z) - 1; z &= z - 1; }
+        if (z) { n2 = w * 32 + __ffs(z) - 1; z &= z - 1; }
+        if (z) { n3 = w * 32 + __ffs(z) - 1; z &= z - 1; }
+        const uint32_t q0 = rk[n0];
+        const uint32_t q1 = n1 >= 0 ? rk[n1] : kNoRank;
+        const uint32_t q2 = n2 >= 0 ? rk[n2] : kNoRank;
+        const uint32_t q3 = n3 >= 0 ? rk[n3] : kNoRank;
+        if (q0 != kNoRank) atomicOr(&drop[q0 >> 5], 1u << (q0 & 31));
+        if (q1 != kNoRank) atomicOr(&drop[q1 >> 5], 1u << (q1 & 31));
+        if (q2 != kNoRank) atomicOr(&drop[q2 >> 5], 1u << (q2 & 31));
+        if (q3 != kNoRank) atomicOr(&drop[q3 >> 5], 1u << (q3 & 31));
+      }
     }
   }
   __syncthreads();
@@ -346,37 +379,53 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
 
 // ---------------------------------------------------------------------------- emit
 
-constexpr int kEmitSegsPerBlock = kWaves;                       // 4 x 1024 positions
-constexpr int kStageWords = ((kSegPos + 3 + 255) / 256) * 256;  // 5 x 256 (unrolled reads)
+constexpr int kEmitBatch = 16;                                   // pods fetched per round
+constexpr int kStageWords = ((kSegPos + 31 + 255) / 256) * 256;  // 5 x 256 (unrolled reads)
+typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
 
-// Row-major emit: block b covers 4 consecutive 1024-position segments of one pod row, pods
-// in bucket order.  Concurrent blocks therefore write a few contiguous row spans (the
-// DRAM-friendly pattern a linear fill has), and the pods of a bucket, which share one
-// permutation, run back to back so the permutation segments are L2 hits.  Each wave does
-// one load round (its permutation segment, the pod's 16 drop words, the segment base),
-// compacts the kept entries into an LDS stage aligned to the destination's 16-byte grid and
-// writes them with dwordx4 stores (dword stores for the two partial end chunks).
+// Non-temporal stores: measured on MI355X for this write pattern (3.7 KB runs in 4096
+// rows), aligned 16-byte nt stores sustain ~5.3 TB/s against ~3.7 TB/s for plain stores
+// and ~3.0 TB/s for unaligned dword nt stores (scripts/diag/write_pattern.hip).
+__device__ __forceinline__ void st_nt16(int32_t* p, v4i32 v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<v4i32*>(p));
+}
+__device__ __forceinline__ void st_nt4(int32_t* p, int32_t v) { __builtin_nontemporal_store(v, p); }
+
+// One wave per (bucket, 1024-position segment): the permutation segment is read once into
+// registers and written, compacted by each pod's drop bits, for every pod of the bucket.
+// Pods are taken in batches of 16: one round of vector loads fetches their ids, segment
+// bases and drop words into the wave's LDS; the store phase then runs without loads.  Each
+// pod's kept entries are compacted (mbcnt) into an LDS stage aligned to the destination's
+// 16-byte grid and written with 16-byte nt stores (dword nt stores for the two partial end
+// chunks).  Waves of a block take different buckets, so no block barrier is used: a wave
+// only touches its own LDS slices, whose operations execute in program order.
 // kAblate (diagnostic timing builds only, PAS_EMIT_ABLATE; outputs wrong): 1 = no stores.
 template <int kAblate>
 __global__ __launch_bounds__(kTpb) void tas_emit_kernel(
-    int32_t N, int32_t M, int32_t D64, int32_t S, int32_t blocks_per_pod,
-    const int32_t* __restrict__ perm, const int32_t* __restrict__ cnt,
-    const pas_rule* __restrict__ prio, const int32_t* __restrict__ pod_list,
-    const int32_t* __restrict__ group_start, int32_t G, const uint64_t* __restrict__ drop,
-    const int32_t* __restrict__ seg_base, int32_t* __restrict__ order_out) {
+    int32_t N, int32_t M, int32_t D64, int32_t S, const int32_t* __restrict__ perm,
+    const int32_t* __restrict__ cnt, const int32_t* __restrict__ pod_list,
+    const int32_t* __restrict__ group_start, const int32_t* __restrict__ seg_start,
+    const int32_t* __restrict__ seg_group, const uint64_t* __restrict__ drop,
+    const int32_t* __restrict__ seg_base, int32_t total_segs_bound,
+    int32_t* __restrict__ order_out) {
   __shared__ __attribute__((aligned(16))) int32_t stage_all[kWaves][kStageWords];
+  __shared__ __attribute__((aligned(16))) uint64_t dbuf_all[kWaves][kEmitBatch][kSegWords];
+  __shared__ int32_t pbuf_all[kWaves][kEmitBatch];
+  __shared__ int32_t bbuf_all[kWaves][kEmitBatch];
   const int wave = threadIdx.x >> 6;
   int32_t* stage = stage_all[wave];
+  uint64_t(*dbuf)[kSegWords] = dbuf_all[wave];
+  int32_t* pbuf = pbuf_all[wave];
+  int32_t* bbuf = bbuf_all[wave];
+  const int32_t gw = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * kWaves + wave));
   const int lane = threadIdx.x & 63;
-  const int32_t pidx = blockIdx.x / blocks_per_pod;
-  if (pidx >= group_start[G]) return;  // pods without a list sit after the buckets
-  const int32_t s = (blockIdx.x % blocks_per_pod) * kEmitSegsPerBlock + wave;
-  const int32_t pod = pod_list[pidx];
-  const pas_rule pr = prio[pod];
-  const int32_t m0 = pr.metric;
+  if (gw >= total_segs_bound) return;
+  const int32_t g = seg_group[gw];  // -1 past the last segment
+  if (g < 0) return;
+  const int32_t m0 = g % M;
+  const int32_t order = g / M;
   const int32_t cnt0 = cnt[m0];
-  if (s * kSegPos >= cnt0) return;
-  const int32_t order = order_of(pr.op);
+  const int32_t s = gw - seg_start[g];
   const int32_t* __restrict__ pm = perm + ((int64_t)order * M + m0) * N;
   const int32_t k0 = s * kSegPos + lane;
   int32_t node[kSegWords];
@@ -385,42 +434,71 @@ __global__ __launch_bounds__(kTpb) void tas_emit_kernel(
     const int32_t kk = k0 + j * 64;
     node[j] = kk < cnt0 ? pm[kk] : 0;
   }
-  const uint64_t* __restrict__ dw = drop + (int64_t)pod * D64 + s * kSegWords;
-  uint64_t d[kSegWords];
+  const bool full = (s + 1) * kSegPos <= cnt0;  // only a bucket's last segment has a tail
+  const int32_t i1 = group_start[g + 1];
+  for (int32_t i0 = group_start[g]; i0 < i1; i0 += kEmitBatch) {
+    const int32_t nb = min(kEmitBatch, i1 - i0);
+    // ---- fetch round: ids, bases, drop words of up to 16 pods ----
+    const int32_t mypod = lane < nb ? pod_list[i0 + lane] : 0;
+    const int pidx = lane >> 2;  // 4 lanes x 32 bytes per pod
+    const int32_t dpod = __shfl(mypod, pidx, 64);
+    if (pidx < nb) {
+      const int4* src = reinterpret_cast<const int4*>(drop + (int64_t)dpod * D64 +
+                                                      s * kSegWords + (lane & 3) * 4);
+      int4* dst = reinterpret_cast<int4*>(&dbuf[pidx][(lane & 3) * 4]);
+      dst[0] = src[0];
+      dst[1] = src[1];
+    }
+    if (lane < nb) {
+      pbuf[lane] = mypod;
+      bbuf[lane] = seg_base[(int64_t)mypod * S + s];
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- store phase: no memory loads below ----
+    for (int32_t p = 0; p < nb; ++p) {
+      const int32_t pod = pbuf[p];
+      const int32_t base = bbuf[p];
+      const int64_t gdst = (int64_t)pod * N + base;  // element index of the first entry
+      // stage aligned to the destination's 128-byte lines: every 1 KB store instruction
+      // then covers whole lines, which take nt stores; only the run's first and last
+      // line (shared with the neighbouring runs) go through L2 with plain stores
+      const int32_t a = (int32_t)(gdst & 31);
+      int32_t k = a;
 #pragma unroll
-  for (int j = 0; j < kSegWords; ++j) d[j] = dw[j];
-  const int32_t base = seg_base[(int64_t)pod * S + s];
-  const bool full = (s + 1) * kSegPos <= cnt0;
-  const int64_t gdst = (int64_t)pod * N + base;  // element index of the first entry
-  const int32_t a = (int32_t)(gdst & 3);
-  int32_t k = a;
+      for (int j = 0; j < kSegWords; ++j) {
+        const uint64_t keep =
+            ~dbuf[p][j] & (full ? ~0ull : tail_mask64(s * kSegWords + j, cnt0));
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(keep >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
+        if ((keep >> lane) & 1ull) stage[k + (int32_t)below] = node[j];
+        k += __popcll(keep);
+      }
+      __builtin_amdgcn_wave_barrier();
+      int32_t* __restrict__ out = order_out + (gdst - a);  // 128-byte aligned
+      constexpr int kChunkIters = kStageWords / 256;
+      v4i32 v[kChunkIters];
 #pragma unroll
-  for (int j = 0; j < kSegWords; ++j) {
-    const uint64_t keep = ~d[j] & (full ? ~0ull : tail_mask64(s * kSegWords + j, cnt0));
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-        (uint32_t)(keep >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
-    if ((keep >> lane) & 1ull) stage[k + (int32_t)below] = node[j];
-    k += __popcll(keep);
-  }
-  __builtin_amdgcn_wave_barrier();
-  int32_t* __restrict__ out = order_out + (gdst - a);  // 16-byte aligned
-  constexpr int kChunkIters = kStageWords / 256;
-  int4 v[kChunkIters];
+      for (int it = 0; it < kChunkIters; ++it)
+        v[it] = *reinterpret_cast<const v4i32*>(stage + (lane + it * 64) * 4);
+      const int32_t full_lo = (a + 31) & ~31;  // first entry of the first whole line
+      const int32_t full_hi = k & ~31;         // end of the last whole line
 #pragma unroll
-  for (int it = 0; it < kChunkIters; ++it)
-    v[it] = *reinterpret_cast<const int4*>(stage + (lane + it * 64) * 4);
-#pragma unroll
-  for (int it = 0; it < kChunkIters; ++it) {
-    const int32_t e0 = (lane + it * 64) * 4;
-    if (kAblate == 1 && gdst >= 0) {
-      asm volatile("" ::"v"(v[it].x), "v"(v[it].y), "v"(v[it].z), "v"(v[it].w));
-    } else if (e0 >= a && e0 + 4 <= k) {
-      *reinterpret_cast<int4*>(out + e0) = v[it];
-    } else if (e0 < k && e0 + 4 > a) {  // one of the two partial end chunks
-      if (e0 + 0 >= a && e0 + 0 < k) out[e0 + 0] = v[it].x;
-      if (e0 + 1 >= a && e0 + 1 < k) out[e0 + 1] = v[it].y;
-      if (e0 + 2 >= a && e0 + 2 < k) out[e0 + 2] = v[it].z;
-      if (e0 + 3 >= a && e0 + 3 < k) out[e0 + 3] = v[it].w;
+      for (int it = 0; it < kChunkIters; ++it) {
+        const int32_t e0 = (lane + it * 64) * 4;
+        if (kAblate == 1 && gdst >= 0) {
+          asm volatile("" ::"v"(v[it].x), "v"(v[it].y), "v"(v[it].z), "v"(v[it].w));
+        } else if (e0 >= full_lo && e0 + 4 <= full_hi) {
+          st_nt16(out + e0, v[it]);
+        } else if (e0 >= a && e0 + 4 <= k) {
+          *reinterpret_cast<v4i32*>(out + e0) = v[it];
+        } else if (e0 < k && e0 + 4 > a) {  // one of the two partial end chunks
+          if (e0 + 0 >= a && e0 + 0 < k) out[e0 + 0] = v[it].x;
+          if (e0 + 1 >= a && e0 + 1 < k) out[e0 + 1] = v[it].y;
+          if (e0 + 2 >= a && e0 + 2 < k) out[e0 + 2] = v[it].z;
+          if (e0 + 3 >= a && e0 + 3 < k) out[e0 + 3] = v[it].w;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   }
 }
@@ -483,13 +561,20 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     return set_error(ctx, PAS_ECAPACITY, "pas_tas_eval: more than 4096 metric columns");
   const bool prio = (flags & PAS_TAS_PRIORITIZE) != 0;
 
-  // scratch: ranges | pod_list | group_start | seg_base | drop
-  const size_t sizes[5] = {
+  // upper bound on emit segments: at most min(P, G) non-empty buckets of S segments
+  const int64_t max_segs = prio ? (int64_t)std::min(n_pods, G) * S : 0;
+  if (max_segs > INT32_MAX) return set_error(ctx, PAS_ECAPACITY, "pas_tas_eval: batch too large");
+
+  // scratch: ranges | pod_list | group_start | seg_start | seg_group | seg_base | drop | desc
+  const size_t sizes[8] = {
       align256(sizeof(int2) * (size_t)std::max(n_rules, 1)),
       align256(sizeof(int32_t) * (size_t)n_pods),
       align256(sizeof(int32_t) * (size_t)(G + 2)),
+      align256(sizeof(int32_t) * (size_t)(G + 1)),
+      align256(sizeof(int32_t) * (size_t)std::max<int64_t>(max_segs, 1)),
       prio ? align256(sizeof(int32_t) * (size_t)n_pods * S) : 0,
-      prio ? align256(sizeof(uint64_t) * (size_t)n_pods * D64) : 0};
+      prio ? align256(sizeof(uint64_t) * (size_t)n_pods * D64) : 0,
+      align256(sizeof(int4) * (size_t)n_pods)};
   size_t need = 0;
   for (size_t b : sizes) need += b;
   if (need > ctx->aux_bytes) {
@@ -503,16 +588,19 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     ctx->aux_bytes = need;
   }
   char* cur = static_cast<char*>(ctx->aux);
-  char* parts[5];
-  for (int i = 0; i < 5; ++i) {
+  char* parts[8];
+  for (int i = 0; i < 8; ++i) {
     parts[i] = cur;
     cur += sizes[i];
   }
   int2* d_ranges = reinterpret_cast<int2*>(parts[0]);
   int32_t* d_list = reinterpret_cast<int32_t*>(parts[1]);
   int32_t* d_gs = reinterpret_cast<int32_t*>(parts[2]);
-  int32_t* d_sb = reinterpret_cast<int32_t*>(parts[3]);
-  uint64_t* d_drop = reinterpret_cast<uint64_t*>(parts[4]);
+  int32_t* d_ss = reinterpret_cast<int32_t*>(parts[3]);
+  int32_t* d_sg = reinterpret_cast<int32_t*>(parts[4]);
+  int32_t* d_sb = reinterpret_cast<int32_t*>(parts[5]);
+  uint64_t* d_drop = reinterpret_cast<uint64_t*>(parts[6]);
+  int4* d_desc = reinterpret_cast<int4*>(parts[7]);
 
   TimedLaunch tl;
   if ((flags & PAS_TAS_FILTER) && n_rules > 0) {
@@ -523,7 +611,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     PAS_HIP(ctx, hipGetLastError());
   }
 
-  GroupParams gp{n_pods, M, N, flags, d_prio, t.cnt, d_list, d_gs};
+  GroupParams gp{n_pods, M, N, flags, d_prio, t.cnt, d_list, d_gs, d_ss, d_sg,
+                 (int32_t)max_segs};
   const size_t group_lds = sizeof(int32_t) * ((size_t)kGroupTpb + G + 1);
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_group_kernel),
@@ -556,6 +645,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   fp.drop = d_drop;
   fp.seg_base = d_sb;
   fp.order_len = d_len;
+  fp.desc = d_desc;
   if (filter_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_filter_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -566,8 +656,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   PAS_HIP(ctx, hipGetLastError());
 
   if (prio) {
-    const int32_t bpp = (S + kEmitSegsPerBlock - 1) / kEmitSegsPerBlock;
-    const int64_t blocks = (int64_t)n_pods * bpp;
+    const int64_t blocks = (max_segs + kWaves - 1) / kWaves;
     if (blocks > 0) {
       timing_begin(ctx, s, PAS_K_TAS_EMIT, &tl);
       static const int ablate = [] {
@@ -575,13 +664,13 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
         return e ? std::atoi(e) : 0;
       }();
       if (ablate == 1)
-        tas_emit_kernel<1><<<(unsigned)blocks, kTpb, 0, s>>>(N, M, D64, S, bpp, t.perm, t.cnt,
-                                                             d_prio, d_list, d_gs, G, d_drop,
-                                                             d_sb, d_order);
+        tas_emit_kernel<1><<<(unsigned)blocks, kTpb, 0, s>>>(N, M, D64, S, t.perm, t.cnt, d_list,
+                                                             d_gs, d_ss, d_sg, d_drop, d_sb,
+                                                             (int32_t)max_segs, d_order);
       else
-        tas_emit_kernel<0><<<(unsigned)blocks, kTpb, 0, s>>>(N, M, D64, S, bpp, t.perm, t.cnt,
-                                                             d_prio, d_list, d_gs, G, d_drop,
-                                                             d_sb, d_order);
+        tas_emit_kernel<0><<<(unsigned)blocks, kTpb, 0, s>>>(N, M, D64, S, t.perm, t.cnt, d_list,
+                                                             d_gs, d_ss, d_sg, d_drop, d_sb,
+                                                             (int32_t)max_segs, d_order);
       timing_end(ctx, s, &tl);
       PAS_HIP(ctx, hipGetLastError());
     }

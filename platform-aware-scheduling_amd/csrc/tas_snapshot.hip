@@ -108,7 +108,8 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     PAS_HIP(ctx, hipMalloc(&t.present, sizeof(uint64_t) * mw));
     PAS_HIP(ctx, hipMalloc(&t.cnt, sizeof(int32_t) * mm));
     PAS_HIP(ctx, hipMalloc(&t.sorted, sizeof(int64_t) * mn));
-    PAS_HIP(ctx, hipMalloc(&t.perm, sizeof(int32_t) * mn * kNumOrders));
+    // +1024 entries: the emit loader reads whole 1024-position segments unconditionally
+    PAS_HIP(ctx, hipMalloc(&t.perm, sizeof(int32_t) * (mn * kNumOrders + 1024)));
     PAS_HIP(ctx, hipMalloc(&t.rank, sizeof(uint32_t) * mn * kNumOrders));
     PAS_HIP(ctx, hipMalloc(&t.vals_c, sizeof(int64_t) * mn));
     PAS_HIP(ctx, hipMalloc(&t.word_scan, sizeof(uint32_t) * (mw + 1)));
