@@ -19,6 +19,7 @@ constexpr int kNumOrders = 3;
 
 inline int64_t w64(int64_t n) { return (n + 63) / 64; }
 inline int64_t w32(int64_t n) { return (n + 31) / 32; }
+inline int64_t rank_row(int64_t n) { return w32(n) * 32; }
 
 // Device-resident TAS snapshot.  Layout in HBM (M metrics, N nodes):
 //   vals     int64 [M][N]      raw v_milli (deschedule sweep reads it directly)
@@ -26,7 +27,9 @@ inline int64_t w32(int64_t n) { return (n + 31) / 32; }
 //   cnt      int32 [M]         nodes that have metric m
 //   sorted   int64 [M][N]      ascending values of the present nodes (first cnt[m])
 //   perm     int32 [3][M][N]   node ids in asc / desc / index order (first cnt[m])
-//   rank     uint32 [3][M][N]  position of node n in each order, kNoRank if absent
+//   rank     uint32 [3][M][Nr] position of node n in each order, kNoRank if absent; rows
+//                              padded to Nr = round_up(N, 32) so that the 32 ranks of
+//                              one 32-node bitmap word fill one 128-byte line
 struct TasSnapshot {
   bool valid = false;
   uint64_t gen = 0;
@@ -38,6 +41,7 @@ struct TasSnapshot {
   int64_t* sorted = nullptr;
   int32_t* perm = nullptr;
   uint32_t* rank = nullptr;
+  int32_t rank_stride = 0;  // Nr
   // build scratch
   int64_t* vals_c = nullptr;       // compacted values in index order
   uint32_t* word_scan = nullptr;   // [M*W64 + 1]

@@ -47,13 +47,6 @@ constexpr int kMaxGroupMetrics = 4096;      // 3 * M + 1 buckets in LDS for K gr
 constexpr int kMiscWords = 4 * kRuleChunk + 16;
 static_assert(kMiscWords >= kTpb, "scan partials live in the misc words");
 
-__device__ __forceinline__ uint32_t tail_mask32(int32_t w, int32_t n) {
-  const int32_t lo = w * 32;
-  if (lo >= n) return 0u;
-  if (lo + 32 <= n) return 0xFFFFFFFFu;
-  return (1u << (n - lo)) - 1u;
-}
-
 __device__ __forceinline__ uint64_t tail_mask64(int32_t c, int32_t n) {
   const int32_t lo = c * 64;
   if (lo >= n) return 0ull;
@@ -155,23 +148,33 @@ struct GroupParams {
   int32_t P, M, N;
   uint32_t flags;
   const pas_rule* prio;
+  const int32_t* rule_off;
   const int32_t* cnt;
   int32_t* pod_list;     // [P]   pods bucketed by key, bucket G (no list) last
   int32_t* group_start;  // [G+2]
   int32_t* seg_start;    // [G+1] first emit segment of each bucket
   int32_t* seg_group;    // [max_segs] bucket of each emit segment, -1 past the last
+  int4* desc;            // [2P] per bucketed position: {pod, ocol, cnt0, n_seg}, {r0, r1, 0, 0}
   int32_t max_segs;
 };
 
-__device__ __forceinline__ int32_t pod_key(const GroupParams& g, int32_t p) {
+// Bucket of pod p: order column (order * M + metric) of its prioritize list, or G when it
+// has none (no PRIORITIZE flag, metric out of range, or a metric no node reports — the
+// ReadMetric error of prioritizeNodesForRule, telemetryscheduler.go:92-96).
+__device__ __forceinline__ int32_t pod_key(const GroupParams& g, int32_t p, int32_t* cnt0) {
   const int32_t G = 3 * g.M;
+  *cnt0 = 0;
   if (!(g.flags & PAS_TAS_PRIORITIZE)) return G;
   const pas_rule r = g.prio[p];
-  if (r.metric < 0 || r.metric >= g.M || g.cnt[r.metric] == 0) return G;
+  if (r.metric < 0 || r.metric >= g.M) return G;
+  const int32_t c = g.cnt[r.metric];
+  if (c == 0) return G;
+  *cnt0 = c;
   return order_of(r.op) * g.M + r.metric;
 }
 
-// One block: counting sort of the pods by bucket + emit-segment table per bucket.
+// One block: counting sort of the pods by bucket, the per-position pod descriptors the
+// filter reads with one load, and the emit-segment table per bucket.
 __global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
   extern __shared__ __attribute__((aligned(16))) int32_t sh[];
   const int32_t G = 3 * g.M;
@@ -180,15 +183,21 @@ __global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
   const int tid = threadIdx.x;
   for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
   __syncthreads();
-  for (int32_t p = tid; p < g.P; p += kGroupTpb) atomicAdd(&hist[pod_key(g, p)], 1);
+  int32_t c0;
+  for (int32_t p = tid; p < g.P; p += kGroupTpb) atomicAdd(&hist[pod_key(g, p, &c0)], 1);
   __syncthreads();
   block_exclusive_scan(hist, G + 1, partial);
   for (int32_t i = tid; i <= G; i += kGroupTpb) g.group_start[i] = hist[i];
   if (tid == 0) g.group_start[G + 1] = g.P;
   __syncthreads();
+  const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
   for (int32_t p = tid; p < g.P; p += kGroupTpb) {
-    const int32_t pos = atomicAdd(&hist[pod_key(g, p)], 1);  // order inside a bucket is free
+    const int32_t key = pod_key(g, p, &c0);
+    const int32_t r0 = filt ? g.rule_off[p] : 0, r1 = filt ? g.rule_off[p + 1] : 0;
+    const int32_t pos = atomicAdd(&hist[key], 1);  // order inside a bucket is free
     g.pod_list[pos] = p;
+    g.desc[2 * pos] = make_int4(p, key < G ? key : -1, c0, (c0 + kSegPos - 1) / kSegPos);
+    g.desc[2 * pos + 1] = make_int4(r0, r1, 0, 0);
   }
   __syncthreads();
   // hist[i] now holds the end of bucket i: emit segments per non-empty bucket
@@ -217,150 +226,196 @@ struct FilterParams {
   int32_t W64;
   int32_t D64;   // drop row stride in 64-bit words (multiple of kSegWords)
   int32_t S;     // seg_base row stride (= D64 / kSegWords)
+  int32_t Nr;    // rank row stride
   uint32_t flags;
-  const int32_t* rule_off;
   const int2* ranges;
   const pas_rule* rules;
-  const pas_rule* prio;
   const uint64_t* cand;
   const int32_t* perm;   // [3][M][N]
-  const uint32_t* rank;  // [3][M][N]
-  const int32_t* cnt;    // [M]
-  const int32_t* pod_list;
+  const uint32_t* rank;  // [3][M][Nr]
+  const int4* desc;      // [2P] from K group
   uint64_t* pass_out;    // [P][W64]
   uint64_t* drop;        // [P][D64]
   int32_t* seg_base;     // [P][S]
   int32_t* order_len;    // [P]
-  int4* desc;            // [P] per bucketed position: {pod, order*M + m0, cnt0, n_seg}
 };
 
+typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int32_t wave_inclusive_sum(int32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+
+// One workgroup per pod.  Phases, each issuing its global loads before their first use:
+//   1. candidates -> LDS pass bitmap over node ids;
+//   2. rule ranges: 16 coalesced perm reads per thread, LDS atomicAnd into the bitmap;
+//   3. prioritize: every clear bit of the final bitmap (a failing node or a non-candidate)
+//      is mapped through the order's rank row into an LDS drop bitmap over positions.
+//      The walk is in node order, 8 lanes per 32-node word: lane q of a word loads the
+//      16-byte quad of ranks of nodes 4q..4q+3 only when one of them is clear, so a wave
+//      instruction touches at most 8 lines and a pod moves one line per word that has a
+//      clear bit.  (A random 4-byte gather per failing node moves a line per node: 2.6x
+//      the line traffic at the C2 shape, measured 0.115 ms of gathers per step; scanning
+//      the whole order row per pod instead is LDS-bank / VALU bound, measured slower.)
+//   4. drop row + kept count per 1024-position segment -> segment output bases.
+// kAblate (diagnostic timing builds only, PAS_FILTER_ABLATE; outputs wrong): bit 1 = no
+// rank loads, 2 = no LDS atomics in the rule loop, 4 = no rule loop, 8 = no row writes.
+template <int kAblate>
 __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  int32_t* s_pref = reinterpret_cast<int32_t*>(lds);  // [kRuleChunk + 1]
-  int32_t* s_lo = s_pref + (kRuleChunk + 4);          // [kRuleChunk]
-  int32_t* s_m = s_lo + kRuleChunk;                   // [kRuleChunk]
-  int32_t* s_partial = reinterpret_cast<int32_t*>(lds);  // [kTpb], after the rule phase
+  int32_t* s_pref = reinterpret_cast<int32_t*>(lds);  // [kRuleChunk] prefix of range lengths
+  int32_t* s_base = s_pref + kRuleChunk;              // [kRuleChunk] perm index of range start
+  int32_t* s_total = s_base + kRuleChunk;             // [1]
   uint32_t* pass = lds + kMiscWords;                  // [W32p]
-  uint32_t* drop = pass + P.W32p;                     // [W32p]
+  uint32_t* drop = pass + P.W32p;                     // [S * 32], then segk [S]
+  uint64_t* pass64 = reinterpret_cast<uint64_t*>(pass);
+  uint64_t* drop64 = reinterpret_cast<uint64_t*>(drop);
 
   // XCD-aware placement: blocks b and b+8 share an XCD (MI355X_MICROARCH.md, Workgroup
   // dispatch), so give each XCD a contiguous run of the bucketed pod list; pods of a
-  // bucket then hit the same rank array in that XCD's L2.  Speed only, never correctness.
+  // bucket then read the same rank row from that XCD's L2.  Speed only, never correctness.
   const int32_t nb = gridDim.x, b = blockIdx.x;
   const int32_t xcd = b & 7, per_xcd = nb >> 3, rem = nb & 7;
   const int32_t pos = xcd * per_xcd + min(xcd, rem) + (b >> 3);
-  const int32_t pod = P.pod_list[pos];
+  const int4 d0 = P.desc[2 * pos], d1 = P.desc[2 * pos + 1];
+  const int32_t pod = d0.x, ocol = d0.y, cnt0 = d0.z, n_seg = d0.w;
+  const int32_t r0 = d1.x, r1 = d1.y;
   const int tid = threadIdx.x;
-  const int32_t N = P.N;
+  const int32_t N = P.N, W64 = P.W64;
+  const bool has_list = ocol >= 0;
 
-  // ---- candidates -> pass bitmap (args.Nodes.Items, telemetryscheduler.go:204) ----
-  const uint32_t* cand32 =
-      P.cand ? reinterpret_cast<const uint32_t*>(P.cand + (int64_t)pod * P.W64) : nullptr;
-  for (int32_t w = tid; w < P.W32p; w += kTpb) {
-    const uint32_t x = cand32 ? cand32[w] : 0xFFFFFFFFu;
-    pass[w] = x & tail_mask32(w, N);
+  // ---- 1. candidates -> pass bitmap (args.Nodes.Items, telemetryscheduler.go:204) ----
+  constexpr int kCU = 8;
+  const uint64_t* __restrict__ cand = P.cand ? P.cand + (int64_t)pod * W64 : nullptr;
+  for (int32_t w0 = tid; w0 < W64; w0 += kTpb * kCU) {
+    uint64_t x[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; ++u) {
+      const int32_t w = w0 + u * kTpb;
+      x[u] = (cand && w < W64) ? cand[w] : ~0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kCU; ++u) {
+      const int32_t w = w0 + u * kTpb;
+      if (w < W64) pass64[w] = x[u] & tail_mask64(w, N);
+    }
   }
+  if (has_list)
+    for (int32_t w = tid; w < n_seg * kSegWords; w += kTpb) drop64[w] = 0ull;
+  else if (tid == 0 && (P.flags & PAS_TAS_PRIORITIZE))
+    P.order_len[pod] = 0;  // no rule / ReadMetric error -> empty HostPriorityList (:92-96)
   __syncthreads();
 
-  // ---- prioritize setup: the order whose positions the drop bitmap indexes ----
-  int32_t cnt0 = 0, n_seg = 0;
-  const uint32_t* __restrict__ rk = nullptr;
-  if (P.flags & PAS_TAS_PRIORITIZE) {
-    const pas_rule pr = P.prio[pod];
-    const int32_t m0 = pr.metric;
-    cnt0 = (m0 >= 0 && m0 < P.M) ? P.cnt[m0] : 0;
-    if (cnt0 > 0) {
-      const int32_t ocol = order_of(pr.op) * P.M + m0;
-      rk = P.rank + (int64_t)ocol * N;
-      n_seg = (cnt0 + kSegPos - 1) / kSegPos;
-      if (tid == 0) P.desc[pos] = make_int4(pod, ocol, cnt0, n_seg);
-      for (int32_t w = tid; w < n_seg * kSegWords * 2; w += kTpb) drop[w] = 0u;
-    } else if (tid == 0) {
-      P.order_len[pod] = 0;  // no rule / ReadMetric error -> empty HostPriorityList (:92-96)
-    }
-    __syncthreads();
-  }
-  const bool has_list = rk != nullptr;
-
-  // ---- dontschedule.Violated: every node of every rule range fails the filter and, when
-  //      the pod has a prioritize list, is dropped at its rank in that order ----
-  if (P.flags & PAS_TAS_FILTER) {
-    const int32_t r0 = P.rule_off[pod], r1 = P.rule_off[pod + 1];
+  // ---- 2. dontschedule.Violated: every node of every rule range fails the filter ----
+  if ((P.flags & PAS_TAS_FILTER) && !(kAblate & 4)) {
     const int32_t* perm_asc = P.perm + (int64_t)kOrderAsc * P.M * N;
     for (int32_t c0 = r0; c0 < r1; c0 += kRuleChunk) {
       const int32_t nr = min(kRuleChunk, r1 - c0);
-      if (tid < nr) {
-        const int2 rg = P.ranges[c0 + tid];
-        s_lo[tid] = rg.x;
-        s_pref[tid + 1] = rg.y - rg.x;
-        const int32_t m = P.rules[c0 + tid].metric;
-        s_m[tid] = (m >= 0 && m < P.M) ? m : 0;
+      if (tid < 64) {  // wave 0: rule table = prefix of range lengths (largest-index search)
+        int32_t len = 0, bse = 0;
+        if (tid < nr) {
+          const int2 rg = P.ranges[c0 + tid];
+          const int32_t m = P.rules[c0 + tid].metric;
+          len = rg.y - rg.x;
+          bse = (m >= 0 && m < P.M) ? m * N + rg.x : 0;
+        }
+        const int32_t incl = wave_inclusive_sum(len);
+        const int32_t total = __shfl(incl, nr - 1, 64);  // all lanes active here
+        s_base[tid] = bse;
+        s_pref[tid] = tid < nr ? incl - len : INT32_MAX;
+        if (tid == 0) *s_total = total;
       }
       __syncthreads();
-      if (tid == 0) {
-        s_pref[0] = 0;
-        for (int32_t i = 0; i < nr; ++i) s_pref[i + 1] += s_pref[i];
-      }
-      __syncthreads();
-      const int32_t total = s_pref[nr];
-      int32_t r = 0;
-      constexpr int U = 8;  // 8 range reads, then 8 rank gathers in flight per thread
+      const int32_t total = *s_total;
+      // 16 range reads in flight per thread.  Loads are unconditional (entries past the
+      // end re-read the last one; clearing a bit twice is harmless): a load under a
+      // divergent branch makes the compiler wait for the previous one first.
+      constexpr int U = 16;
       for (int32_t base = tid; base < total; base += kTpb * U) {
         int32_t v[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int32_t f = base + u * kTpb;
-          v[u] = -1;
-          if (f < total) {
-            while (s_pref[r + 1] <= f) ++r;
-            v[u] = perm_asc[(int64_t)s_m[r] * N + s_lo[r] + (f - s_pref[r])];
-          }
-        }
-        uint32_t q[U];
+          const int32_t f = min(base + u * kTpb, total - 1);
+          int32_t r = 0;  // largest r with s_pref[r] <= f (zero-length ranges are skipped)
 #pragma unroll
-        for (int u = 0; u < U; ++u) q[u] = (has_list && v[u] >= 0) ? rk[v[u]] : kNoRank;
+          for (int st = kRuleChunk / 2; st > 0; st >>= 1)
+            r = s_pref[r + st] <= f ? r + st : r;
+          v[u] = perm_asc[s_base[r] + (f - s_pref[r])];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if (v[u] >= 0) atomicAnd(&pass[v[u] >> 5], ~(1u << (v[u] & 31)));
-          if (q[u] != kNoRank) atomicOr(&drop[q[u] >> 5], 1u << (q[u] & 31));
+          if (kAblate & 2) {
+            asm volatile("" ::"v"(v[u]));
+            continue;
+          }
+          atomicAnd(&pass[v[u] >> 5], ~(1u << (v[u] & 31)));
         }
       }
       __syncthreads();
     }
-    uint64_t* out = P.pass_out + (int64_t)pod * P.W64;
-    for (int32_t w = tid; w < P.W64; w += kTpb)
-      out[w] = (uint64_t)pass[2 * w] | ((uint64_t)pass[2 * w + 1] << 32);
   }
-  if (!has_list) return;
+  // FilterResult row -> HBM.  Written after phase 3 when there is one: a store ahead of
+  // phase 3's loads would make their first wait also wait for the store.
+  const bool write_pass = (P.flags & PAS_TAS_FILTER) && !(kAblate & 8);
+  uint64_t* pass_row = P.pass_out + (int64_t)pod * W64;
+  if (!has_list) {
+    if (write_pass)
+      for (int32_t w = tid; w < W64; w += kTpb) pass_row[w] = pass64[w];
+    return;
+  }
 
-  // ---- nodes outside the candidate set are dropped too (4 rank gathers in flight) ----
-  if (cand32) {
-    for (int32_t w = tid; w < P.W32; w += kTpb) {
-      uint32_t z = ~cand32[w] & tail_mask32(w, N);
-      while (z) {
-        int32_t n0 = -1, n1 = -1, n2 = -1, n3 = -1;
-        n0 = w * 32 + __ffs(z) - 1; z &= z - 1;
-        if (z) { n1 = w * 32 + __ffs(z) - 1; z &= z - 1; }
-        if (z) { n2 = w * 32 + __ffs(z) - 1; z &= z - 1; }
-        if (z) { n3 = w * 32 + __ffs(z) - 1; z &= z - 1; }
-        const uint32_t q0 = rk[n0];
-        const uint32_t q1 = n1 >= 0 ? rk[n1] : kNoRank;
-        const uint32_t q2 = n2 >= 0 ? rk[n2] : kNoRank;
-        const uint32_t q3 = n3 >= 0 ? rk[n3] : kNoRank;
-        if (q0 != kNoRank) atomicOr(&drop[q0 >> 5], 1u << (q0 & 31));
-        if (q1 != kNoRank) atomicOr(&drop[q1 >> 5], 1u << (q1 & 31));
-        if (q2 != kNoRank) atomicOr(&drop[q2 >> 5], 1u << (q2 & 31));
-        if (q3 != kNoRank) atomicOr(&drop[q3 >> 5], 1u << (q3 & 31));
+  // ---- 3. clear bits -> drop bitmap over the order's positions (line-quad rank loads) ----
+  {
+    // buffer resource over the rank row (128-B aligned rows); built from wave-uniform
+    // values only (cdna_hip_programming.md T8)
+    const uint32_t* row = P.rank + (int64_t)ocol * P.Nr;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(row), 0, P.Nr * 4, 0x00020000);
+    const int q = tid & 7;                       // quad of the word: nodes 4q..4q+3
+    const int32_t wl = tid >> 3;                 // word slot: 32 per block step
+    constexpr int UQ = 8;                        // words per lane in flight
+    for (int32_t w0 = 0; w0 < P.W32; w0 += (kTpb / 8) * UQ) {
+      // The loads are unconditional buffer loads (a load under a divergent branch makes
+      // the compiler wait for the previous one first); a lane with nothing to map passes
+      // an out-of-range offset, which the range check turns into no fetch at all.
+      uint32_t zq[UQ];
+      v4i32 r[UQ];
+#pragma unroll
+      for (int u = 0; u < UQ; ++u) {
+        const int32_t w = min(w0 + u * (kTpb / 8) + wl, P.W32 - 1);
+        const int32_t lo = w * 32;
+        const uint32_t tail = lo + 32 <= N ? 0xFFFFFFFFu : (1u << (N - lo)) - 1u;
+        zq[u] = w0 + u * (kTpb / 8) + wl < P.W32 ? ((~pass[w] & tail) >> (4 * q)) & 0xFu : 0u;
+        const uint32_t voff = (zq[u] && !(kAblate & 1)) ? (uint32_t)(w * 8 + q) * 16u : 0x80000000u;
+        r[u] = __builtin_bit_cast(v4i32, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, 0));
+      }
+#pragma unroll
+      for (int u = 0; u < UQ; ++u) {
+        if (!zq[u]) continue;
+        const uint32_t rr[4] = {(uint32_t)r[u].x, (uint32_t)r[u].y, (uint32_t)r[u].z,
+                                (uint32_t)r[u].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (((zq[u] >> j) & 1u) && rr[j] != kNoRank)
+            atomicOr(&drop[rr[j] >> 5], 1u << (rr[j] & 31));
       }
     }
   }
   __syncthreads();
 
-  // drop row -> HBM; kept count per segment -> output base of each segment
-  const uint64_t* drop64 = reinterpret_cast<const uint64_t*>(drop);
+  // ---- 4. pass and drop rows -> HBM; kept count per segment -> segment output bases ----
+  if (write_pass)
+    for (int32_t w = tid; w < W64; w += kTpb) pass_row[w] = pass64[w];
   uint64_t* drow = P.drop + (int64_t)pod * P.D64;
-  for (int32_t w = tid; w < n_seg * kSegWords; w += kTpb) drow[w] = drop64[w];
-  int32_t* segk = reinterpret_cast<int32_t*>(pass);  // pass is dead now
+  if (!(kAblate & 8))
+    for (int32_t w = tid; w < n_seg * kSegWords; w += kTpb) drow[w] = drop64[w];
+  int32_t* segk = reinterpret_cast<int32_t*>(drop + (size_t)P.S * kSegWords * 2);  // [S]
   for (int32_t sgi = tid; sgi < n_seg; sgi += kTpb) {
     int32_t kept = 0;
 #pragma unroll
@@ -371,17 +426,26 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
     segk[sgi] = kept;
   }
   __syncthreads();
-  const int32_t total = block_exclusive_scan(segk, n_seg, s_partial);
-  int32_t* sb = P.seg_base + (int64_t)pod * P.S;
-  for (int32_t sgi = tid; sgi < n_seg; sgi += kTpb) sb[sgi] = segk[sgi];
-  if (tid == 0) P.order_len[pod] = total;
+  if (tid < 64) {  // wave 0: exclusive scan of the segment counts
+    const int32_t per = (n_seg + 63) / 64;
+    const int32_t lo = min(n_seg, tid * per), hi = min(n_seg, lo + per);
+    int32_t sum = 0;
+    for (int32_t i = lo; i < hi; ++i) sum += segk[i];
+    const int32_t incl = wave_inclusive_sum(sum);
+    int32_t run = incl - sum;
+    int32_t* sb = P.seg_base + (int64_t)pod * P.S;
+    for (int32_t i = lo; i < hi; ++i) {
+      sb[i] = run;
+      run += segk[i];
+    }
+    if (tid == 63) P.order_len[pod] = incl;
+  }
 }
 
 // ---------------------------------------------------------------------------- emit
 
 constexpr int kEmitBatch = 16;                                   // pods fetched per round
 constexpr int kStageWords = ((kSegPos + 31 + 255) / 256) * 256;  // 5 x 256 (unrolled reads)
-typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
 
 // Non-temporal stores: measured on MI355X for this write pattern (3.7 KB runs in 4096
 // rows), aligned 16-byte nt stores sustain ~5.3 TB/s against ~3.7 TB/s for plain stores
@@ -389,7 +453,6 @@ typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ void st_nt16(int32_t* p, v4i32 v) {
   __builtin_nontemporal_store(v, reinterpret_cast<v4i32*>(p));
 }
-__device__ __forceinline__ void st_nt4(int32_t* p, int32_t v) { __builtin_nontemporal_store(v, p); }
 
 // One wave per (bucket, 1024-position segment): the permutation segment is read once into
 // registers and written, compacted by each pod's drop bits, for every pod of the bucket.
@@ -551,9 +614,9 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   const int32_t S = (int32_t)((N + kSegPos - 1) / kSegPos);
   const int32_t D64 = S * kSegWords;
   const int32_t G = 3 * M;
-  // LDS: misc | pass bitmap (2*W64 words) | drop bitmap (S segments x 32 words)
-  const size_t filter_lds =
-      sizeof(uint32_t) * ((size_t)kMiscWords + 2 * (size_t)W64 + (size_t)S * kSegWords * 2);
+  // LDS: misc | pass bitmap (2*W64 words) | drop bitmap (S segments x 32 words) | segk (S)
+  const size_t filter_lds = sizeof(uint32_t) * ((size_t)kMiscWords + 2 * (size_t)W64 +
+                                                (size_t)S * kSegWords * 2 + (size_t)S);
   if (filter_lds > 160 * 1024)
     return set_error(ctx, PAS_ECAPACITY,
                      "pas_tas_eval: n_nodes too large for the LDS bitmaps (max ~620k nodes)");
@@ -574,7 +637,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
       align256(sizeof(int32_t) * (size_t)std::max<int64_t>(max_segs, 1)),
       prio ? align256(sizeof(int32_t) * (size_t)n_pods * S) : 0,
       prio ? align256(sizeof(uint64_t) * (size_t)n_pods * D64) : 0,
-      align256(sizeof(int4) * (size_t)n_pods)};
+      align256(sizeof(int4) * 2 * (size_t)std::max(n_pods, 1))};
   size_t need = 0;
   for (size_t b : sizes) need += b;
   if (need > ctx->aux_bytes) {
@@ -611,8 +674,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     PAS_HIP(ctx, hipGetLastError());
   }
 
-  GroupParams gp{n_pods, M, N, flags, d_prio, t.cnt, d_list, d_gs, d_ss, d_sg,
-                 (int32_t)max_segs};
+  GroupParams gp{n_pods, M,    N,    flags, d_prio, d_rule_off,         t.cnt,
+                 d_list, d_gs, d_ss, d_sg,  d_desc, (int32_t)max_segs};
   const size_t group_lds = sizeof(int32_t) * ((size_t)kGroupTpb + G + 1);
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_group_kernel),
@@ -631,27 +694,39 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   fp.W64 = W64;
   fp.D64 = D64;
   fp.S = S;
+  fp.Nr = t.rank_stride;
+  fp.rank = t.rank;
   fp.flags = flags;
-  fp.rule_off = d_rule_off;
   fp.ranges = d_ranges;
   fp.rules = d_rules;
-  fp.prio = d_prio;
   fp.cand = d_cand;
   fp.perm = t.perm;
-  fp.rank = t.rank;
-  fp.cnt = t.cnt;
-  fp.pod_list = d_list;
   fp.pass_out = d_pass;
   fp.drop = d_drop;
   fp.seg_base = d_sb;
   fp.order_len = d_len;
   fp.desc = d_desc;
   if (filter_lds > 64 * 1024)
-    PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_filter_kernel),
-                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)filter_lds));
+    for (const void* f : {reinterpret_cast<const void*>(&tas_filter_kernel<0>),
+                          reinterpret_cast<const void*>(&tas_filter_kernel<1>),
+                          reinterpret_cast<const void*>(&tas_filter_kernel<2>),
+                          reinterpret_cast<const void*>(&tas_filter_kernel<4>),
+                          reinterpret_cast<const void*>(&tas_filter_kernel<8>)})
+      PAS_HIP(ctx, hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)filter_lds));
   timing_begin(ctx, s, PAS_K_TAS_FILTER, &tl);
-  tas_filter_kernel<<<n_pods, kTpb, filter_lds, s>>>(fp);
+  static const int filter_ablate = [] {
+    const char* e = std::getenv("PAS_FILTER_ABLATE");
+    return e ? std::atoi(e) : 0;
+  }();
+  const unsigned fblocks = (unsigned)n_pods;
+  switch (filter_ablate) {
+    case 1: tas_filter_kernel<1><<<fblocks, kTpb, filter_lds, s>>>(fp); break;
+    case 2: tas_filter_kernel<2><<<fblocks, kTpb, filter_lds, s>>>(fp); break;
+    case 4: tas_filter_kernel<4><<<fblocks, kTpb, filter_lds, s>>>(fp); break;
+    case 8: tas_filter_kernel<8><<<fblocks, kTpb, filter_lds, s>>>(fp); break;
+    default: tas_filter_kernel<0><<<fblocks, kTpb, filter_lds, s>>>(fp); break;
+  }
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
 

@@ -44,8 +44,8 @@ __global__ void popc_words(const uint64_t* __restrict__ present, int64_t total_w
 // perm[2][m][pos] = n, rank[2][m][n] = pos, vals_c[m][pos] = vals[m][n].
 __global__ void compact_present(const uint64_t* __restrict__ present,
                                 const int64_t* __restrict__ vals,
-                                const uint32_t* __restrict__ scan, int32_t N, int32_t M,
-                                int64_t W, int32_t* __restrict__ perm_index,
+                                const uint32_t* __restrict__ scan, int32_t N, int32_t Nr,
+                                int32_t M, int64_t W, int32_t* __restrict__ perm_index,
                                 uint32_t* __restrict__ rank_index,
                                 int64_t* __restrict__ vals_c) {
   const int64_t i = (int64_t)blockIdx.x * kTpb + threadIdx.x;
@@ -61,7 +61,7 @@ __global__ void compact_present(const uint64_t* __restrict__ present,
     bits &= bits - 1;
     const int32_t n = (int32_t)(lo + b);
     perm_index[col + pos] = n;
-    rank_index[col + n] = pos;
+    rank_index[m * (int64_t)Nr + n] = pos;
     vals_c[col + pos] = vals[col + n];
     ++pos;
   }
@@ -80,12 +80,11 @@ __global__ void segment_bounds(const uint32_t* __restrict__ scan, int32_t N, int
 
 // rank[o][m][perm[o][m][k]] = k for k < cnt[m]
 __global__ void invert_order(const int32_t* __restrict__ perm, const int32_t* __restrict__ cnt,
-                             int32_t N, uint32_t* __restrict__ rank) {
+                             int32_t N, int32_t Nr, uint32_t* __restrict__ rank) {
   const int m = blockIdx.y;
   const int32_t k = blockIdx.x * kTpb + threadIdx.x;
   if (k >= cnt[m]) return;
-  const int64_t col = (int64_t)m * N;
-  rank[col + perm[col + k]] = (uint32_t)k;
+  rank[(int64_t)m * Nr + perm[(int64_t)m * N + k]] = (uint32_t)k;
 }
 
 }  // namespace
@@ -96,7 +95,9 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
   t.valid = false;
   const int64_t W = w64(N);
   const int64_t MN = (int64_t)M * N;
-  if (MN > 0x7fffffffLL)
+  const int32_t Nr = (int32_t)rank_row(N);
+  const int64_t MNr = (int64_t)M * Nr;
+  if (MNr > 0x7fffffffLL)
     return set_error(ctx, PAS_ECAPACITY, "TAS snapshot: n_metrics * n_nodes must be < 2^31");
   if (t.n_nodes != N || t.n_metrics != M || !t.cnt) {
     PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -110,7 +111,8 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     PAS_HIP(ctx, hipMalloc(&t.sorted, sizeof(int64_t) * mn));
     // +1024 entries: the emit loader reads whole 1024-position segments unconditionally
     PAS_HIP(ctx, hipMalloc(&t.perm, sizeof(int32_t) * (mn * kNumOrders + 1024)));
-    PAS_HIP(ctx, hipMalloc(&t.rank, sizeof(uint32_t) * mn * kNumOrders));
+    PAS_HIP(ctx, hipMalloc(&t.rank,
+                           sizeof(uint32_t) * (size_t)std::max<int64_t>(MNr, 1) * kNumOrders));
     PAS_HIP(ctx, hipMalloc(&t.vals_c, sizeof(int64_t) * mn));
     PAS_HIP(ctx, hipMalloc(&t.word_scan, sizeof(uint32_t) * (mw + 1)));
     PAS_HIP(ctx, hipMalloc(&t.seg_begin, sizeof(int32_t) * mm));
@@ -131,6 +133,7 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     PAS_HIP(ctx, hipMalloc(&t.scan_tmp, t.scan_tmp_bytes));
     t.n_nodes = N;
     t.n_metrics = M;
+    t.rank_stride = Nr;
   }
   if (MN > 0) {
     if (d_vals != t.vals)
@@ -140,7 +143,7 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
       PAS_HIP(ctx, hipMemcpyAsync(t.present, d_present, sizeof(uint64_t) * M * W,
                                   hipMemcpyDeviceToDevice, s));
     const int64_t mw = (int64_t)M * W;
-    // popcounts into rank (scratch at this point), then scan into word_scan
+    // popcounts into rank (scratch at this point; MNr >= M*W + 1), then scan into word_scan
     uint32_t* popc = t.rank;
     popc_words<<<(unsigned)((mw + 1 + kTpb - 1) / kTpb), kTpb, 0, s>>>(t.present, mw, N, W,
                                                                          popc);
@@ -148,13 +151,13 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     size_t scan_bytes = t.scan_tmp_bytes;
     PAS_HIP(ctx, rocprim::exclusive_scan(t.scan_tmp, scan_bytes, popc, t.word_scan, 0u,
                                          (size_t)(mw + 1), rocprim::plus<uint32_t>(), s));
-    PAS_HIP(ctx, hipMemsetAsync(t.rank, 0xFF, sizeof(uint32_t) * MN * kNumOrders, s));
+    PAS_HIP(ctx, hipMemsetAsync(t.rank, 0xFF, sizeof(uint32_t) * MNr * kNumOrders, s));
     int32_t* perm_asc = t.perm + (size_t)kOrderAsc * MN;
     int32_t* perm_desc = t.perm + (size_t)kOrderDesc * MN;
     int32_t* perm_index = t.perm + (size_t)kOrderIndex * MN;
     compact_present<<<(unsigned)((mw + kTpb - 1) / kTpb), kTpb, 0, s>>>(
-        t.present, t.vals, t.word_scan, N, M, W, perm_index,
-        t.rank + (size_t)kOrderIndex * MN, t.vals_c);
+        t.present, t.vals, t.word_scan, N, Nr, M, W, perm_index,
+        t.rank + (size_t)kOrderIndex * MNr, t.vals_c);
     PAS_HIP(ctx, hipGetLastError());
     segment_bounds<<<(M + kTpb - 1) / kTpb, kTpb, 0, s>>>(t.word_scan, N, M, W, t.cnt,
                                                         t.seg_begin, t.seg_end);
@@ -169,9 +172,10 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
                      t.sort_tmp, sort_bytes, t.vals_c, t.sorted, perm_index, perm_asc,
                      (unsigned)MN, (unsigned)M, t.seg_begin, t.seg_end, 0, 64, s));
     const dim3 grid((unsigned)((N + kTpb - 1) / kTpb), (unsigned)M);
-    invert_order<<<grid, kTpb, 0, s>>>(perm_asc, t.cnt, N, t.rank + (size_t)kOrderAsc * MN);
+    invert_order<<<grid, kTpb, 0, s>>>(perm_asc, t.cnt, N, Nr, t.rank + (size_t)kOrderAsc * MNr);
     PAS_HIP(ctx, hipGetLastError());
-    invert_order<<<grid, kTpb, 0, s>>>(perm_desc, t.cnt, N, t.rank + (size_t)kOrderDesc * MN);
+    invert_order<<<grid, kTpb, 0, s>>>(perm_desc, t.cnt, N, Nr,
+                                        t.rank + (size_t)kOrderDesc * MNr);
     PAS_HIP(ctx, hipGetLastError());
   }
   t.gen = gen;
