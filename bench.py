@@ -27,53 +27,12 @@ sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
 
 import pas_amd  # noqa: E402
 from pas_amd import _lib  # noqa: E402
+from pas_amd import distrib  # noqa: E402
+from pas_amd.distrib import timed_steps, whole_job_rate  # noqa: E402
 from pas_amd import workload as wl  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "pod-node evals/sec (filter+prioritize), 4k pods×100k nodes; % of HBM peak"
-
-
-def dist_setup(n_gpus):
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-    return world, rank, local
-
-
-def barrier(world):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-
-
-def max_over_ranks(x, world):
-    if world == 1:
-        return x
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def timed_steps(step, steps, warmup, world):
-    for _ in range(warmup):
-        step()
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step()
-    torch.cuda.synchronize()
-    barrier(world)
-    t1 = time.perf_counter()
-    return max_over_ranks(t1 - t0, world)
 
 
 def dev(a):
@@ -98,7 +57,7 @@ def bench_tas(args, world, rank):
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
     snap = wl.make_tas_snapshot(N, M, seed=0xC2)
-    batch = wl.make_tas_batch(snap, P, R, seed=0xC2 + 7919 * rank)
+    batch = wl.make_tas_batch(snap, P, R, seed=distrib.batch_seed(0xC2, rank))
     v_t, p_t = dev(snap.v_milli), dev(snap.present.view(np.int64))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -137,8 +96,7 @@ def bench_tas(args, world, rank):
     alg_bytes = 8 * M * N + 8 * M * w + 8 * P * w + 4 * sum_len + 4 * P + 16 * (n_rules + P)
     kernel_s = sum(kern.values()) / 1e3
     achieved = alg_bytes / kernel_s / 1e9
-    evals = P * N * world
-    value = evals * args.steps / elapsed
+    value = whole_job_rate(P * N, world, args.steps, elapsed)
     traffic = load_traffic("tas_path")
     out = {
         "metric": METRIC,
@@ -208,7 +166,7 @@ def bench_gas(args, world, rank):
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
     snap = wl.make_gas_snapshot(N, seed=0xC3)
-    batch = wl.make_gas_batch(P, seed=0xC3 + 7919 * rank)
+    batch = wl.make_gas_batch(P, seed=distrib.batch_seed(0xC3, rank))
     K, Q = snap.used.shape[1], snap.used.shape[2]
     C = batch.req.shape[1]
     ctx.gas_snapshot_set_device(1, N, K, Q, dev(snap.n_cards), dev(snap.cap), dev(snap.used),
@@ -232,7 +190,7 @@ def bench_gas(args, world, rank):
     achieved = alg_bytes / kernel_s / 1e9
     out = {
         "metric": "GAS per-card fit evals/sec (pod-node fits), 10k pods×50k nodes×8 cards",
-        "value": P * N * world * args.steps / elapsed, "unit": "pod-node fits/s",
+        "value": whole_job_rate(P * N, world, args.steps, elapsed), "unit": "pod-node fits/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C3)",
@@ -292,7 +250,8 @@ def bench_deschedule(args, world, rank):
     achieved = alg_bytes / kernel_s / 1e9
     out = {
         "metric": "TAS deschedule sweep node-rule evals/sec, 1M nodes×64 rules per GPU",
-        "value": N * len(rules) * world * args.steps / elapsed, "unit": "node-rule evals/s",
+        "value": whole_job_rate(N * len(rules), world, args.steps, elapsed),
+        "unit": "node-rule evals/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C4)",
@@ -324,14 +283,12 @@ def main():
     dp, dn = defaults[args.workload]
     args.pods = args.pods or dp
     args.nodes = args.nodes or dn
-    world, rank, _ = dist_setup(args.gpus)
+    world, rank, _ = distrib.setup()
     fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule}[args.workload]
     out = fn(args, world, rank)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
+    distrib.teardown(world)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,97 @@
+"""Process-per-GPU plumbing for bench.py: rendezvous, barriers, max-over-ranks timing.
+
+The TAS/GAS batches shard by pod (every pending pod is scheduled independently against
+the same snapshot, telemetryscheduler.go:184-225 and gpuscheduler/scheduler.go:449-482 take
+one pod per request), so N ranks run N independent batches with no data-path collective.
+The only cross-rank traffic is the timing protocol below: a barrier on both sides of the
+timed region and an all-reduce(MAX) of the elapsed time.  The same code runs over RCCL
+("nccl") on GPUs and over gloo on CPU in the tests.
+"""
+import os
+import time
+
+import torch
+
+
+def setup(backend=None):
+    """Read RANK/LOCAL_RANK/WORLD_SIZE (torchrun) and join the process group when N > 1.
+
+    backend None picks "nccl" (RCCL) when HIP devices are visible, else "gloo"."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    gpu = backend != "gloo" and torch.cuda.is_available()
+    if gpu:
+        torch.cuda.set_device(local if world > 1 else 0)
+    if world > 1:
+        import torch.distributed as dist
+        if backend is None:
+            backend = "nccl" if gpu else "gloo"
+        kw = {"device_id": torch.device("cuda", local)} if backend == "nccl" else {}
+        dist.init_process_group(backend=backend, **kw)
+    return world, rank, local
+
+
+def teardown(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def _device():
+    import torch.distributed as dist
+    return "cuda" if dist.get_backend() == "nccl" else "cpu"
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x, world):
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=_device())
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def gather_objects(obj, world):
+    """All ranks' `obj`, in rank order (tests and result checks only)."""
+    if world == 1:
+        return [obj]
+    import torch.distributed as dist
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def timed_steps(step, steps, warmup, world, sync=None):
+    """Run `warmup` untimed steps, then time exactly `steps` steps bracketed by
+    sync + barrier on both sides; returns the MAX elapsed seconds over ranks."""
+    if sync is None:
+        sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier(world)
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier(world)
+    t1 = time.perf_counter()
+    return max_over_ranks(t1 - t0, world)
+
+
+def whole_job_rate(units_per_rank_per_step, world, steps, elapsed_s):
+    """bench.py's `value`: units ALL ranks processed / the max-over-ranks wall time."""
+    return units_per_rank_per_step * world * steps / elapsed_s
+
+
+def batch_seed(base, rank):
+    """Seed of rank `rank`'s independent pod batch (weak scaling: same size per rank)."""
+    return base + 7919 * rank

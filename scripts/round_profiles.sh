@@ -1,0 +1,18 @@
+#!/bin/bash
+# Round-end evidence: all GPU tests, the three bench workloads (default tas line with the CPU
+# baseline), and rocprofv3 kernel-trace/stats + PMC passes per workload into gpurun_out/.
+set -u
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -m gpu -q --timeout 600 -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+if [ $rc -ne 0 ]; then exit $rc; fi
+timeout -k 10 400 python bench.py > gpurun_out/bench_tas.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_tas.log
+for w in gas deschedule; do
+  timeout -k 10 400 python bench.py --workload $w --steps 20 --warmup 3 > gpurun_out/bench_$w.log 2>&1 || exit $?
+  tail -1 gpurun_out/bench_$w.log
+done
+for w in tas gas deschedule; do
+  bash scripts/profile.sh $w $w || exit $?
+done
