@@ -364,11 +364,20 @@ static int check_tas_gen(pas_ctx* ctx, uint64_t gen) {
 // Host-side rule validation: an unknown operator string panics in core.EvaluateRule
 // (operator.go:25) only when the rule is evaluated, i.e. when its metric is cached
 // (dontschedule/strategy.go:28-32 skips missing metrics first).  Here: PAS_EINVAL.
+// An unknown operator panics in the reference only when EvaluateRule runs, i.e. when the
+// rule's metric map has at least one node (dontschedule/strategy.go:33-41, operator.go:25);
+// otherwise the rule is never evaluated.  The column count is read back only in that
+// (rare) case.  The *_device entry points do not validate: their callers parse operators
+// with pas_parse_operator when the policy is built, and the kernels skip unknown ones.
 static int validate_rules(pas_ctx* ctx, int32_t n, const pas_rule* rules) {
   for (int32_t i = 0; i < n; ++i) {
     const pas_rule& r = rules[i];
     if (r.op >= 0 && r.op <= 2) continue;
     if (r.metric < 0 || r.metric >= ctx->tas.n_metrics) continue;  // never evaluated
+    int32_t c = 0;
+    PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    PAS_HIP(ctx, hipMemcpy(&c, ctx->tas.cnt + r.metric, sizeof(c), hipMemcpyDeviceToHost));
+    if (c == 0) continue;  // empty metric map: no EvaluateRule call
     return set_error(ctx, PAS_EINVAL, "rule " + std::to_string(i) + ": unknown operator " +
                                           std::to_string(r.op) +
                                           " (the reference panics in EvaluateRule)");

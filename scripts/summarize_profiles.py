@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""gpurun_out/prof_<workload>/ (scripts/profile.sh) -> profiles/<round>_<workload>_*.
+
+Writes per workload:
+  <round>_<w>_kernel_stats.csv  rocprofv3 --kernel-trace --stats summary, short kernel names
+  <round>_<w>_pmc.csv           per-kernel average PMC values per launch
+and updates profiles/traffic.json with HBM bytes per launch of the bench's dominant kernel(s):
+  bytes = 2 * FETCH_SIZE + WRITE_SIZE  (KB -> bytes).  FETCH_SIZE on gfx950 reports half the
+  bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for
+  16-B stores; Infinity-Cache hits are counted in FETCH_SIZE.
+usage: summarize_profiles.py <round> [workload ...]
+"""
+import csv
+import json
+import os
+import re
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "profiles")
+TAS_PATH = ("tas_ranges_kernel", "tas_group_kernel", "tas_filter_kernel", "tas_emit_kernel")
+
+
+def short(name):
+    m = re.search(r"(?:anonymous namespace\)::|pas::)(\w+)", name)
+    if m:
+        return m.group(1)
+    if "rocprim" in name:
+        kind = re.search(r"detail::(\w+?)(?:_impl|_config|<)", name)
+        return "rocprim::" + (kind.group(1) if kind else "kernel")
+    return name.split("(")[0][-60:]
+
+
+def kernel_stats(d):
+    rows = []
+    with open(os.path.join(d, "kt", "kt_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            rows.append({"kernel": short(r["Name"]), "calls": int(r["Calls"]),
+                         "total_us": float(r["TotalDurationNs"]) / 1e3,
+                         "avg_us": float(r["AverageNs"]) / 1e3,
+                         "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3,
+                         "pct": float(r["Percentage"])})
+    return rows
+
+
+def pmc(d):
+    agg = defaultdict(list)
+    for sub in os.listdir(d):
+        f = os.path.join(d, sub, "pmc_counter_collection.csv")
+        if not sub.startswith("pmc_") or not os.path.exists(f):
+            continue
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                agg[(short(r["Kernel_Name"]), r["Counter_Name"])].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}
+
+
+def main():
+    rnd = sys.argv[1]
+    wls = sys.argv[2:] or ["tas", "gas", "deschedule"]
+    os.makedirs(OUT, exist_ok=True)
+    tpath = os.path.join(OUT, "traffic.json")
+    traffic = json.load(open(tpath)) if os.path.exists(tpath) else {}
+    for w in wls:
+        d = os.path.join(ROOT, "gpurun_out", f"prof_{w}")
+        rows = kernel_stats(d)
+        with open(os.path.join(OUT, f"{rnd}_{w}_kernel_stats.csv"), "w", newline="") as f:
+            wr = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
+            wr.writeheader()
+            wr.writerows(rows)
+        p = pmc(d)
+        kernels = sorted({k for k, _ in p})
+        counters = sorted({c for _, c in p})
+        with open(os.path.join(OUT, f"{rnd}_{w}_pmc.csv"), "w", newline="") as f:
+            wr = csv.writer(f)
+            wr.writerow(["kernel"] + counters + ["hbm_bytes_per_launch"])
+            for k in kernels:
+                vals = [p.get((k, c), "") for c in counters]
+                b = 1024 * (2 * p.get((k, "FETCH_SIZE"), 0) + p.get((k, "WRITE_SIZE"), 0))
+                wr.writerow([k] + vals + [round(b)])
+
+        def hbm(k):
+            return 1024 * (2 * p.get((k, "FETCH_SIZE"), 0) + p.get((k, "WRITE_SIZE"), 0))
+        if w == "tas":
+            traffic["tas_path"] = round(sum(hbm(k) for k in TAS_PATH))
+            traffic["tas_path_by_kernel"] = {k: round(hbm(k)) for k in TAS_PATH}
+        elif w == "gas":
+            traffic["gas_fit_kernel"] = round(hbm("gas_fit_kernel") + hbm("gas_prep_kernel"))
+        elif w == "deschedule":
+            traffic["tas_violations_kernel"] = round(hbm("tas_violations_kernel"))
+        print(w, "->", [r["kernel"] + f" {r['avg_us']:.1f}us x{r['calls']}" for r in rows[:8]])
+    traffic["_source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, round {rnd}; "
+                          "bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB->B)")
+    with open(tpath, "w") as f:
+        json.dump(traffic, f, indent=1)
+    print(json.dumps(traffic, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -318,3 +318,22 @@ def test_errors(ctx):
     with pytest.raises(pas_amd.PasError) as e:
         ctx.tas_eval(gen, pas_amd.make_rules([0], [0], [1]), np.array([1, 1], np.int32), prio)
     assert e.value.code == -1
+
+
+def test_unknown_operator_on_empty_metric_map(ctx, oracle):
+    """A cached metric with no node entries: Violated ranges over an empty map, so
+    EvaluateRule (and its panic on an unknown operator, operator.go:25) never runs."""
+    n = 300
+    v = np.arange(2 * n, dtype=np.int64).reshape(2, n) * 1000
+    present = np.ones((2, n), bool)
+    present[1] = False
+    pres = wl.pack_bits(present)
+    gen = upload(ctx, v, pres)
+    rules = pas_amd.make_rules([1, 0], [9, 1], [0, 100])
+    off = np.array([0, 2], np.int32)
+    prio = pas_amd.make_rules([0], [0], [0])
+    got = ctx.tas_eval(gen, rules, off, prio)
+    want = oracle.tas_eval(v, pres, rules, off, prio, None, 3)
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[2], want[2])
+    np.testing.assert_array_equal(got[1][0, :got[2][0]], want[1][0, :want[2][0]])
