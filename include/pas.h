@@ -229,7 +229,8 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
 #define PAS_K_GAS_FIT 4        /* per (pod, node) first fit */
 #define PAS_K_TAS_GROUP 5      /* bucket pods by prioritize order */
 #define PAS_K_TAS_EMIT 6       /* ordered host lists */
-#define PAS_K_COUNT 7
+#define PAS_K_TAS_SPAN 7       /* whole pas_tas_eval path: first launch start to last launch end */
+#define PAS_K_COUNT 8
 int pas_set_timing(pas_ctx* ctx, int enable);
 /* Sum of elapsed ms and number of launches recorded for a kernel since the last reset. */
 int pas_kernel_time(pas_ctx* ctx, int32_t kernel_id, double* total_ms, int64_t* launches);

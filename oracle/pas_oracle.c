@@ -51,9 +51,10 @@ int or_violated(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
   memset(violating, 0, (size_t)n_nodes);
   for (int32_t r = 0; r < n_rules; ++r) {            /* for _, rule := range d.Rules */
     const or_rule* rule = &rules[r];
-    if (rule->op < 0 || rule->op > 2) return -1;
     if (!metric_in_cache(n_nodes, n_metrics, present, rule->metric))
       continue;                                      /* ReadMetric err -> continue :28-32 */
+    if (rule->op < 0 || rule->op > 2)
+      return -1; /* EvaluateRule runs for >= 1 node of the map: panic (operator.go:25) */
     const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
     const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
     for (int32_t n = 0; n < n_nodes; ++n) {          /* for nodeName, nodeMetric := range */

@@ -665,7 +665,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   uint64_t* d_drop = reinterpret_cast<uint64_t*>(parts[6]);
   int4* d_desc = reinterpret_cast<int4*>(parts[7]);
 
-  TimedLaunch tl;
+  TimedLaunch span, tl;
+  timing_begin(ctx, s, PAS_K_TAS_SPAN, &span);
   if ((flags & PAS_TAS_FILTER) && n_rules > 0) {
     timing_begin(ctx, s, PAS_K_TAS_RANGES, &tl);
     tas_ranges_kernel<<<(n_rules + kTpb - 1) / kTpb, kTpb, 0, s>>>(n_rules, d_rules, t.cnt,
@@ -750,6 +751,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
       PAS_HIP(ctx, hipGetLastError());
     }
   }
+  timing_end(ctx, s, &span);
   return PAS_OK;
 }
 

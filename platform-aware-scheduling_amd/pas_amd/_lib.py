@@ -52,6 +52,7 @@ PAS_K_GAS_PREP = 3
 PAS_K_GAS_FIT = 4
 PAS_K_TAS_GROUP = 5
 PAS_K_TAS_EMIT = 6
+PAS_K_TAS_SPAN = 7
 KERNEL_NAMES = {
     PAS_K_TAS_RANGES: "tas_ranges_kernel",
     PAS_K_TAS_FILTER: "tas_filter_kernel",
@@ -60,6 +61,7 @@ KERNEL_NAMES = {
     PAS_K_GAS_FIT: "gas_fit_kernel",
     PAS_K_TAS_GROUP: "tas_group_kernel",
     PAS_K_TAS_EMIT: "tas_emit_kernel",
+    PAS_K_TAS_SPAN: "tas_eval_span",
 }
 
 

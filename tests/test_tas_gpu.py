@@ -172,6 +172,19 @@ def test_random_parity_ties_and_dense_violations(ctx, oracle, seed):
     assert_same(ctx, oracle, v, pres, rules, off, prio, cand, 3)
 
 
+@pytest.mark.parametrize("p", [1024, 1101])
+def test_random_parity_large_batches(ctx, oracle, p):
+    """Batches of ~1k pods over few metrics: large buckets (hundreds of pods per order
+    column, so many 16-pod emit rounds per segment), with and without candidate masks."""
+    rng = np.random.default_rng(p)
+    for cand_frac in (None, 0.8):
+        v, pres, rules, off, prio, cand = random_case(
+            rng, 2000, 3, p, 6, tie_vals=[0, 1000, 2000, 3000, -4000] if cand_frac else None,
+            cand_frac=cand_frac)
+        assert_same(ctx, oracle, v, pres, rules, off, prio, cand, 3)
+        assert_same(ctx, oracle, v, pres, rules, off, prio, cand, 2)
+
+
 def test_many_rules_per_pod_chunked(ctx, oracle):
     # more than the kernel's 64-rule LDS chunk
     rng = np.random.default_rng(7)
