@@ -241,6 +241,7 @@ struct FilterParams {
 };
 
 typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
+typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int32_t wave_inclusive_sum(int32_t x) {
   const int lane = threadIdx.x & 63;
@@ -444,24 +445,24 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
 
 // ---------------------------------------------------------------------------- emit
 
-constexpr int kEmitBatch = 16;                                   // pods fetched per round
+constexpr int kEmitBatch = 16;                                   // pods per LDS fetch round
 constexpr int kStageWords = ((kSegPos + 31 + 255) / 256) * 256;  // 5 x 256 (unrolled reads)
-
-// Non-temporal stores: measured on MI355X for this write pattern (3.7 KB runs in 4096
-// rows), aligned 16-byte nt stores sustain ~5.3 TB/s against ~3.7 TB/s for plain stores
-// and ~3.0 TB/s for unaligned dword nt stores (scripts/diag/write_pattern.hip).
-__device__ __forceinline__ void st_nt16(int32_t* p, v4i32 v) {
-  __builtin_nontemporal_store(v, reinterpret_cast<v4i32*>(p));
-}
+constexpr int kDumpSlot = kStageWords - 1;  // compaction target of dropped lanes (> 1055)
+constexpr uint32_t kOob = 0x80000000u;      // buffer offset past every range: no access
+constexpr int kNtAux = 2;                   // buffer store cache policy: nt
 
 // One wave per (bucket, 1024-position segment): the permutation segment is read once into
 // registers and written, compacted by each pod's drop bits, for every pod of the bucket.
-// Pods are taken in batches of 16: one round of vector loads fetches their ids, segment
-// bases and drop words into the wave's LDS; the store phase then runs without loads.  Each
-// pod's kept entries are compacted (mbcnt) into an LDS stage aligned to the destination's
-// 16-byte grid and written with 16-byte nt stores (dword nt stores for the two partial end
-// chunks).  Waves of a block take different buckets, so no block barrier is used: a wave
-// only touches its own LDS slices, whose operations execute in program order.
+// Per pod (ids, bases and drop words of 16 pods are fetched into LDS in one round):
+//   compaction  16 x (mbcnt, one unconditional LDS write: dropped lanes write a dump slot)
+//               into a stage aligned to the destination's 128-byte lines;
+//   stores      range-checked buffer stores against a descriptor of the pod's run: every
+//               chunk of whole lines takes an nt 16-byte store, the other full chunks a
+//               plain one, the <= 2 partial chunks dword stores; a lane with nothing to
+//               store passes an out-of-range offset, so there are no per-lane branches.
+// Measured (scripts/diag/fill_shapes.py): the HBM write rate follows the number of
+// stores in flight, so the per-pod instruction count between store bursts is what this
+// layout minimises.  Waves of a block take different buckets and never synchronise.
 // kAblate (diagnostic timing builds only, PAS_EMIT_ABLATE; outputs wrong): 1 = no stores.
 template <int kAblate>
 __global__ __launch_bounds__(kTpb) void tas_emit_kernel(
@@ -473,13 +474,13 @@ __global__ __launch_bounds__(kTpb) void tas_emit_kernel(
     int32_t* __restrict__ order_out) {
   __shared__ __attribute__((aligned(16))) int32_t stage_all[kWaves][kStageWords];
   __shared__ __attribute__((aligned(16))) uint64_t dbuf_all[kWaves][kEmitBatch][kSegWords];
-  __shared__ int32_t pbuf_all[kWaves][kEmitBatch];
-  __shared__ int32_t bbuf_all[kWaves][kEmitBatch];
+  __shared__ int32_t pods_all[kWaves][kEmitBatch];
+  __shared__ int32_t bases_all[kWaves][kEmitBatch];
   const int wave = threadIdx.x >> 6;
   int32_t* stage = stage_all[wave];
   uint64_t(*dbuf)[kSegWords] = dbuf_all[wave];
-  int32_t* pbuf = pbuf_all[wave];
-  int32_t* bbuf = bbuf_all[wave];
+  int32_t* pods = pods_all[wave];
+  int32_t* bases = bases_all[wave];
   const int32_t gw = __builtin_amdgcn_readfirstlane((int32_t)(blockIdx.x * kWaves + wave));
   const int lane = threadIdx.x & 63;
   if (gw >= total_segs_bound) return;
@@ -498,46 +499,58 @@ __global__ __launch_bounds__(kTpb) void tas_emit_kernel(
     node[j] = kk < cnt0 ? pm[kk] : 0;
   }
   const bool full = (s + 1) * kSegPos <= cnt0;  // only a bucket's last segment has a tail
-  const int32_t i1 = group_start[g + 1];
-  for (int32_t i0 = group_start[g]; i0 < i1; i0 += kEmitBatch) {
-    const int32_t nb = min(kEmitBatch, i1 - i0);
-    // ---- fetch round: ids, bases, drop words of up to 16 pods ----
-    const int32_t mypod = lane < nb ? pod_list[i0 + lane] : 0;
-    const int pidx = lane >> 2;  // 4 lanes x 32 bytes per pod
-    const int32_t dpod = __shfl(mypod, pidx, 64);
-    if (pidx < nb) {
-      const int4* src = reinterpret_cast<const int4*>(drop + (int64_t)dpod * D64 +
-                                                      s * kSegWords + (lane & 3) * 4);
-      int4* dst = reinterpret_cast<int4*>(&dbuf[pidx][(lane & 3) * 4]);
-      dst[0] = src[0];
-      dst[1] = src[1];
-    }
-    if (lane < nb) {
-      pbuf[lane] = mypod;
-      bbuf[lane] = seg_base[(int64_t)mypod * S + s];
+
+  const int32_t i0 = group_start[g], i1 = group_start[g + 1];
+  // Pods in batches of 16: one round of vector loads puts their ids, segment bases and
+  // drop words into the wave's LDS (its wait is the only vmcnt wait of a batch); the pod
+  // loop then reads LDS only, so up to 16 pods' stores stay in flight per wave.
+  for (int32_t ic = i0; ic < i1; ic += kEmitBatch) {
+    const int32_t nc = min(kEmitBatch, i1 - ic);
+    const int32_t my_pod = pod_list[ic + min(lane & (kEmitBatch - 1), nc - 1)];
+    const int pidx = lane >> 2;  // 4 lanes x 32 bytes of drop words per pod
+    const int32_t dpod = __shfl(my_pod, pidx, 64);
+    const int4* src = reinterpret_cast<const int4*>(drop + (int64_t)dpod * D64 +
+                                                    s * kSegWords + (lane & 3) * 4);
+    const int4 d0 = src[0], d1 = src[1];
+    const int32_t my_base = seg_base[(int64_t)my_pod * S + s];
+    int4* dst = reinterpret_cast<int4*>(&dbuf[pidx][(lane & 3) * 4]);
+    dst[0] = d0;
+    dst[1] = d1;
+    if (lane < kEmitBatch) {
+      pods[lane] = my_pod;
+      bases[lane] = my_base;
     }
     __builtin_amdgcn_wave_barrier();
-    // ---- store phase: no memory loads below ----
-    for (int32_t p = 0; p < nb; ++p) {
-      const int32_t pod = pbuf[p];
-      const int32_t base = bbuf[p];
+    for (int32_t q = 0; q < nc; ++q) {
+      const int32_t pod = __builtin_amdgcn_readfirstlane(pods[q]);
+      const int32_t base = __builtin_amdgcn_readfirstlane(bases[q]);
+      uint64_t dw[kSegWords];
+#pragma unroll
+      for (int j = 0; j < kSegWords; ++j) {
+        const uint64_t x = dbuf[q][j];  // broadcast read
+        dw[j] = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(x >> 32)) << 32) |
+                (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)x);
+      }
+
       const int64_t gdst = (int64_t)pod * N + base;  // element index of the first entry
-      // stage aligned to the destination's 128-byte lines: every 1 KB store instruction
-      // then covers whole lines, which take nt stores; only the run's first and last
-      // line (shared with the neighbouring runs) go through L2 with plain stores
-      const int32_t a = (int32_t)(gdst & 31);
+      const int32_t a = (int32_t)(gdst & 31);         // stage offset: 128-B line alignment
       int32_t k = a;
 #pragma unroll
       for (int j = 0; j < kSegWords; ++j) {
-        const uint64_t keep =
-            ~dbuf[p][j] & (full ? ~0ull : tail_mask64(s * kSegWords + j, cnt0));
+        const uint64_t keep = ~dw[j] & (full ? ~0ull : tail_mask64(s * kSegWords + j, cnt0));
         const uint32_t below = __builtin_amdgcn_mbcnt_hi(
             (uint32_t)(keep >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
-        if ((keep >> lane) & 1ull) stage[k + (int32_t)below] = node[j];
+        int32_t addr;  // per-lane select on the SGPR keep mask: k + below, or the dump slot
+        asm("v_cndmask_b32_e64 %0, %1, %2, %3"
+            : "=v"(addr)
+            : "v"(kDumpSlot), "v"(k + (int32_t)below), "s"(keep));
+        stage[addr] = node[j];
         k += __popcll(keep);
       }
       __builtin_amdgcn_wave_barrier();
-      int32_t* __restrict__ out = order_out + (gdst - a);  // 128-byte aligned
+      // the run [a, k) of the stage goes to order_out[gdst - a + a .. gdst - a + k)
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          order_out + (gdst - a), 0, k * 4, 0x00020000);
       constexpr int kChunkIters = kStageWords / 256;
       v4i32 v[kChunkIters];
 #pragma unroll
@@ -545,24 +558,35 @@ __global__ __launch_bounds__(kTpb) void tas_emit_kernel(
         v[it] = *reinterpret_cast<const v4i32*>(stage + (lane + it * 64) * 4);
       const int32_t full_lo = (a + 31) & ~31;  // first entry of the first whole line
       const int32_t full_hi = k & ~31;         // end of the last whole line
+      // the <= 2 partial chunks: lanes 0..3 the chunk holding a, lanes 4..7 the one holding
+      // k - 1 (the same chunk twice when both ends share it: same values, same addresses)
+      const int32_t pidx = lane < 4 ? (a & ~3) + lane : (k & ~3) + (lane - 4);
+      const bool pchunk_full = (pidx & ~3) >= a && (pidx & ~3) + 4 <= k;
+      const bool pvalid = lane < 8 && pidx >= a && pidx < k && !pchunk_full;
+      const int32_t pval = stage[pvalid ? pidx : 0];
+      if (kAblate == 1) {
 #pragma unroll
-      for (int it = 0; it < kChunkIters; ++it) {
-        const int32_t e0 = (lane + it * 64) * 4;
-        if (kAblate == 1 && gdst >= 0) {
+        for (int it = 0; it < kChunkIters; ++it)
           asm volatile("" ::"v"(v[it].x), "v"(v[it].y), "v"(v[it].z), "v"(v[it].w));
-        } else if (e0 >= full_lo && e0 + 4 <= full_hi) {
-          st_nt16(out + e0, v[it]);
-        } else if (e0 >= a && e0 + 4 <= k) {
-          *reinterpret_cast<v4i32*>(out + e0) = v[it];
-        } else if (e0 < k && e0 + 4 > a) {  // one of the two partial end chunks
-          if (e0 + 0 >= a && e0 + 0 < k) out[e0 + 0] = v[it].x;
-          if (e0 + 1 >= a && e0 + 1 < k) out[e0 + 1] = v[it].y;
-          if (e0 + 2 >= a && e0 + 2 < k) out[e0 + 2] = v[it].z;
-          if (e0 + 3 >= a && e0 + 3 < k) out[e0 + 3] = v[it].w;
+        asm volatile("" ::"v"(pval));
+      } else {
+#pragma unroll
+        for (int it = 0; it < kChunkIters; ++it) {
+          const int32_t e0 = (lane + it * 64) * 4;
+          const bool nt = e0 >= full_lo && e0 + 4 <= full_hi;
+          const bool plain = !nt && e0 >= a && e0 + 4 <= k;
+          const uint32_t off = (uint32_t)e0 * 4u;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v[it]), rsrc,
+                                                 nt ? off : kOob, 0, kNtAux);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v[it]), rsrc,
+                                                 plain ? off : kOob, 0, 0);
         }
+        __builtin_amdgcn_raw_buffer_store_b32((uint32_t)pval, rsrc,
+                                              pvalid ? (uint32_t)pidx * 4u : kOob, 0, 0);
       }
       __builtin_amdgcn_wave_barrier();
     }
+    __builtin_amdgcn_wave_barrier();  // the next batch rewrites pods/bases/drop words
   }
 }
 

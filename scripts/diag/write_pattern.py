@@ -23,3 +23,7 @@ for kind, wg, name, nbytes in ((0, 1024, "linear fill wg=1024", n * 4), (0, 4096
 for wg in (1024, 4096):
     lib.run3(ctypes.c_void_p(x.data_ptr()), wg, 20, ctypes.byref(ms))
     print(f"pieces NT dword wg={wg}: {ms.value:.3f} ms  {gb/ms.value*1e3:.0f} GB/s")
+for R in (1, 2, 4, 8, 98):
+    for wg in (2048, 8192):
+        lib.run4(ctypes.c_void_p(x.data_ptr()), wg, R, 20, ctypes.byref(ms))
+        print(f"runs of {R} pieces NT wg={wg}: {ms.value:.3f} ms  {gb/ms.value*1e3:.0f} GB/s")
