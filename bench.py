@@ -86,8 +86,7 @@ def bench_tas(args, world, rank):
     # per-step device time of each kernel, and the span of the whole path (HIP events on
     # the launch stream around the first and last launch)
     kern, launches = {}, {}
-    for kid in (_lib.PAS_K_TAS_RANGES, _lib.PAS_K_TAS_GROUP, _lib.PAS_K_TAS_FILTER,
-                _lib.PAS_K_TAS_EMIT):
+    for kid in (_lib.PAS_K_TAS_GROUP, _lib.PAS_K_TAS_FILTER, _lib.PAS_K_TAS_EMIT):
         ms, n = ctx.kernel_time(kid)
         kern[_lib.KERNEL_NAMES[kid]] = ms / args.steps
         launches[_lib.KERNEL_NAMES[kid]] = n // args.steps
@@ -126,8 +125,8 @@ def bench_tas(args, world, rank):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "tas path span: tas_ranges, tas_group, tas_filter, tas_emit on one stream "
-                      "(HIP events around the four launches)",
+            "kernel": "tas path span: tas_prep (pod grouping + rule ranges), tas_filter, "
+                      "tas_emit on one stream (HIP events around the three launches)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

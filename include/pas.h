@@ -222,12 +222,12 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
 
 /* Kernel timing with HIP events on the stream each kernel is launched on.
  * Kernel ids: */
-#define PAS_K_TAS_RANGES 0     /* rule -> violating range of the sorted metric */
+#define PAS_K_TAS_RANGES 0     /* (rule ranges now run inside the PAS_K_TAS_GROUP launch) */
 #define PAS_K_TAS_FILTER 1     /* per pod: pass bitmap, drop bitmap, segment bases */
 #define PAS_K_TAS_VIOLATIONS 2 /* deschedule sweep */
 #define PAS_K_GAS_PREP 3       /* per-GPU container requests */
 #define PAS_K_GAS_FIT 4        /* per (pod, node) first fit */
-#define PAS_K_TAS_GROUP 5      /* bucket pods by prioritize order */
+#define PAS_K_TAS_GROUP 5      /* prep: bucket pods by prioritize order + rule ranges */
 #define PAS_K_TAS_EMIT 6       /* ordered host lists */
 #define PAS_K_TAS_SPAN 7       /* whole pas_tas_eval path: first launch start to last launch end */
 #define PAS_K_COUNT 8

@@ -116,19 +116,28 @@ __device__ int32_t block_exclusive_scan(int32_t* a, int32_t n, int32_t* partial)
   return total;
 }
 
-// ---------------------------------------------------------------------------- ranges
+// ---------------------------------------------------------------------------- prep
+//
+// One launch, two roles: block 0 groups the pods (below); blocks 1.. map every rule to its
+// range (a3).  The two are independent, so the binary searches run beside the grouping.
 
-__global__ void tas_ranges_kernel(int32_t n_rules, const pas_rule* __restrict__ rules,
-                                  const int32_t* __restrict__ cnt,
-                                  const int64_t* __restrict__ sorted, int32_t N, int32_t M,
-                                  int2* __restrict__ ranges) {
-  const int32_t r = blockIdx.x * kTpb + threadIdx.x;
-  if (r >= n_rules) return;
-  const pas_rule rule = rules[r];
+struct RangesParams {
+  int32_t n_rules, N, M;
+  const pas_rule* rules;
+  const int32_t* cnt;
+  const int64_t* sorted;
+  int2* ranges;
+};
+
+// EvaluateRule (operator.go:13-26) over the ascending column: the nodes a rule selects form
+// one range, [lower_bound, upper_bound) of t*1000 for Equals, the prefix below it for
+// LessThan, the suffix above it for GreaterThan (t*1000 saturates).
+__device__ void ranges_body(const RangesParams& R, int32_t r) {
+  const pas_rule rule = R.rules[r];
   int2 out = make_int2(0, 0);
-  if (rule.metric >= 0 && rule.metric < M && rule.op >= 0 && rule.op <= 2) {
-    const int32_t c = cnt[rule.metric];
-    const int64_t* sv = sorted + (int64_t)rule.metric * N;
+  if (rule.metric >= 0 && rule.metric < R.M && rule.op >= 0 && rule.op <= 2) {
+    const int32_t c = R.cnt[rule.metric];
+    const int64_t* sv = R.sorted + (int64_t)rule.metric * R.N;
     int64_t tm = 0;
     const int sat = target_milli(rule.target, &tm);
     int32_t lb, ub;
@@ -139,10 +148,8 @@ __global__ void tas_ranges_kernel(int32_t n_rules, const pas_rule* __restrict__ 
     else if (rule.op == PAS_OP_GREATER_THAN) out = make_int2(ub, c);
     else out = make_int2(lb, ub);
   }
-  ranges[r] = out;
+  R.ranges[r] = out;
 }
-
-// ---------------------------------------------------------------------------- group
 
 struct GroupParams {
   int32_t P, M, N;
@@ -150,6 +157,7 @@ struct GroupParams {
   const pas_rule* prio;
   const int32_t* rule_off;
   const int32_t* cnt;
+  int2* keys;            // [P]   scratch: {bucket, cnt0} of each pod
   int32_t* pod_list;     // [P]   pods bucketed by key, bucket G (no list) last
   int32_t* group_start;  // [G+2]
   int32_t* seg_start;    // [G+1] first emit segment of each bucket
@@ -158,46 +166,73 @@ struct GroupParams {
   int32_t max_segs;
 };
 
-// Bucket of pod p: order column (order * M + metric) of its prioritize list, or G when it
-// has none (no PRIORITIZE flag, metric out of range, or a metric no node reports — the
-// ReadMetric error of prioritizeNodesForRule, telemetryscheduler.go:92-96).
-__device__ __forceinline__ int32_t pod_key(const GroupParams& g, int32_t p, int32_t* cnt0) {
-  const int32_t G = 3 * g.M;
-  *cnt0 = 0;
-  if (!(g.flags & PAS_TAS_PRIORITIZE)) return G;
-  const pas_rule r = g.prio[p];
-  if (r.metric < 0 || r.metric >= g.M) return G;
-  const int32_t c = g.cnt[r.metric];
-  if (c == 0) return G;
-  *cnt0 = c;
-  return order_of(r.op) * g.M + r.metric;
-}
+constexpr int kGU = 4;  // pods per thread per round of loads (all issued before use)
 
-// One block: counting sort of the pods by bucket, the per-position pod descriptors the
-// filter reads with one load, and the emit-segment table per bucket.
-__global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
-  extern __shared__ __attribute__((aligned(16))) int32_t sh[];
+// Counting sort of the pods by bucket = order column (order * M + metric) of the pod's
+// prioritize list, or G when it has none (no PRIORITIZE flag, metric out of range, or a
+// metric no node reports: the ReadMetric error of prioritizeNodesForRule,
+// telemetryscheduler.go:92-96).  Also writes the per-position pod descriptors the filter
+// reads with one load, and the emit-segment table per bucket.  Loads are unconditional
+// (clamped indices) so that each round's are in flight together.
+__device__ void group_body(const GroupParams& g, int32_t* sh) {
   const int32_t G = 3 * g.M;
   int32_t* partial = sh;                  // [kGroupTpb]
   int32_t* hist = sh + kGroupTpb;         // [G + 1]
   const int tid = threadIdx.x;
+  const bool prio = (g.flags & PAS_TAS_PRIORITIZE) != 0 && g.M > 0;
   for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
   __syncthreads();
-  int32_t c0;
-  for (int32_t p = tid; p < g.P; p += kGroupTpb) atomicAdd(&hist[pod_key(g, p, &c0)], 1);
+  for (int32_t p0 = tid; p0 < g.P; p0 += kGroupTpb * kGU) {
+    pas_rule r[kGU];
+    int32_t c[kGU];
+    if (prio) {  // uniform: prio may be null without the PRIORITIZE flag
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) r[u] = g.prio[min(p0 + u * kGroupTpb, g.P - 1)];
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) c[u] = g.cnt[min(max(r[u].metric, 0), g.M - 1)];
+    } else {
+#pragma unroll
+      for (int u = 0; u < kGU; ++u) {
+        r[u] = pas_rule{-1, 0, 0};
+        c[u] = 0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int32_t p = p0 + u * kGroupTpb;
+      if (p >= g.P) continue;
+      const bool listed = prio && r[u].metric >= 0 && r[u].metric < g.M && c[u] > 0;
+      const int32_t key = listed ? order_of(r[u].op) * g.M + r[u].metric : G;
+      g.keys[p] = make_int2(key, listed ? c[u] : 0);
+      atomicAdd(&hist[key], 1);
+    }
+  }
   __syncthreads();
   block_exclusive_scan(hist, G + 1, partial);
   for (int32_t i = tid; i <= G; i += kGroupTpb) g.group_start[i] = hist[i];
   if (tid == 0) g.group_start[G + 1] = g.P;
   __syncthreads();
   const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
-  for (int32_t p = tid; p < g.P; p += kGroupTpb) {
-    const int32_t key = pod_key(g, p, &c0);
-    const int32_t r0 = filt ? g.rule_off[p] : 0, r1 = filt ? g.rule_off[p + 1] : 0;
-    const int32_t pos = atomicAdd(&hist[key], 1);  // order inside a bucket is free
-    g.pod_list[pos] = p;
-    g.desc[2 * pos] = make_int4(p, key < G ? key : -1, c0, (c0 + kSegPos - 1) / kSegPos);
-    g.desc[2 * pos + 1] = make_int4(r0, r1, 0, 0);
+  for (int32_t p0 = tid; p0 < g.P; p0 += kGroupTpb * kGU) {
+    int2 kc[kGU];
+    int32_t r0[kGU], r1[kGU];
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int32_t p = min(p0 + u * kGroupTpb, g.P - 1);
+      kc[u] = g.keys[p];
+      r0[u] = filt ? g.rule_off[p] : 0;
+      r1[u] = filt ? g.rule_off[p + 1] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int32_t p = p0 + u * kGroupTpb;
+      if (p >= g.P) continue;
+      const int32_t key = kc[u].x, c0 = kc[u].y;
+      const int32_t pos = atomicAdd(&hist[key], 1);  // order inside a bucket is free
+      g.pod_list[pos] = p;
+      g.desc[2 * pos] = make_int4(p, key < G ? key : -1, c0, (c0 + kSegPos - 1) / kSegPos);
+      g.desc[2 * pos + 1] = make_int4(r0[u], r1[u], 0, 0);
+    }
   }
   __syncthreads();
   // hist[i] now holds the end of bucket i: emit segments per non-empty bucket
@@ -215,6 +250,16 @@ __global__ __launch_bounds__(kGroupTpb) void tas_group_kernel(GroupParams g) {
     for (int32_t k = hist[i]; k < end; ++k) g.seg_group[k] = i;
   }
   for (int32_t k = total + tid; k < g.max_segs; k += kGroupTpb) g.seg_group[k] = -1;
+}
+
+__global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, RangesParams R) {
+  extern __shared__ __attribute__((aligned(16))) int32_t sh[];
+  if (blockIdx.x == 0) {
+    group_body(g, sh);
+    return;
+  }
+  const int32_t r = (int32_t)(blockIdx.x - 1) * kGroupTpb + threadIdx.x;
+  if (r < R.n_rules) ranges_body(R, r);
 }
 
 // ---------------------------------------------------------------------------- filter
@@ -653,7 +698,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   if (max_segs > INT32_MAX) return set_error(ctx, PAS_ECAPACITY, "pas_tas_eval: batch too large");
 
   // scratch: ranges | pod_list | group_start | seg_start | seg_group | seg_base | drop | desc
-  const size_t sizes[8] = {
+  //          | keys
+  const size_t sizes[9] = {
       align256(sizeof(int2) * (size_t)std::max(n_rules, 1)),
       align256(sizeof(int32_t) * (size_t)n_pods),
       align256(sizeof(int32_t) * (size_t)(G + 2)),
@@ -661,7 +707,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
       align256(sizeof(int32_t) * (size_t)std::max<int64_t>(max_segs, 1)),
       prio ? align256(sizeof(int32_t) * (size_t)n_pods * S) : 0,
       prio ? align256(sizeof(uint64_t) * (size_t)n_pods * D64) : 0,
-      align256(sizeof(int4) * 2 * (size_t)std::max(n_pods, 1))};
+      align256(sizeof(int4) * 2 * (size_t)std::max(n_pods, 1)),
+      align256(sizeof(int2) * (size_t)std::max(n_pods, 1))};
   size_t need = 0;
   for (size_t b : sizes) need += b;
   if (need > ctx->aux_bytes) {
@@ -675,8 +722,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     ctx->aux_bytes = need;
   }
   char* cur = static_cast<char*>(ctx->aux);
-  char* parts[8];
-  for (int i = 0; i < 8; ++i) {
+  char* parts[9];
+  for (int i = 0; i < 9; ++i) {
     parts[i] = cur;
     cur += sizes[i];
   }
@@ -688,25 +735,22 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   int32_t* d_sb = reinterpret_cast<int32_t*>(parts[5]);
   uint64_t* d_drop = reinterpret_cast<uint64_t*>(parts[6]);
   int4* d_desc = reinterpret_cast<int4*>(parts[7]);
+  int2* d_keys = reinterpret_cast<int2*>(parts[8]);
 
   TimedLaunch span, tl;
   timing_begin(ctx, s, PAS_K_TAS_SPAN, &span);
-  if ((flags & PAS_TAS_FILTER) && n_rules > 0) {
-    timing_begin(ctx, s, PAS_K_TAS_RANGES, &tl);
-    tas_ranges_kernel<<<(n_rules + kTpb - 1) / kTpb, kTpb, 0, s>>>(n_rules, d_rules, t.cnt,
-                                                                   t.sorted, N, M, d_ranges);
-    timing_end(ctx, s, &tl);
-    PAS_HIP(ctx, hipGetLastError());
-  }
-
-  GroupParams gp{n_pods, M,    N,    flags, d_prio, d_rule_off,         t.cnt,
-                 d_list, d_gs, d_ss, d_sg,  d_desc, (int32_t)max_segs};
+  // ranges (blocks 1..) beside the grouping (block 0), one launch
+  const int32_t range_rules = (flags & PAS_TAS_FILTER) ? n_rules : 0;
+  RangesParams rp{range_rules, N, M, d_rules, t.cnt, t.sorted, d_ranges};
+  GroupParams gp{n_pods, M,    N,    flags, d_prio, d_rule_off, t.cnt,
+                 d_keys, d_list, d_gs, d_ss,  d_sg,   d_desc,     (int32_t)max_segs};
   const size_t group_lds = sizeof(int32_t) * ((size_t)kGroupTpb + G + 1);
   if (group_lds > 64 * 1024)
-    PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_group_kernel),
+    PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_prep_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_lds));
+  const unsigned prep_blocks = 1u + (unsigned)((range_rules + kGroupTpb - 1) / kGroupTpb);
   timing_begin(ctx, s, PAS_K_TAS_GROUP, &tl);
-  tas_group_kernel<<<1, kGroupTpb, group_lds, s>>>(gp);
+  tas_prep_kernel<<<prep_blocks, kGroupTpb, group_lds, s>>>(gp, rp);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
 

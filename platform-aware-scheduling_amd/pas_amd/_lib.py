@@ -59,7 +59,7 @@ KERNEL_NAMES = {
     PAS_K_TAS_VIOLATIONS: "tas_violations_kernel",
     PAS_K_GAS_PREP: "gas_prep_kernel",
     PAS_K_GAS_FIT: "gas_fit_kernel",
-    PAS_K_TAS_GROUP: "tas_group_kernel",
+    PAS_K_TAS_GROUP: "tas_prep_kernel",
     PAS_K_TAS_EMIT: "tas_emit_kernel",
     PAS_K_TAS_SPAN: "tas_eval_span",
 }
