@@ -116,6 +116,19 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
                           int32_t* n_metrics);
 
+/* Composed-order index.  A dontschedule rule selects a contiguous range of its metric's
+ * ascending order; the positions of those nodes in a pod's prioritize order are then the
+ * same range of phi[ocol][m][k] = position of node perm_asc[m][k] in order column ocol
+ * (ocol = order * n_metrics + metric; order 0 ascending, 1 descending, 2 node index).
+ * pas_tas_snapshot_set* builds phi when its 3 * n_metrics^2 * n_nodes * 4 bytes fit the
+ * budget set here: bytes >= 0 is an explicit cap (0 = never build), -1 (the default)
+ * means a quarter of the device memory free at upload time.  Takes effect at the next
+ * upload.  Without phi the evaluation maps each failing node through a rank array
+ * instead; results are identical either way. */
+int pas_tas_set_index_budget(pas_ctx* ctx, int64_t bytes);
+/* Bytes of the resident composed-order index (0 = not built). */
+int pas_tas_index_bytes(const pas_ctx* ctx, int64_t* bytes);
+
 #define PAS_TAS_FILTER 1u      /* produce pass_out (MetricsExtender.filterNodes) */
 #define PAS_TAS_PRIORITIZE 2u  /* produce order_out/order_len (prioritizeNodesForRule) */
 

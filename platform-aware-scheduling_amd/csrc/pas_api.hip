@@ -98,6 +98,7 @@ void free_tas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(t.sorted));
   free_ptr(reinterpret_cast<void*&>(t.perm));
   free_ptr(reinterpret_cast<void*&>(t.rank));
+  free_ptr(reinterpret_cast<void*&>(t.phi));
   free_ptr(reinterpret_cast<void*&>(t.vals_c));
   free_ptr(reinterpret_cast<void*&>(t.word_scan));
   free_ptr(reinterpret_cast<void*&>(t.seg_begin));
@@ -340,6 +341,19 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
   if (rc) return rc;
   return tas_snapshot_build(ctx, gen, n_nodes, n_metrics, d_v_milli, d_present,
                             pick_stream(ctx, hip_stream));
+}
+
+int pas_tas_set_index_budget(pas_ctx* ctx, int64_t bytes) {
+  if (!ctx) return PAS_EINVAL;
+  if (bytes < -1) return set_error(ctx, PAS_EINVAL, "pas_tas_set_index_budget: bytes < -1");
+  ctx->tas_index_budget = bytes;
+  return PAS_OK;
+}
+
+int pas_tas_index_bytes(const pas_ctx* ctx, int64_t* bytes) {
+  if (!ctx || !bytes) return PAS_EINVAL;
+  *bytes = ctx->tas.valid && ctx->tas.phi ? (int64_t)ctx->tas.phi_bytes : 0;
+  return PAS_OK;
 }
 
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,

@@ -27,6 +27,7 @@ inline int64_t rank_row(int64_t n) { return w32(n) * 32; }
 //   cnt      int32 [M]         nodes that have metric m
 //   sorted   int64 [M][N]      ascending values of the present nodes (first cnt[m])
 //   perm     int32 [3][M][N]   node ids in asc / desc / index order (first cnt[m])
+//   phi      int32 [3M][M][N]  optional: phi[ocol][m][k] = rank[ocol][perm_asc[m][k]]
 //   rank     uint32 [3][M][Nr] position of node n in each order, kNoRank if absent; rows
 //                              padded to Nr = round_up(N, 32) so that the 32 ranks of
 //                              one 32-node bitmap word fill one 128-byte line
@@ -42,6 +43,8 @@ struct TasSnapshot {
   int32_t* perm = nullptr;
   uint32_t* rank = nullptr;
   int32_t rank_stride = 0;  // Nr
+  int32_t* phi = nullptr;   // [3M][M][N] composed orders (pas_tas_set_index_budget), or null
+  size_t phi_bytes = 0;
   // build scratch
   int64_t* vals_c = nullptr;       // compacted values in index order
   uint32_t* word_scan = nullptr;   // [M*W64 + 1]
@@ -82,6 +85,7 @@ struct pas_ctx {
   std::string err;
   pas::TasSnapshot tas;
   pas::GasSnapshot gas;
+  int64_t tas_index_budget = -1;  // pas_tas_set_index_budget
   // per-call scratch (grown on demand, never freed inside a launch function)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;

@@ -278,6 +278,7 @@ struct FilterParams {
   const uint64_t* cand;
   const int32_t* perm;   // [3][M][N]
   const uint32_t* rank;  // [3][M][Nr]
+  const int32_t* phi;    // [3M][M][N] composed orders, or null
   const int4* desc;      // [2P] from K group
   uint64_t* pass_out;    // [P][W64]
   uint64_t* drop;        // [P][D64]
@@ -298,18 +299,64 @@ __device__ __forceinline__ int32_t wave_inclusive_sum(int32_t x) {
   return x;
 }
 
+// Clear bits of the LDS node bitmap `pass` -> bits at their positions in order column
+// `ocol` of the LDS drop bitmap, through the rank row.  The walk is in node order, 8 lanes
+// per 32-node word: lane q of a word loads the 16-byte quad of ranks of nodes 4q..4q+3 only
+// when one of them is clear, so a wave instruction touches at most 8 lines and a pod moves
+// one line per word with a clear bit.  (A random 4-byte gather per node moves a line per
+// node: 2.6x the line traffic at the C2 shape.)  The loads are unconditional buffer loads
+// (a load under a divergent branch makes the compiler wait for the previous one first); a
+// lane with nothing to map passes an out-of-range offset: the range check drops the fetch.
+template <int kAblate>
+__device__ __forceinline__ void map_clear_bits(const FilterParams& P, const uint32_t* pass,
+                                               uint32_t* drop, int32_t ocol, int tid) {
+  const int32_t N = P.N;
+  // buffer resource over the rank row (128-B aligned rows); built from wave-uniform
+  // values only (cdna_hip_programming.md T8)
+  const uint32_t* row = P.rank + (int64_t)ocol * P.Nr;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(row), 0, P.Nr * 4, 0x00020000);
+  const int q = tid & 7;                       // quad of the word: nodes 4q..4q+3
+  const int32_t wl = tid >> 3;                 // word slot: 32 per block step
+  constexpr int UQ = 8;                        // words per lane in flight
+  for (int32_t w0 = 0; w0 < P.W32; w0 += (kTpb / 8) * UQ) {
+    uint32_t zq[UQ];
+    v4i32 r[UQ];
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      const int32_t w = min(w0 + u * (kTpb / 8) + wl, P.W32 - 1);
+      const int32_t lo = w * 32;
+      const uint32_t tail = lo + 32 <= N ? 0xFFFFFFFFu : (1u << (N - lo)) - 1u;
+      zq[u] = w0 + u * (kTpb / 8) + wl < P.W32 ? ((~pass[w] & tail) >> (4 * q)) & 0xFu : 0u;
+      const uint32_t voff =
+          (zq[u] && !(kAblate & 1)) ? (uint32_t)(w * 8 + q) * 16u : 0x80000000u;
+      r[u] = __builtin_bit_cast(v4i32, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < UQ; ++u) {
+      if (!zq[u]) continue;
+      const uint32_t rr[4] = {(uint32_t)r[u].x, (uint32_t)r[u].y, (uint32_t)r[u].z,
+                              (uint32_t)r[u].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (((zq[u] >> j) & 1u) && rr[j] != kNoRank)
+          atomicOr(&drop[rr[j] >> 5], 1u << (rr[j] & 31));
+    }
+  }
+}
+
 // One workgroup per pod.  Phases, each issuing its global loads before their first use:
 //   1. candidates -> LDS pass bitmap over node ids;
-//   2. rule ranges: 16 coalesced perm reads per thread, LDS atomicAnd into the bitmap;
-//   3. prioritize: every clear bit of the final bitmap (a failing node or a non-candidate)
-//      is mapped through the order's rank row into an LDS drop bitmap over positions.
-//      The walk is in node order, 8 lanes per 32-node word: lane q of a word loads the
-//      16-byte quad of ranks of nodes 4q..4q+3 only when one of them is clear, so a wave
-//      instruction touches at most 8 lines and a pod moves one line per word that has a
-//      clear bit.  (A random 4-byte gather per failing node moves a line per node: 2.6x
-//      the line traffic at the C2 shape, measured 0.115 ms of gathers per step; scanning
-//      the whole order row per pod instead is LDS-bank / VALU bound, measured slower.)
+//   2. rule ranges: 16 coalesced perm reads per thread, LDS atomicAnd into the bitmap.
+//      With the composed-order index (phi, pas_tas_set_index_budget) the same range of
+//      phi gives the nodes' positions in the pod's prioritize order: a second coalesced
+//      read and an LDS atomicOr into the drop bitmap over positions;
+//   3. without phi: every clear bit of the final bitmap (failing node or non-candidate)
+//      goes to the drop bitmap through the rank row (map_clear_bits); with phi only the
+//      non-candidates do, before phase 2;
 //   4. drop row + kept count per 1024-position segment -> segment output bases.
+// (Measured at C2: random rank gathers per failing node 0.115 ms/step; whole-row scans per
+// pod are LDS-bank / VALU bound and slower; line-quad rank loads ~0.08 ms/step.)
 // kAblate (diagnostic timing builds only, PAS_FILTER_ABLATE; outputs wrong): bit 1 = no
 // rank loads, 2 = no LDS atomics in the rule loop, 4 = no rule loop, 8 = no row writes.
 template <int kAblate>
@@ -335,6 +382,9 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
   const int tid = threadIdx.x;
   const int32_t N = P.N, W64 = P.W64;
   const bool has_list = ocol >= 0;
+  const bool use_phi = P.phi != nullptr && (P.flags & PAS_TAS_FILTER);
+  const int32_t* __restrict__ phi_o =
+      (use_phi && has_list) ? P.phi + (int64_t)ocol * P.M * N : nullptr;
 
   // ---- 1. candidates -> pass bitmap (args.Nodes.Items, telemetryscheduler.go:204) ----
   constexpr int kCU = 8;
@@ -357,6 +407,9 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
   else if (tid == 0 && (P.flags & PAS_TAS_PRIORITIZE))
     P.order_len[pod] = 0;  // no rule / ReadMetric error -> empty HostPriorityList (:92-96)
   __syncthreads();
+
+  // with phi, the non-candidates are the only clear bits that phase 2 does not map
+  if (use_phi && has_list && cand) map_clear_bits<kAblate>(P, pass, drop, ocol, tid);
 
   // ---- 2. dontschedule.Violated: every node of every rule range fails the filter ----
   if ((P.flags & PAS_TAS_FILTER) && !(kAblate & 4)) {
@@ -384,7 +437,7 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
       // divergent branch makes the compiler wait for the previous one first.
       constexpr int U = 16;
       for (int32_t base = tid; base < total; base += kTpb * U) {
-        int32_t v[U];
+        int32_t v[U], q[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int32_t f = min(base + u * kTpb, total - 1);
@@ -392,15 +445,18 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
 #pragma unroll
           for (int st = kRuleChunk / 2; st > 0; st >>= 1)
             r = s_pref[r + st] <= f ? r + st : r;
-          v[u] = perm_asc[s_base[r] + (f - s_pref[r])];
+          const int32_t idx = s_base[r] + (f - s_pref[r]);
+          v[u] = perm_asc[idx];
+          q[u] = phi_o ? phi_o[idx] : -1;  // uniform branch
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           if (kAblate & 2) {
-            asm volatile("" ::"v"(v[u]));
+            asm volatile("" ::"v"(v[u]), "v"(q[u]));
             continue;
           }
           atomicAnd(&pass[v[u] >> 5], ~(1u << (v[u] & 31)));
+          if (q[u] >= 0) atomicOr(&drop[q[u] >> 5], 1u << (q[u] & 31));
         }
       }
       __syncthreads();
@@ -416,43 +472,8 @@ __global__ __launch_bounds__(kTpb) void tas_filter_kernel(FilterParams P) {
     return;
   }
 
-  // ---- 3. clear bits -> drop bitmap over the order's positions (line-quad rank loads) ----
-  {
-    // buffer resource over the rank row (128-B aligned rows); built from wave-uniform
-    // values only (cdna_hip_programming.md T8)
-    const uint32_t* row = P.rank + (int64_t)ocol * P.Nr;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(row), 0, P.Nr * 4, 0x00020000);
-    const int q = tid & 7;                       // quad of the word: nodes 4q..4q+3
-    const int32_t wl = tid >> 3;                 // word slot: 32 per block step
-    constexpr int UQ = 8;                        // words per lane in flight
-    for (int32_t w0 = 0; w0 < P.W32; w0 += (kTpb / 8) * UQ) {
-      // The loads are unconditional buffer loads (a load under a divergent branch makes
-      // the compiler wait for the previous one first); a lane with nothing to map passes
-      // an out-of-range offset, which the range check turns into no fetch at all.
-      uint32_t zq[UQ];
-      v4i32 r[UQ];
-#pragma unroll
-      for (int u = 0; u < UQ; ++u) {
-        const int32_t w = min(w0 + u * (kTpb / 8) + wl, P.W32 - 1);
-        const int32_t lo = w * 32;
-        const uint32_t tail = lo + 32 <= N ? 0xFFFFFFFFu : (1u << (N - lo)) - 1u;
-        zq[u] = w0 + u * (kTpb / 8) + wl < P.W32 ? ((~pass[w] & tail) >> (4 * q)) & 0xFu : 0u;
-        const uint32_t voff = (zq[u] && !(kAblate & 1)) ? (uint32_t)(w * 8 + q) * 16u : 0x80000000u;
-        r[u] = __builtin_bit_cast(v4i32, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff, 0, 0));
-      }
-#pragma unroll
-      for (int u = 0; u < UQ; ++u) {
-        if (!zq[u]) continue;
-        const uint32_t rr[4] = {(uint32_t)r[u].x, (uint32_t)r[u].y, (uint32_t)r[u].z,
-                                (uint32_t)r[u].w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if (((zq[u] >> j) & 1u) && rr[j] != kNoRank)
-            atomicOr(&drop[rr[j] >> 5], 1u << (rr[j] & 31));
-      }
-    }
-  }
+  // ---- 3. without phi: every clear bit (failing node or non-candidate) -> drop ----
+  if (!use_phi) map_clear_bits<kAblate>(P, pass, drop, ocol, tid);
   __syncthreads();
 
   // ---- 4. pass and drop rows -> HBM; kept count per segment -> segment output bases ----
@@ -765,6 +786,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   fp.S = S;
   fp.Nr = t.rank_stride;
   fp.rank = t.rank;
+  fp.phi = t.phi;
   fp.flags = flags;
   fp.ranges = d_ranges;
   fp.rules = d_rules;

@@ -87,7 +87,59 @@ __global__ void invert_order(const int32_t* __restrict__ perm, const int32_t* __
   rank[(int64_t)m * Nr + perm[(int64_t)m * N + k]] = (uint32_t)k;
 }
 
+// phi[ocol][m][k] = rank[ocol][perm_asc[m][k]] for k < cnt[m].  Blocks run ocol-major
+// (grid z), so one rank row serves all M metrics from L2 while it is hot.
+__global__ void compose_orders(const int32_t* __restrict__ perm_asc,
+                               const uint32_t* __restrict__ rank,
+                               const int32_t* __restrict__ cnt, int32_t N, int32_t Nr,
+                               int32_t M, int32_t* __restrict__ phi) {
+  const int32_t m = blockIdx.y;
+  const int32_t ocol = blockIdx.z;
+  const int32_t k = blockIdx.x * kTpb + threadIdx.x;
+  if (k >= cnt[m]) return;
+  const int32_t n = perm_asc[(int64_t)m * N + k];
+  phi[((int64_t)ocol * M + m) * N + k] = (int32_t)rank[(int64_t)ocol * Nr + n];
+}
+
 }  // namespace
+
+// The composed-order index, when it fits the context's budget (pas.h,
+// pas_tas_set_index_budget); otherwise none (the evaluation then uses the rank arrays).
+static int build_phi(pas_ctx* ctx, int32_t N, int32_t M, hipStream_t s) {
+  TasSnapshot& t = ctx->tas;
+  const size_t need = sizeof(int32_t) * 3 * (size_t)M * (size_t)M * (size_t)N;
+  size_t cap = 0;
+  if (ctx->tas_index_budget >= 0) {
+    cap = (size_t)ctx->tas_index_budget;
+  } else {
+    size_t free_b = 0, total_b = 0;
+    PAS_HIP(ctx, hipMemGetInfo(&free_b, &total_b));
+    cap = (free_b + (t.phi ? t.phi_bytes : 0)) / 4;
+  }
+  if (need == 0 || need > cap) {
+    if (t.phi) {
+      PAS_HIP(ctx, hipStreamSynchronize(s));
+      PAS_HIP(ctx, hipFree(t.phi));
+    }
+    t.phi = nullptr;
+    t.phi_bytes = 0;
+    return PAS_OK;
+  }
+  if (!t.phi || t.phi_bytes != need) {
+    if (t.phi) {
+      PAS_HIP(ctx, hipStreamSynchronize(s));
+      PAS_HIP(ctx, hipFree(t.phi));
+      t.phi = nullptr;
+    }
+    PAS_HIP(ctx, hipMalloc(&t.phi, need));
+    t.phi_bytes = need;
+  }
+  const dim3 grid((unsigned)((N + kTpb - 1) / kTpb), (unsigned)M, (unsigned)(3 * M));
+  compose_orders<<<grid, kTpb, 0, s>>>(t.perm + (size_t)kOrderAsc * M * N, t.rank, t.cnt, N,
+                                       t.rank_stride, M, t.phi);
+  PAS_HIP(ctx, hipGetLastError());
+  return PAS_OK;
+}
 
 int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
                        const int64_t* d_vals, const uint64_t* d_present, hipStream_t s) {
@@ -177,6 +229,7 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     invert_order<<<grid, kTpb, 0, s>>>(perm_desc, t.cnt, N, Nr,
                                         t.rank + (size_t)kOrderDesc * MNr);
     PAS_HIP(ctx, hipGetLastError());
+    if (int rc = build_phi(ctx, N, M, s)) return rc;
   }
   t.gen = gen;
   t.valid = true;

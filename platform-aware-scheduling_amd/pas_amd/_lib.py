@@ -90,6 +90,8 @@ SIGNATURES = {
     "pas_tas_snapshot_set": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P]),
     "pas_tas_snapshot_set_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P]),
     "pas_tas_snapshot_info": (c_int, [_P, POINTER(c_uint64), POINTER(c_int32), POINTER(c_int32)]),
+    "pas_tas_set_index_budget": (c_int, [_P, c_int64]),
+    "pas_tas_index_bytes": (c_int, [_P, POINTER(c_int64)]),
     "pas_tas_eval": (c_int, [_P, c_uint64, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P]),
     "pas_tas_eval_device": (
         c_int,

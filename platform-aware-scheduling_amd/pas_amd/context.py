@@ -156,6 +156,16 @@ class Context:
                     "pas_tas_snapshot_set_device")
         self.n_nodes, self.n_metrics = n_nodes, n_metrics
 
+    def tas_set_index_budget(self, nbytes: int):
+        """Cap (bytes) for the composed-order index built at the next snapshot upload;
+        -1 = a quarter of free device memory (default), 0 = never."""
+        self._check(self._l.pas_tas_set_index_budget(self._h, nbytes), "pas_tas_set_index_budget")
+
+    def tas_index_bytes(self) -> int:
+        b = c_int64()
+        self._check(self._l.pas_tas_index_bytes(self._h, byref(b)), "pas_tas_index_bytes")
+        return b.value
+
     def tas_snapshot_info(self):
         g = c_uint64()
         n = c_int32()

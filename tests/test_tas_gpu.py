@@ -185,6 +185,26 @@ def test_random_parity_large_batches(ctx, oracle, p):
         assert_same(ctx, oracle, v, pres, rules, off, prio, cand, 2)
 
 
+@pytest.mark.parametrize("budget", [0, -1])
+def test_random_parity_with_and_without_composed_index(ctx, oracle, budget):
+    """Both evaluation forms (pas.h, pas_tas_set_index_budget): with the composed-order index
+    rule violations map to positions by coalesced reads; without it through the rank rows."""
+    ctx.tas_set_index_budget(budget)
+    try:
+        rng = np.random.default_rng(500 + budget)
+        for n, cand_frac, ties in ((777, None, None), (2048, 0.8, None),
+                                   (3001, 0.9, [0, 1000, 2000, -3000])):
+            v, pres, rules, off, prio, cand = random_case(rng, n, 5, 40, 12, tie_vals=ties,
+                                                          cand_frac=cand_frac)
+            for flags in (1, 2, 3):
+                assert_same(ctx, oracle, v, pres, rules, off, prio, cand, flags)
+            m = v.shape[0]
+            want = 3 * m * m * n * 4 if budget else 0
+            assert ctx.tas_index_bytes() == want
+    finally:
+        ctx.tas_set_index_budget(-1)
+
+
 def test_many_rules_per_pod_chunked(ctx, oracle):
     # more than the kernel's 64-rule LDS chunk
     rng = np.random.default_rng(7)
