@@ -79,19 +79,24 @@ def bench_tas(args, world, rank):
 
     for _ in range(args.warmup):
         step()
+    # timed steps: span events only (HIP events on the launch stream around the path)
     ctx.reset_timing()
-    ctx.set_timing(True)
+    ctx.set_timing(1)
     elapsed = timed_steps(step, args.steps, 0, world)
-    ctx.set_timing(False)
-    # per-step device time of each kernel, and the span of the whole path (HIP events on
-    # the launch stream around the first and last launch)
-    kern, launches = {}, {}
-    for kid in (_lib.PAS_K_TAS_GROUP, _lib.PAS_K_TAS_FILTER, _lib.PAS_K_TAS_EMIT):
-        ms, n = ctx.kernel_time(kid)
-        kern[_lib.KERNEL_NAMES[kid]] = ms / args.steps
-        launches[_lib.KERNEL_NAMES[kid]] = n // args.steps
     span_ms, span_n = ctx.kernel_time(_lib.PAS_K_TAS_SPAN)
     span_ms /= max(span_n, 1)
+    # per-kernel breakdown from extra, untimed steps (events around every launch)
+    ctx.reset_timing()
+    ctx.set_timing(2)
+    n_detail = min(args.steps, 5)
+    for _ in range(n_detail):
+        step()
+    ctx.set_timing(0)
+    kern, launches = {}, {}
+    for kid in (_lib.PAS_K_TAS_PREP, _lib.PAS_K_TAS_EVAL):
+        ms, n = ctx.kernel_time(kid)
+        kern[_lib.KERNEL_NAMES[kid]] = ms / n_detail
+        launches[_lib.KERNEL_NAMES[kid]] = n // n_detail
     sum_len = int(len_t.sum().item())
     # algorithmic bytes per step: columns + presence + pass bitmaps +
     # ordered lists + lengths, plus the rule tables; divided by the span of the path
@@ -125,8 +130,8 @@ def bench_tas(args, world, rank):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "tas path span: tas_prep (pod grouping + rule ranges), tas_filter, "
-                      "tas_emit on one stream (HIP events around the three launches)",
+            "kernel": "tas path span: tas_prep (rule ranges + pod grouping) and tas_eval "
+                      "(filter + ordered lists) on one stream (HIP events around both launches)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -186,9 +191,9 @@ def bench_gas(args, world, rank):
     for _ in range(args.warmup):
         step()
     ctx.reset_timing()
-    ctx.set_timing(True)
+    ctx.set_timing(1)
     elapsed = timed_steps(step, args.steps, 0, world)
-    ctx.set_timing(False)
+    ctx.set_timing(0)
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
     alg_bytes = N * (8 * Q + 8 * K * Q + 4) + P * (8 * C * Q + 4 * C + 4) + 4 * P * N
     kernel_s = (k_ms / max(k_n, 1)) / 1e3
@@ -245,9 +250,9 @@ def bench_deschedule(args, world, rank):
     for _ in range(args.warmup):
         step()
     ctx.reset_timing()
-    ctx.set_timing(True)
+    ctx.set_timing(1)
     elapsed = timed_steps(step, args.steps, 0, world)
-    ctx.set_timing(False)
+    ctx.set_timing(0)
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_VIOLATIONS)
     w = pas_amd.w64(N)
     alg_bytes = 8 * M * N + 8 * M * w + 8 * S * w

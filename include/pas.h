@@ -116,19 +116,6 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
                           int32_t* n_metrics);
 
-/* Composed-order index.  A dontschedule rule selects a contiguous range of its metric's
- * ascending order; the positions of those nodes in a pod's prioritize order are then the
- * same range of phi[ocol][m][k] = position of node perm_asc[m][k] in order column ocol
- * (ocol = order * n_metrics + metric; order 0 ascending, 1 descending, 2 node index).
- * pas_tas_snapshot_set* builds phi when its 3 * n_metrics^2 * n_nodes * 4 bytes fit the
- * budget set here: bytes >= 0 is an explicit cap (0 = never build), -1 (the default)
- * means a quarter of the device memory free at upload time.  Takes effect at the next
- * upload.  Without phi the evaluation maps each failing node through a rank array
- * instead; results are identical either way. */
-int pas_tas_set_index_budget(pas_ctx* ctx, int64_t bytes);
-/* Bytes of the resident composed-order index (0 = not built). */
-int pas_tas_index_bytes(const pas_ctx* ctx, int64_t* bytes);
-
 #define PAS_TAS_FILTER 1u      /* produce pass_out (MetricsExtender.filterNodes) */
 #define PAS_TAS_PRIORITIZE 2u  /* produce order_out/order_len (prioritizeNodesForRule) */
 
@@ -235,16 +222,16 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
 
 /* Kernel timing with HIP events on the stream each kernel is launched on.
  * Kernel ids: */
-#define PAS_K_TAS_RANGES 0     /* (rule ranges now run inside the PAS_K_TAS_GROUP launch) */
-#define PAS_K_TAS_FILTER 1     /* per pod: pass bitmap, drop bitmap, segment bases */
+#define PAS_K_TAS_EVAL 1       /* per pod: pass bitmap + ordered host list (fused) */
 #define PAS_K_TAS_VIOLATIONS 2 /* deschedule sweep */
 #define PAS_K_GAS_PREP 3       /* per-GPU container requests */
 #define PAS_K_GAS_FIT 4        /* per (pod, node) first fit */
-#define PAS_K_TAS_GROUP 5      /* prep: bucket pods by prioritize order + rule ranges */
-#define PAS_K_TAS_EMIT 6       /* ordered host lists */
+#define PAS_K_TAS_PREP 5       /* rule ranges + pods bucketed by prioritize order */
 #define PAS_K_TAS_SPAN 7       /* whole pas_tas_eval path: first launch start to last launch end */
 #define PAS_K_COUNT 8
-int pas_set_timing(pas_ctx* ctx, int enable);
+#define PAS_TIMING_SPAN 1    /* whole paths: PAS_K_TAS_SPAN, the GAS fit and deschedule launches */
+#define PAS_TIMING_KERNELS 2 /* every launch (events between launches add small gaps) */
+int pas_set_timing(pas_ctx* ctx, int level); /* 0 = off */
 /* Sum of elapsed ms and number of launches recorded for a kernel since the last reset. */
 int pas_kernel_time(pas_ctx* ctx, int32_t kernel_id, double* total_ms, int64_t* launches);
 int pas_reset_timing(pas_ctx* ctx);

@@ -57,7 +57,11 @@ static hipEvent_t take_event(pas_ctx* ctx) {
 
 void timing_begin(pas_ctx* ctx, hipStream_t s, int kernel, TimedLaunch* tl) {
   tl->kernel = -1;
-  if (!ctx->timing) return;
+  // span-level timing brackets whole paths only: events between the launches of a path
+  // would add gaps to the span they measure
+  if (!ctx->timing || (ctx->timing == PAS_TIMING_SPAN && kernel != PAS_K_TAS_SPAN &&
+                       kernel != PAS_K_GAS_FIT && kernel != PAS_K_TAS_VIOLATIONS))
+    return;
   tl->start = take_event(ctx);
   tl->stop = take_event(ctx);
   if (!tl->start || !tl->stop) return;
@@ -97,8 +101,6 @@ void free_tas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(t.cnt));
   free_ptr(reinterpret_cast<void*&>(t.sorted));
   free_ptr(reinterpret_cast<void*&>(t.perm));
-  free_ptr(reinterpret_cast<void*&>(t.rank));
-  free_ptr(reinterpret_cast<void*&>(t.phi));
   free_ptr(reinterpret_cast<void*&>(t.vals_c));
   free_ptr(reinterpret_cast<void*&>(t.word_scan));
   free_ptr(reinterpret_cast<void*&>(t.seg_begin));
@@ -341,19 +343,6 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
   if (rc) return rc;
   return tas_snapshot_build(ctx, gen, n_nodes, n_metrics, d_v_milli, d_present,
                             pick_stream(ctx, hip_stream));
-}
-
-int pas_tas_set_index_budget(pas_ctx* ctx, int64_t bytes) {
-  if (!ctx) return PAS_EINVAL;
-  if (bytes < -1) return set_error(ctx, PAS_EINVAL, "pas_tas_set_index_budget: bytes < -1");
-  ctx->tas_index_budget = bytes;
-  return PAS_OK;
-}
-
-int pas_tas_index_bytes(const pas_ctx* ctx, int64_t* bytes) {
-  if (!ctx || !bytes) return PAS_EINVAL;
-  *bytes = ctx->tas.valid && ctx->tas.phi ? (int64_t)ctx->tas.phi_bytes : 0;
-  return PAS_OK;
 }
 
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
@@ -697,7 +686,9 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
 
 int pas_set_timing(pas_ctx* ctx, int enable) {
   if (!ctx) return PAS_EINVAL;
-  ctx->timing = enable != 0;
+  if (enable < 0 || enable > PAS_TIMING_KERNELS)
+    return set_error(ctx, PAS_EINVAL, "pas_set_timing: level must be 0, 1 or 2");
+  ctx->timing = enable;
   return PAS_OK;
 }
 

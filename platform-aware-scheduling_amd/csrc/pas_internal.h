@@ -11,7 +11,6 @@
 
 namespace pas {
 
-constexpr uint32_t kNoRank = 0xFFFFFFFFu;
 constexpr int kOrderAsc = 0;   // LessThan   (operator.go:38-39)
 constexpr int kOrderDesc = 1;  // GreaterThan (operator.go:36-37)
 constexpr int kOrderIndex = 2; // any other operator: no sort
@@ -19,34 +18,33 @@ constexpr int kNumOrders = 3;
 
 inline int64_t w64(int64_t n) { return (n + 63) / 64; }
 inline int64_t w32(int64_t n) { return (n + 31) / 32; }
-inline int64_t rank_row(int64_t n) { return w32(n) * 32; }
 
-// Device-resident TAS snapshot.  Layout in HBM (M metrics, N nodes):
+// Order rows are padded to whole 1024-position segments plus one more segment, filled with
+// a sentinel node id (see TasSnapshot), so that a segment load never needs a bound check.
+constexpr int kOrderPad = 1024;
+inline int64_t order_row(int64_t n) { return (n + kOrderPad - 1) / kOrderPad * kOrderPad + kOrderPad; }
+
+// Device-resident TAS snapshot.  Layout in HBM (M metrics, N nodes, R = order_row(N)):
 //   vals     int64 [M][N]      raw v_milli (deschedule sweep reads it directly)
 //   present  uint64 [M][W64]
 //   cnt      int32 [M]         nodes that have metric m
-//   sorted   int64 [M][N]      ascending values of the present nodes (first cnt[m])
-//   perm     int32 [3][M][N]   node ids in asc / desc / index order (first cnt[m])
-//   phi      int32 [3M][M][N]  optional: phi[ocol][m][k] = rank[ocol][perm_asc[m][k]]
-//   rank     uint32 [3][M][Nr] position of node n in each order, kNoRank if absent; rows
-//                              padded to Nr = round_up(N, 32) so that the 32 ranks of
-//                              one 32-node bitmap word fill one 128-byte line
+//   sorted   int64 [M][R]      ascending values of the present nodes (first cnt[m])
+//   perm     int32 [3][M][R]   node ids in asc / desc / index order (first cnt[m]); the
+//                              rest of each row holds the sentinel W64 * 64, a node id
+//                              whose bit in the evaluator's LDS pass bitmap is always 0
 struct TasSnapshot {
   bool valid = false;
   uint64_t gen = 0;
   int32_t n_nodes = 0;
   int32_t n_metrics = 0;
+  int32_t row = 0;  // R
   int64_t* vals = nullptr;
   uint64_t* present = nullptr;
   int32_t* cnt = nullptr;
   int64_t* sorted = nullptr;
   int32_t* perm = nullptr;
-  uint32_t* rank = nullptr;
-  int32_t rank_stride = 0;  // Nr
-  int32_t* phi = nullptr;   // [3M][M][N] composed orders (pas_tas_set_index_budget), or null
-  size_t phi_bytes = 0;
   // build scratch
-  int64_t* vals_c = nullptr;       // compacted values in index order
+  int64_t* vals_c = nullptr;       // [M][R] compacted values in index order
   uint32_t* word_scan = nullptr;   // [M*W64 + 1]
   int32_t* seg_begin = nullptr;    // [M]
   int32_t* seg_end = nullptr;      // [M]
@@ -85,14 +83,13 @@ struct pas_ctx {
   std::string err;
   pas::TasSnapshot tas;
   pas::GasSnapshot gas;
-  int64_t tas_index_budget = -1;  // pas_tas_set_index_budget
   // per-call scratch (grown on demand, never freed inside a launch function)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   void* aux = nullptr;  // per-call device table: TAS rule ranges / GAS container steps
   size_t aux_bytes = 0;
   // timing
-  bool timing = false;
+  int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;
   std::vector<hipEvent_t> event_pool;
   double total_ms[PAS_K_COUNT] = {};

@@ -45,22 +45,18 @@ PAS_GAS_MAX_CARDS = 8
 PAS_GAS_MAX_RES = 4
 PAS_GAS_MAX_SELECTIONS = 8
 
-PAS_K_TAS_RANGES = 0
-PAS_K_TAS_FILTER = 1
+PAS_K_TAS_EVAL = 1
 PAS_K_TAS_VIOLATIONS = 2
 PAS_K_GAS_PREP = 3
 PAS_K_GAS_FIT = 4
-PAS_K_TAS_GROUP = 5
-PAS_K_TAS_EMIT = 6
+PAS_K_TAS_PREP = 5
 PAS_K_TAS_SPAN = 7
 KERNEL_NAMES = {
-    PAS_K_TAS_RANGES: "tas_ranges_kernel",
-    PAS_K_TAS_FILTER: "tas_filter_kernel",
+    PAS_K_TAS_EVAL: "tas_eval_kernel",
     PAS_K_TAS_VIOLATIONS: "tas_violations_kernel",
     PAS_K_GAS_PREP: "gas_prep_kernel",
     PAS_K_GAS_FIT: "gas_fit_kernel",
-    PAS_K_TAS_GROUP: "tas_prep_kernel",
-    PAS_K_TAS_EMIT: "tas_emit_kernel",
+    PAS_K_TAS_PREP: "tas_prep_kernel",
     PAS_K_TAS_SPAN: "tas_eval_span",
 }
 
@@ -90,8 +86,6 @@ SIGNATURES = {
     "pas_tas_snapshot_set": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P]),
     "pas_tas_snapshot_set_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P]),
     "pas_tas_snapshot_info": (c_int, [_P, POINTER(c_uint64), POINTER(c_int32), POINTER(c_int32)]),
-    "pas_tas_set_index_budget": (c_int, [_P, c_int64]),
-    "pas_tas_index_bytes": (c_int, [_P, POINTER(c_int64)]),
     "pas_tas_eval": (c_int, [_P, c_uint64, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P]),
     "pas_tas_eval_device": (
         c_int,

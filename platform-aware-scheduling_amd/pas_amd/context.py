@@ -125,8 +125,10 @@ class Context:
         self._check(self._l.pas_synchronize(self._h), "pas_synchronize")
 
     # ------------------------------------------------------------------ timing
-    def set_timing(self, enable: bool):
-        self._check(self._l.pas_set_timing(self._h, 1 if enable else 0), "pas_set_timing")
+    def set_timing(self, level):
+        """0/False = off, 1 = whole paths (PAS_TIMING_SPAN), 2/True = every launch."""
+        level = 2 if level is True else int(level)
+        self._check(self._l.pas_set_timing(self._h, level), "pas_set_timing")
 
     def kernel_time(self, kernel_id: int) -> Tuple[float, int]:
         ms = c_double()
@@ -155,16 +157,6 @@ class Context:
                                                         _stream(stream)),
                     "pas_tas_snapshot_set_device")
         self.n_nodes, self.n_metrics = n_nodes, n_metrics
-
-    def tas_set_index_budget(self, nbytes: int):
-        """Cap (bytes) for the composed-order index built at the next snapshot upload;
-        -1 = a quarter of free device memory (default), 0 = never."""
-        self._check(self._l.pas_tas_set_index_budget(self._h, nbytes), "pas_tas_set_index_budget")
-
-    def tas_index_bytes(self) -> int:
-        b = c_int64()
-        self._check(self._l.pas_tas_index_bytes(self._h, byref(b)), "pas_tas_index_bytes")
-        return b.value
 
     def tas_snapshot_info(self):
         g = c_uint64()

@@ -19,7 +19,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles")
-TAS_PATH = ("tas_prep_kernel", "tas_filter_kernel", "tas_emit_kernel")
+TAS_PATH = ("tas_prep_kernel", "tas_eval_kernel")
 
 
 def short(name):

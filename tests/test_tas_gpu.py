@@ -185,24 +185,29 @@ def test_random_parity_large_batches(ctx, oracle, p):
         assert_same(ctx, oracle, v, pres, rules, off, prio, cand, 2)
 
 
-@pytest.mark.parametrize("budget", [0, -1])
-def test_random_parity_with_and_without_composed_index(ctx, oracle, budget):
-    """Both evaluation forms (pas.h, pas_tas_set_index_budget): with the composed-order index
-    rule violations map to positions by coalesced reads; without it through the rank rows."""
-    ctx.tas_set_index_budget(budget)
-    try:
-        rng = np.random.default_rng(500 + budget)
-        for n, cand_frac, ties in ((777, None, None), (2048, 0.8, None),
-                                   (3001, 0.9, [0, 1000, 2000, -3000])):
-            v, pres, rules, off, prio, cand = random_case(rng, n, 5, 40, 12, tie_vals=ties,
-                                                          cand_frac=cand_frac)
-            for flags in (1, 2, 3):
-                assert_same(ctx, oracle, v, pres, rules, off, prio, cand, flags)
-            m = v.shape[0]
-            want = 3 * m * m * n * 4 if budget else 0
-            assert ctx.tas_index_bytes() == want
-    finally:
-        ctx.tas_set_index_budget(-1)
+@pytest.mark.parametrize("seed", [0, 1])
+def test_random_parity_flags_candidates_ties(ctx, oracle, seed):
+    """Filter only, prioritize only (candidates = cand) and both, with candidate masks and
+    tie-heavy columns."""
+    rng = np.random.default_rng(500 + seed)
+    for n, cand_frac, ties in ((777, None, None), (2048, 0.8, None),
+                               (3001, 0.9, [0, 1000, 2000, -3000])):
+        v, pres, rules, off, prio, cand = random_case(rng, n, 5, 40, 12, tie_vals=ties,
+                                                      cand_frac=cand_frac)
+        for flags in (1, 2, 3):
+            assert_same(ctx, oracle, v, pres, rules, off, prio, cand, flags)
+
+
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1023, 1024, 1025, 2047, 2048, 4096, 4097])
+def test_segment_boundaries(ctx, oracle, n):
+    """Node counts around the 64-node words and the 1024-position order segments (the
+    padded order rows end in a sentinel segment)."""
+    rng = np.random.default_rng(n)
+    v, pres, rules, off, prio, cand = random_case(rng, n, 4, 24, 6, cand_frac=0.9)
+    for flags in (2, 3):
+        assert_same(ctx, oracle, v, pres, rules, off, prio, cand, flags)
+    v, pres, rules, off, prio, _ = random_case(rng, n, 4, 24, 6)
+    assert_same(ctx, oracle, v, pres, rules, off, prio, None, 3)
 
 
 def test_many_rules_per_pod_chunked(ctx, oracle):
