@@ -101,6 +101,8 @@ void free_tas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(t.cnt));
   free_ptr(reinterpret_cast<void*&>(t.sorted));
   free_ptr(reinterpret_cast<void*&>(t.perm));
+  free_ptr(reinterpret_cast<void*&>(t.f1k));
+  free_ptr(reinterpret_cast<void*&>(t.f32));
   free_ptr(reinterpret_cast<void*&>(t.vals_c));
   free_ptr(reinterpret_cast<void*&>(t.word_scan));
   free_ptr(reinterpret_cast<void*&>(t.seg_begin));

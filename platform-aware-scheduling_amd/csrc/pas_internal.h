@@ -32,6 +32,8 @@ inline int64_t order_row(int64_t n) { return (n + kOrderPad - 1) / kOrderPad * k
 //   perm     int32 [3][M][R]   node ids in asc / desc / index order (first cnt[m]); the
 //                              rest of each row holds the sentinel W64 * 64, a node id
 //                              whose bit in the evaluator's LDS pass bitmap is always 0
+//   f1k, f32 int64 [M][R/1024], [M][R/32]  every 1024th / 32nd sorted value (rule ranges
+//                              are found in three coalesced rounds: tas_eval.hip)
 struct TasSnapshot {
   bool valid = false;
   uint64_t gen = 0;
@@ -43,6 +45,8 @@ struct TasSnapshot {
   int32_t* cnt = nullptr;
   int64_t* sorted = nullptr;
   int32_t* perm = nullptr;
+  int64_t* f1k = nullptr;  // [M][R / 1024] sorted[m][1024 a]: fences of the range search
+  int64_t* f32 = nullptr;  // [M][R / 32]   sorted[m][32 b]
   // build scratch
   int64_t* vals_c = nullptr;       // [M][R] compacted values in index order
   uint32_t* word_scan = nullptr;   // [M*W64 + 1]

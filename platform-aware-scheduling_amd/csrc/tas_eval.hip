@@ -56,26 +56,6 @@ __device__ __forceinline__ uint64_t tail_mask64(int32_t c, int32_t n) {
   return (1ull << (n - lo)) - 1ull;
 }
 
-__device__ __forceinline__ int32_t lower_bound_i64(const int64_t* __restrict__ a, int32_t n,
-                                                   int64_t x) {
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (a[mid] < x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
-__device__ __forceinline__ int32_t upper_bound_i64(const int64_t* __restrict__ a, int32_t n,
-                                                   int64_t x) {
-  int32_t lo = 0, hi = n;
-  while (lo < hi) {
-    const int32_t mid = (lo + hi) >> 1;
-    if (a[mid] <= x) lo = mid + 1; else hi = mid;
-  }
-  return lo;
-}
-
 // target * 1000 with saturation: +1 (above every int64 milli value), -1 (below every
 // value) or 0 with *tm exact.
 __device__ __forceinline__ int target_milli(int64_t t, int64_t* tm) {
@@ -91,31 +71,33 @@ __device__ __forceinline__ int order_of(int32_t op) {
   return op == PAS_OP_GREATER_THAN ? kOrderDesc : op == PAS_OP_LESS_THAN ? kOrderAsc : kOrderIndex;
 }
 
-// Exclusive scan of a[0..n) in LDS by the whole block; returns the total.
-// `partial` holds blockDim.x ints of LDS.
-__device__ int32_t block_exclusive_scan(int32_t* a, int32_t n, int32_t* partial) {
-  const int T = blockDim.x, tid = threadIdx.x;
-  const int32_t per = (n + T - 1) / T;
-  const int32_t lo = min(n, tid * per), hi = min(n, lo + per);
-  int32_t s = 0;
-  for (int32_t i = lo; i < hi; ++i) s += a[i];
-  partial[tid] = s;
-  __syncthreads();
-  for (int off = 1; off < T; off <<= 1) {
-    const int32_t v = tid >= off ? partial[tid - off] : 0;
-    __syncthreads();
-    partial[tid] += v;
-    __syncthreads();
+__device__ __forceinline__ int32_t wave_inclusive_sum(int32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int32_t y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
   }
-  int32_t run = partial[tid] - s;
-  const int32_t total = partial[T - 1];
-  for (int32_t i = lo; i < hi; ++i) {
-    const int32_t t = a[i];
-    a[i] = run;
-    run += t;
+  return x;
+}
+
+// Exclusive scan of a[0..n) in LDS by wave 0 of the block (each lane a contiguous run of
+// ceil(n / 64) entries), then a block barrier.
+__device__ void block_exclusive_scan(int32_t* a, int32_t n) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int32_t per = (n + 63) / 64;
+    const int32_t lo = min(n, lane * per), hi = min(n, lo + per);
+    int32_t sum = 0;
+    for (int32_t i = lo; i < hi; ++i) sum += a[i];
+    int32_t run = wave_inclusive_sum(sum) - sum;
+    for (int32_t i = lo; i < hi; ++i) {
+      const int32_t v = a[i];
+      a[i] = run;
+      run += v;
+    }
   }
   __syncthreads();
-  return total;
 }
 
 // ---------------------------------------------------------------------------- prep
@@ -128,30 +110,83 @@ struct RangesParams {
   int32_t R;  // order row stride
   const pas_rule* rules;
   const int32_t* cnt;
-  const int64_t* sorted;
+  const int64_t* sorted;  // [M][R]
+  const int64_t* f1k;     // [M][R / 1024] sorted[m][1024 a]
+  const int64_t* f32;     // [M][R / 32]   sorted[m][32 b]
   int2* ranges;
 };
 
+constexpr int kRuleLanes = 8;  // lanes per rule in the range search
+
+// Numbers of entries of a[0..n) below t (cl: v < t) and not above t (cu: v <= t), for an
+// ascending a, counted by the rule's lane group (gl = lane within the group, gmask = the
+// group's lanes) with every load of the window in flight at once.
+template <int kMaxPerLane>
+__device__ __forceinline__ void count_below(const int64_t* __restrict__ al, int32_t nl,
+                                            const int64_t* __restrict__ au, int32_t nu,
+                                            int64_t t, int gl, uint64_t gmask, int32_t* cl,
+                                            int32_t* cu) {
+  int32_t sl = 0, su = 0;
+#pragma unroll
+  for (int q = 0; q < kMaxPerLane; ++q) {
+    const int32_t i = gl + q * kRuleLanes;
+    const int64_t vl = al[min(i, max(nl - 1, 0))];
+    const int64_t vu = au[min(i, max(nu - 1, 0))];
+    sl += __popcll(__ballot(i < nl && vl < t) & gmask);
+    su += __popcll(__ballot(i < nu && vu <= t) & gmask);
+  }
+  *cl = sl;
+  *cu = su;
+}
+
 // EvaluateRule (operator.go:13-26) over the ascending column: the nodes a rule selects form
 // one range, [lower_bound, upper_bound) of t*1000 for Equals, the prefix below it for
-// LessThan, the suffix above it for GreaterThan (t*1000 saturates).
-__device__ void ranges_body(const RangesParams& R, int32_t r) {
+// LessThan, the suffix above it for GreaterThan (t*1000 saturates).  A group
+// of 8 lanes per rule finds both bounds in three dependent rounds of loads: the 1024-stride
+// fences (f1k), the 32-stride fences of one 1024-block (f32), the 32 values of one
+// 32-block; each round counts the window's entries below the target.
+__device__ void ranges_group(const RangesParams& R, int32_t r) {
+  const int lane = threadIdx.x & 63, gl = lane & (kRuleLanes - 1);
+  const uint64_t gmask = 0xFFull << (lane & ~(kRuleLanes - 1));
   const pas_rule rule = R.rules[r];
   int2 out = make_int2(0, 0);
   if (rule.metric >= 0 && rule.metric < R.M && rule.op >= 0 && rule.op <= 2) {
-    const int32_t c = R.cnt[rule.metric];
-    const int64_t* sv = R.sorted + (int64_t)rule.metric * R.R;
-    int64_t tm = 0;
-    const int sat = target_milli(rule.target, &tm);
+    const int32_t m = rule.metric;
+    const int32_t c = R.cnt[m];
+    int64_t t = 0;
+    const int sat = target_milli(rule.target, &t);
     int32_t lb, ub;
-    if (sat > 0) { lb = ub = c; }
-    else if (sat < 0) { lb = ub = 0; }
-    else { lb = lower_bound_i64(sv, c, tm); ub = upper_bound_i64(sv, c, tm); }
+    if (sat != 0) {
+      lb = ub = sat > 0 ? c : 0;
+    } else {
+      const int64_t* sv = R.sorted + (int64_t)m * R.R;
+      const int64_t* f1 = R.f1k + (int64_t)m * (R.R >> 10);
+      const int64_t* f2 = R.f32 + (int64_t)m * (R.R >> 5);
+      const int32_t na = (c + 1023) >> 10, nb = (c + 31) >> 5;
+      int32_t n1l = 0, n1u = 0;  // fences (1024 apart) below the target
+      for (int32_t i0 = 0; i0 < na; i0 += 4 * kRuleLanes) {
+        int32_t a, b;
+        count_below<4>(f1 + i0, na - i0, f1 + i0, na - i0, t, gl, gmask, &a, &b);
+        n1l += a;
+        n1u += b;
+      }
+      // 1024-blocks holding each bound (sorted[1024 b1] is below; block 0 if none is)
+      const int32_t b1l = max(n1l - 1, 0), b1u = max(n1u - 1, 0);
+      int32_t n2l, n2u;
+      count_below<4>(f2 + b1l * 32, n1l ? min(32, nb - b1l * 32) : 0, f2 + b1u * 32,
+                     n1u ? min(32, nb - b1u * 32) : 0, t, gl, gmask, &n2l, &n2u);
+      const int32_t b2l = b1l * 32 + max(n2l - 1, 0), b2u = b1u * 32 + max(n2u - 1, 0);
+      int32_t n3l, n3u;
+      count_below<4>(sv + b2l * 32, n1l ? min(32, c - b2l * 32) : 0, sv + b2u * 32,
+                     n1u ? min(32, c - b2u * 32) : 0, t, gl, gmask, &n3l, &n3u);
+      lb = n1l ? b2l * 32 + n3l : 0;
+      ub = n1u ? b2u * 32 + n3u : 0;
+    }
     if (rule.op == PAS_OP_LESS_THAN) out = make_int2(0, lb);
     else if (rule.op == PAS_OP_GREATER_THAN) out = make_int2(ub, c);
     else out = make_int2(lb, ub);
   }
-  R.ranges[r] = out;
+  if (gl == 0) R.ranges[r] = out;
 }
 
 struct GroupParams {
@@ -175,8 +210,7 @@ constexpr int kGU = 4;  // pods per thread per round of loads (all issued before
 // are in flight together.
 __device__ void group_body(const GroupParams& g, int32_t* sh) {
   const int32_t G = 3 * g.M;
-  int32_t* partial = sh;                  // [kGroupTpb]
-  int32_t* hist = sh + kGroupTpb;         // [G + 1]
+  int32_t* hist = sh;  // [G + 1]
   const int tid = threadIdx.x;
   const bool prio = (g.flags & PAS_TAS_PRIORITIZE) != 0 && g.M > 0;
   for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
@@ -207,7 +241,7 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
     }
   }
   __syncthreads();
-  block_exclusive_scan(hist, G + 1, partial);
+  block_exclusive_scan(hist, G + 1);
   const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
   for (int32_t p0 = tid; p0 < g.P; p0 += kGroupTpb * kGU) {
     int2 kc[kGU];
@@ -232,27 +266,21 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
   }
 }
 
-__global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, RangesParams R) {
+__global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, RangesParams R,
+                                                             int ablate) {
   extern __shared__ __attribute__((aligned(16))) int32_t sh[];
   if (blockIdx.x == 0) {
-    group_body(g, sh);
+    if (!(ablate & 2)) group_body(g, sh);
     return;
   }
-  const int32_t r = (int32_t)(blockIdx.x - 1) * kGroupTpb + threadIdx.x;
-  if (r < R.n_rules) ranges_body(R, r);
+  if (ablate & 1) return;
+  const int32_t r =
+      (int32_t)(blockIdx.x - 1) * (kGroupTpb / kRuleLanes) + (int32_t)(threadIdx.x / kRuleLanes);
+  if (r < R.n_rules) ranges_group(R, r);
 }
 
 // ---------------------------------------------------------------------------- eval
 
-__device__ __forceinline__ int32_t wave_inclusive_sum(int32_t x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const int32_t y = __shfl_up(x, off, 64);
-    if (lane >= off) x += y;
-  }
-  return x;
-}
 
 // Barrier over the block's waves that orders LDS only: outstanding global loads and stores
 // stay in flight across it (a __syncthreads would wait for them; vmcnt counts stores).
@@ -271,6 +299,7 @@ __device__ __forceinline__ void lds_barrier() {
 // unconditional and range-checked against a buffer descriptor of exactly its part of the
 // run (out-of-range lanes store nothing), so there are no per-lane predicates; a call with
 // no kept entries issues the same 7 stores and writes nothing.
+template <int kAux>
 __device__ __forceinline__ void compact_store(int32_t* stage, uint32_t stage_off,
                                               const int32_t (&node)[kSegWords],
                                               const uint64_t (&keep)[kSegWords],
@@ -305,7 +334,7 @@ __device__ __forceinline__ void compact_store(int32_t* stage, uint32_t stage_off
 #pragma unroll
   for (int it = 0; it < kChunkIters; ++it)
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, v[it]), mid,
-                                           moff + it * 1024, 0, kNtAux);
+                                           moff + it * 1024, 0, kAux);
   const __amdgpu_buffer_rsrc_t head =
       __builtin_amdgcn_make_buffer_rsrc(line0 + a, 0, (head_end - a) * 4, 0x00020000);
   __builtin_amdgcn_raw_buffer_store_b32((uint32_t)hv, head, lane * 4, 0, 0);
@@ -350,7 +379,7 @@ struct EvalParams {
 // kS: adjacent segments per wave per round.  kAblate (diagnostic timing builds only,
 // PAS_EVAL_ABLATE; outputs wrong): 1 = no stores, 2 = no count exchange, 4 = no pass-bit
 // lookups, 8 = no rule loop.
-template <int kW, int kS, int kAblate>
+template <int kW, int kS, int kAblate, int kAux = kNtAux>
 __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
   constexpr int T = kW * 64;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -465,7 +494,7 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
       for (int j = 0; j < kSegWords; ++j) none[j] = 0;
 #pragma unroll
       for (int i = 0; i < kS; ++i)
-        compact_store(stage, stage_off, node[i], none, P.order_out, (int64_t)pod * N, lane);
+        compact_store<kAux>(stage, stage_off, node[i], none, P.order_out, (int64_t)pod * N, lane);
     }
     for (int32_t r = 0; r < rounds; ++r) {
       uint64_t keep[kS][kSegWords];
@@ -510,7 +539,7 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
 #pragma unroll
       for (int i = 0; i < kS; ++i) {
         if (!(kAblate & 1))
-          compact_store(stage, stage_off, node[i], keep[i], P.order_out,
+          compact_store<kAux>(stage, stage_off, node[i], keep[i], P.order_out,
                         (int64_t)pod * N + base, lane);
         base += cnt[i];
       }
@@ -583,6 +612,8 @@ struct TasTuning {
   int32_t seg_per_wave = 1;  // adjacent order segments per wave per round (1 or 2)
   int32_t no_group = 0;      // diagnostic: pods in index order (no XCD locality)
   int32_t ablate = 0;
+  int32_t prep_ablate = 0;
+  int32_t store_aux = kNtAux;  // cache policy of the whole-line stores
 };
 
 const TasTuning& tas_tuning() {
@@ -592,6 +623,8 @@ const TasTuning& tas_tuning() {
     x.seg_per_wave = env_int("PAS_EVAL_SEGS", x.seg_per_wave) == 2 ? 2 : 1;
     x.no_group = env_int("PAS_EVAL_NOGROUP", 0);
     x.ablate = env_int("PAS_EVAL_ABLATE", 0);
+    x.prep_ablate = env_int("PAS_PREP_ABLATE", 0);
+    x.store_aux = env_int("PAS_EVAL_AUX", x.store_aux);
     return x;
   }();
   return t;
@@ -648,15 +681,17 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   timing_begin(ctx, s, PAS_K_TAS_SPAN, &span);
   // ranges (blocks 1..) beside the grouping (block 0), one launch
   const int32_t range_rules = (flags & PAS_TAS_FILTER) ? n_rules : 0;
-  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, d_ranges};
+  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges};
   GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, tune.no_group};
-  const size_t group_lds = sizeof(int32_t) * ((size_t)kGroupTpb + G + 1);
+  const size_t group_lds = sizeof(int32_t) * ((size_t)G + 1);
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_prep_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_lds));
-  const unsigned prep_blocks = 1u + (unsigned)((range_rules + kGroupTpb - 1) / kGroupTpb);
+  constexpr int kRulesPerBlock = kGroupTpb / kRuleLanes;
+  const unsigned prep_blocks =
+      1u + (unsigned)((range_rules + kRulesPerBlock - 1) / kRulesPerBlock);
   timing_begin(ctx, s, PAS_K_TAS_PREP, &tl);
-  tas_prep_kernel<<<prep_blocks, kGroupTpb, group_lds, s>>>(gp, rp);
+  tas_prep_kernel<<<prep_blocks, kGroupTpb, group_lds, s>>>(gp, rp, tune.prep_ablate);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
 
@@ -677,6 +712,11 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   PAS_EVAL_CASE(4, 1, 1) PAS_EVAL_CASE(4, 1, 2) PAS_EVAL_CASE(4, 1, 4) PAS_EVAL_CASE(4, 1, 8)
   PAS_EVAL_CASE(4, 1, 7) PAS_EVAL_CASE(4, 2, 1) PAS_EVAL_CASE(4, 2, 2)
 #undef PAS_EVAL_CASE
+  if (tune.store_aux == 0) fn = &tas_eval_kernel<4, 1, 0, 0>;
+  if (tune.store_aux == 3) fn = &tas_eval_kernel<4, 1, 0, 3>;
+  if (tune.store_aux == 16) fn = &tas_eval_kernel<4, 1, 0, 16>;
+  if (tune.store_aux == 18) fn = &tas_eval_kernel<4, 1, 0, 18>;
+  if (tune.store_aux == 19) fn = &tas_eval_kernel<4, 1, 0, 19>;
   if (eval_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds));

@@ -77,6 +77,19 @@ __global__ void segment_bounds(const uint32_t* __restrict__ scan, int32_t R, int
   seg_end[m] = m * R + c;
 }
 
+// f32[m][b] = sorted[m][32 b], and f1k[m][a] = sorted[m][1024 a], for positions < cnt[m]
+__global__ void build_fences(const int64_t* __restrict__ sorted, const int32_t* __restrict__ cnt,
+                             int32_t R, int32_t M, int64_t* __restrict__ f1k,
+                             int64_t* __restrict__ f32) {
+  const int32_t nb = R >> 5;
+  const int64_t i = (int64_t)blockIdx.x * kTpb + threadIdx.x;
+  if (i >= (int64_t)M * nb) return;
+  const int32_t m = (int32_t)(i / nb), b = (int32_t)(i % nb);
+  const int64_t v = b * 32 < cnt[m] ? sorted[(int64_t)m * R + b * 32] : 0;
+  f32[i] = v;
+  if ((b & 31) == 0) f1k[(int64_t)m * (R >> 10) + (b >> 5)] = v;
+}
+
 }  // namespace
 
 int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
@@ -104,6 +117,8 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     PAS_HIP(ctx, hipMalloc(&t.sorted, sizeof(int64_t) * mr));
     PAS_HIP(ctx, hipMalloc(&t.perm, sizeof(int32_t) * mr * kNumOrders));
     PAS_HIP(ctx, hipMalloc(&t.vals_c, sizeof(int64_t) * mr));
+    PAS_HIP(ctx, hipMalloc(&t.f1k, sizeof(int64_t) * (mr / 1024 + 1)));
+    PAS_HIP(ctx, hipMalloc(&t.f32, sizeof(int64_t) * (mr / 32 + 1)));
     PAS_HIP(ctx, hipMalloc(&t.word_scan, sizeof(uint32_t) * (mw + 1)));
     PAS_HIP(ctx, hipMalloc(&t.seg_begin, sizeof(int32_t) * mm));
     PAS_HIP(ctx, hipMalloc(&t.seg_end, sizeof(int32_t) * mm));
@@ -161,6 +176,9 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     PAS_HIP(ctx, rocprim::segmented_radix_sort_pairs(
                      t.sort_tmp, sort_bytes, t.vals_c, t.sorted, perm_index, perm_asc,
                      (unsigned)MR, (unsigned)M, t.seg_begin, t.seg_end, 0, 64, s));
+    build_fences<<<(unsigned)((MR / 32 + kTpb - 1) / kTpb), kTpb, 0, s>>>(t.sorted, t.cnt, R, M,
+                                                                          t.f1k, t.f32);
+    PAS_HIP(ctx, hipGetLastError());
   }
   t.gen = gen;
   t.valid = true;
