@@ -7,14 +7,21 @@
 //   per-GPU request to that card's usage (addRM, resource_map.go:38-53), so later
 //   selections of the same pod see it; no fit -> errWontFit.
 //
-// Device formulation: one lane per node, holding the node's frozen per-card usage
-// (Cache.getNodeResourceStatus, node_resource_cache.go:474-491) in registers, walks a
-// chunk of pods (the pod loop is wave-uniform, so container/step tables are scalar
-// loads).  checkResourceCapacity for a requested kind q with need >= 0 and cap > 0 is
-// exactly   0 <= used <= cap - need   (then used + need cannot overflow), i.e. one
-// unsigned 64-bit compare against slack = cap - need; kinds not requested get
-// slack = UINT64_MAX.  A negative need or non-positive cap on a requested kind makes
-// the container unplaceable on this node (:343-354).
+// Device formulation: one lane per node holds the node's free capacity per card and kind,
+//   free[k][q] = cap[q] - used[k][q]   if cap[q] > 0 and used[k][q] >= 0, else -1
+// (cards in lexicographic order; missing cards -1), built once from the frozen snapshot
+// (Cache.getNodeResourceStatus, node_resource_cache.go:474-491).  For a requested kind
+// with need >= 0, checkResourceCapacity (:341-383) holds exactly when need <= free: a
+// non-positive capacity or negative usage gives -1, and used + need overflowing int64
+// means need > INT64_MAX - used >= free.  Taking a card (addRM) is free -= need.  A
+// negative need on a requested kind fails every card (:343-347).
+//
+// The pod loop is wave-uniform: pod records are staged in LDS per batch and read into
+// SGPRs, so each card check is one 64-bit compare against an SGPR.  The prep kernel splits
+// the batch: pods with at most one card selection (the common case: one container, one
+// i915) go to a kernel that only reads free; pods with several selections go to a kernel
+// that takes cards in place (per-card lane-masked updates) and undoes them afterwards, so
+// the first kernel keeps a small register footprint.
 #include <hip/hip_runtime.h>
 
 #include "pas_internal.h"
@@ -24,119 +31,295 @@ namespace {
 
 constexpr int kTpb = 256;
 constexpr int kMaxCards = PAS_GAS_MAX_CARDS;
+constexpr int kPodBatch = 64;  // pod records staged in LDS per round
 
-// Per (pod, container) step table built by gas_prep_kernel.
-struct alignas(16) GasContainer {
-  int64_t req[PAS_GAS_MAX_RES];  // per-GPU request (getPerGPUResourceRequest :180-190); 0 if
-                                 // the kind is not requested
-  uint32_t mask;                 // requested kinds
-  int32_t num_i915;              // getNumI915 (:192-198)
+// A (pod, container) step, in compare form: cmp[q] = per-GPU need of a requested kind
+// (getPerGPUResourceRequest :180-190), INT64_MIN for the others, so every card passes them
+// and the check needs no mask; take[q] = the need, 0 for the others (addRM).
+struct alignas(16) GasStep {
+  int64_t cmp[PAS_GAS_MAX_RES];
+  int64_t take[PAS_GAS_MAX_RES];
+  int32_t num_i915;  // getNumI915 (:192-198); 0 = no selection (skipped, :206-208, :215)
+  int32_t bad;       // a requested kind has a negative per-GPU need (:343-347)
   int32_t pad[2];
+};
+
+// One card selection of a pod with several: compare and take vectors (kinds as GasStep).
+struct alignas(16) GasSel {
+  int64_t cmp[PAS_GAS_MAX_RES];
+  int64_t take[PAS_GAS_MAX_RES];
+  int32_t bad;
+  int32_t pad[3];
+};
+constexpr int kMultiBatch = 8;  // multi-selection pods staged in LDS per round
+
+// Pod with at most one card selection: its selecting step, or steps == 0.
+struct alignas(16) GasSingle {
+  int64_t cmp[PAS_GAS_MAX_RES];
+  int32_t pod;
+  int32_t steps;
+  int32_t bad;
+  int32_t pad;
 };
 
 // getPerGPUResourceRequest: copy the container's map and, when numI915 > 1, divide
 // every entry (the i915 entry included) by numI915, truncating (resource_map.go:129-145).
-__global__ void gas_prep_kernel(int32_t n, int32_t n_res, int32_t i915,
-                                const int64_t* __restrict__ req,
-                                const uint32_t* __restrict__ mask,
-                                GasContainer* __restrict__ out) {
-  const int32_t i = blockIdx.x * kTpb + threadIdx.x;
-  if (i >= n) return;
-  GasContainer g;
-  g.mask = mask[i];
+__device__ GasStep container_step(int64_t i, int32_t n_res, int32_t i915,
+                                  const int64_t* __restrict__ req,
+                                  const uint32_t* __restrict__ mask) {
+  const uint32_t m = mask[i];
   int64_t ni = 0;
-  if (i915 >= 0 && ((g.mask >> i915) & 1u)) {
-    const int64_t v = req[(int64_t)i * n_res + i915];
+  if (i915 >= 0 && ((m >> i915) & 1u)) {
+    const int64_t v = req[i * n_res + i915];
     if (v > 0) ni = v;
   }
-  g.num_i915 = (int32_t)ni;
+  GasStep g = {};
+  g.num_i915 = m != 0u ? (int32_t)min(ni, (int64_t)PAS_GAS_MAX_SELECTIONS + 1) : 0;
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
-    int64_t v = 0;
-    if (q < n_res && ((g.mask >> q) & 1u)) {
-      v = req[(int64_t)i * n_res + q];
-      if (ni > 1) v /= ni;
-    }
-    g.req[q] = v;
+    const bool has = q < n_res && ((m >> q) & 1u);
+    int64_t v = has ? req[i * n_res + q] : 0;
+    if (ni > 1) v /= ni;
+    if (has && v < 0) g.bad = 1;
+    g.take[q] = v;
+    g.cmp[q] = has ? v : INT64_MIN;
   }
-  g.pad[0] = g.pad[1] = 0;
-  out[i] = g;
+  return g;
 }
 
+// One thread per pod files it under `single` (<= 1 selection: its selecting step) or
+// `multi` (several: its steps, containers in order then gpuNum, expanded into its slot of
+// the selection list; more than PAS_GAS_MAX_SELECTIONS are beyond the packed result and
+// keep only the count).
+__global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
+                                int32_t i915, const int64_t* __restrict__ req,
+                                const uint32_t* __restrict__ mask,
+                                const int32_t* __restrict__ n_containers,
+                                GasSingle* __restrict__ single, int32_t* __restrict__ multi,
+                                GasSel* __restrict__ sels, int32_t* __restrict__ counts) {
+  const int32_t p = blockIdx.x * kTpb + threadIdx.x;
+  if (p >= n_pods) return;
+  const int32_t nc = min(max(n_containers[p], 0), max_containers);
+  const int64_t row = (int64_t)p * max_containers;
+  int32_t steps = 0;
+  GasSingle one = {};
+  one.pod = p;
+  for (int32_t c = 0; c < nc; ++c) {
+    const GasStep g = container_step(row + c, n_res, i915, req, mask);
+    if (g.num_i915 > 0) {
+      if (steps == 0) {
+#pragma unroll
+        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) one.cmp[q] = g.cmp[q];
+        one.bad = g.bad;
+      }
+      steps = min(steps + g.num_i915, PAS_GAS_MAX_SELECTIONS + 1);
+    }
+  }
+  if (steps <= 1) {
+    one.steps = steps;
+    single[atomicAdd(&counts[0], 1)] = one;
+    return;
+  }
+  const int32_t slot = atomicAdd(&counts[1], 1);
+  multi[slot] = p | (steps << 24);
+  if (steps > PAS_GAS_MAX_SELECTIONS) return;
+  GasSel* out = sels + (int64_t)slot * PAS_GAS_MAX_SELECTIONS;
+  int32_t k = 0;
+  for (int32_t c = 0; c < nc; ++c) {
+    const GasStep g = container_step(row + c, n_res, i915, req, mask);
+    for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
+      GasSel e = {};
+#pragma unroll
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+        e.cmp[q] = g.cmp[q];
+        e.take[q] = g.take[q];
+      }
+      e.bad = g.bad;
+      out[k] = e;
+    }
+  }
+}
+
+// free[k][q] = cap[q] - used[k][q] if cap[q] > 0 and used[k][q] >= 0, else -1 (and -1 for
+// cards the node does not have).
 template <int Q>
-__global__ __launch_bounds__(kTpb) void gas_fit_kernel(
-    int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
-    const int64_t* __restrict__ used, int32_t n_pods, int32_t pods_per_block, int32_t C, int32_t max_containers,
-    const GasContainer* __restrict__ table, const int32_t* __restrict__ n_containers,
-    uint32_t* __restrict__ res) {
-  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
+__device__ __forceinline__ void load_free(int32_t n, bool valid, int32_t ncard, int32_t K,
+                                          const int64_t* __restrict__ cap,
+                                          const int64_t* __restrict__ used,
+                                          int64_t (&free)[kMaxCards][Q]) {
   int64_t cap_r[Q];
-  int64_t snap[kMaxCards][Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) cap_r[q] = valid ? cap[(int64_t)n * Q + q] : 0;
 #pragma unroll
   for (int k = 0; k < kMaxCards; ++k)
 #pragma unroll
-    for (int q = 0; q < Q; ++q)
-      snap[k][q] = (valid && k < K) ? used[((int64_t)n * K + k) * Q + q] : 0;
+    for (int q = 0; q < Q; ++q) {
+      const int64_t u = k < ncard ? used[((int64_t)n * K + k) * Q + q] : -1;
+      free[k][q] = (cap_r[q] > 0 && u >= 0) ? cap_r[q] - u : -1;
+    }
+}
 
-  const int32_t p0 = blockIdx.y * pods_per_block;
-  const int32_t p1 = min(n_pods, p0 + pods_per_block);
-  for (int32_t p = p0; p < p1; ++p) {
-    // FetchNode error / missing cards label -> errWontFit before any container
-    // (scheduler.go:282-298).
-    bool fits = nc > 0;
-    uint32_t word = 0;
-    int32_t nsel = 0;
-    int64_t u[kMaxCards][Q];
+// First card (lexicographic rank) passing checkResourceCapacity, or -1: cmp[q] <= free[k][q]
+// for every kind (cmp is INT64_MIN for kinds the container does not request).
+template <int Q>
+__device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
+                                         const int64_t (&cmp)[Q]) {
+  int chosen = -1;
 #pragma unroll
-    for (int k = 0; k < kMaxCards; ++k)
+  for (int k = kMaxCards - 1; k >= 0; --k) {  // first fit = lowest k
+    bool ok = true;
 #pragma unroll
-      for (int q = 0; q < Q; ++q) u[k][q] = snap[k][q];
-    const int32_t ncont = min(n_containers[p], max_containers);
-    for (int32_t c = 0; c < ncont; ++c) {
-      const GasContainer& g = table[(int64_t)p * C + c];
-      const uint32_t mask = g.mask;
-      const int32_t ni = g.num_i915;
-      if (mask == 0u || ni == 0) continue;  // no GPU request / zero gpuNum iterations
-      uint64_t slack[Q];
-      bool placeable = true;
+    for (int q = 0; q < Q; ++q) ok = ok && cmp[q] <= free[k][q];
+    chosen = ok ? k : chosen;
+  }
+  return chosen;
+}
+
+__device__ __forceinline__ int64_t uniform64(int64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// This block's share [*b, *e) of a device-counted list, split evenly over gridDim.y.
+__device__ __forceinline__ void list_share(const int32_t* count, int32_t* b, int32_t* e) {
+  const int32_t cnt = __builtin_amdgcn_readfirstlane(*count);
+  const int32_t per = (cnt + (int32_t)gridDim.y - 1) / (int32_t)gridDim.y;
+  *b = min(cnt, (int32_t)blockIdx.y * per);
+  *e = min(cnt, *b + per);
+}
+
+// Pods with at most one selection: a read-only first fit per (pod, node lane).
+template <int Q>
+__global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
+    int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
+    const int64_t* __restrict__ used, const GasSingle* __restrict__ single,
+    const int32_t* __restrict__ counts, uint32_t* __restrict__ res) {
+  __shared__ GasSingle stage[kPodBatch];
+  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  int64_t free[kMaxCards][Q];
+  load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
+  // FetchNode error / missing cards label -> errWontFit before any container (:282-298)
+  const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
+  int32_t i0, i1;
+  list_share(&counts[0], &i0, &i1);
+  for (int32_t b0 = i0; b0 < i1; b0 += kPodBatch) {
+    const int32_t nb = min(kPodBatch, i1 - b0);
+    constexpr int kWords = (int)(sizeof(GasSingle) / 16);
+    const int4* src = reinterpret_cast<const int4*>(single + b0);
+    int4* dst = reinterpret_cast<int4*>(stage);
+    for (int32_t i = threadIdx.x; i < nb * kWords; i += kTpb) dst[i] = src[i];
+    __syncthreads();
+    for (int32_t j = 0; j < nb; ++j) {
+      const GasSingle& r = stage[j];  // broadcast LDS reads, then SGPRs
+      const int64_t pod = __builtin_amdgcn_readfirstlane(r.pod);
+      uint32_t out = node_ok;
+      if (__builtin_amdgcn_readfirstlane(r.steps) == 1) {
+        int64_t cmp[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        if ((mask >> q) & 1u) {
-          const int64_t need = g.req[q];
-          if (need < 0 || cap_r[q] <= 0) placeable = false;
-          const int64_t s = (int64_t)((uint64_t)cap_r[q] - (uint64_t)need);
-          if (s < 0) placeable = false;
-          slack[q] = (uint64_t)s;
-        } else {
-          slack[q] = ~0ull;
-        }
+        for (int q = 0; q < Q; ++q) cmp[q] = uniform64(r.cmp[q]);
+        const int k = __builtin_amdgcn_readfirstlane(r.bad) ? -1 : first_fit<Q>(free, cmp);
+        out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
       }
-      if (!placeable) fits = false;
-      for (int32_t step = 0; step < ni; ++step) {
-        int chosen = -1;
+      if (valid) res[pod * N + n] = out;
+    }
+    __syncthreads();  // the next batch rewrites the stage
+  }
+}
+
+// Pods with several selections: the steps in order (containers, then gpuNum), each taking
+// the first fitting card (free drops by the need for the following steps).  Two
+// selections need no state (the second sees the first take added to card c0's need);
+// more work on a copy of free.  Pod step lists are staged in LDS per batch.
+template <int Q>
+__global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
+    int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
+    const int64_t* __restrict__ used, const int32_t* __restrict__ multi,
+    const GasSel* __restrict__ sels, const int32_t* __restrict__ counts,
+    uint32_t* __restrict__ res) {
+  __shared__ GasSel stage[kMultiBatch][PAS_GAS_MAX_SELECTIONS];
+  __shared__ int32_t stage_pod[kMultiBatch];
+  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  int64_t free[kMaxCards][Q];
+  load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
+  const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
+  int32_t i0, i1;
+  list_share(&counts[1], &i0, &i1);
+  for (int32_t b0 = i0; b0 < i1; b0 += kMultiBatch) {
+    const int32_t nb = min(kMultiBatch, i1 - b0);
+    constexpr int kWords = (int)(sizeof(GasSel) / 16) * PAS_GAS_MAX_SELECTIONS;
+    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * PAS_GAS_MAX_SELECTIONS);
+    int4* dst = reinterpret_cast<int4*>(&stage[0][0]);
+    for (int32_t i = threadIdx.x; i < nb * kWords; i += kTpb) dst[i] = src[i];
+    if (threadIdx.x < nb) stage_pod[threadIdx.x] = multi[b0 + threadIdx.x];
+    __syncthreads();
+    for (int32_t j = 0; j < nb; ++j) {
+      const int32_t pw = __builtin_amdgcn_readfirstlane(stage_pod[j]);
+      const int64_t p = pw & 0xFFFFFF;
+      const int32_t steps = pw >> 24;
+      uint32_t out = 0u;
+      if (steps == 2) {
+        // two selections without touching free: the second one sees card c0 with the
+        // first take added to its need, every other card as it was
+        const GasSel& e0 = stage[j][0];
+        const GasSel& e1 = stage[j][1];
+        int64_t cmp0[Q], cmp1[Q], cmp1t[Q];
 #pragma unroll
-        for (int k = kMaxCards - 1; k >= 0; --k) {  // first fit = lowest k
-          bool ok = k < nc;
-#pragma unroll
-          for (int q = 0; q < Q; ++q) ok = ok && ((uint64_t)u[k][q] <= slack[q]);
-          if (ok) chosen = k;
+        for (int q = 0; q < Q; ++q) {
+          cmp0[q] = uniform64(e0.cmp[q]);
+          cmp1[q] = uniform64(e1.cmp[q]);
+          cmp1t[q] = cmp1[q] + uniform64(e0.take[q]);  // INT64_MIN + 0 stays unrequested
         }
-        if (chosen < 0) fits = false;
+        const int c0 = __builtin_amdgcn_readfirstlane(e0.bad) ? -1 : first_fit<Q>(free, cmp0);
+        int c1 = -1;
+        if (!__builtin_amdgcn_readfirstlane(e1.bad)) {
+#pragma unroll
+          for (int k = kMaxCards - 1; k >= 0; --k) {
+            bool ok = true;
+#pragma unroll
+            for (int q = 0; q < Q; ++q) ok = ok && (c0 == k ? cmp1t[q] : cmp1[q]) <= free[k][q];
+            c1 = ok ? k : c1;
+          }
+        }
+        out = (c0 >= 0 && c1 >= 0) ? (node_ok | (2u << 24) | (uint32_t)c0 | ((uint32_t)c1 << 3))
+                                   : 0u;
+      } else if (steps <= PAS_GAS_MAX_SELECTIONS) {
+        // three or more selections: take cards in a working copy of free
+        int64_t w[kMaxCards][Q];
 #pragma unroll
         for (int k = 0; k < kMaxCards; ++k)
 #pragma unroll
-          for (int q = 0; q < Q; ++q)
-            if (chosen == k) u[k][q] += g.req[q];
-        word |= (uint32_t)(chosen & 7) << (3 * nsel);
-        ++nsel;
+          for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
+        bool fits = true;
+        uint32_t word = 0;
+        for (int32_t t = 0; t < steps; ++t) {
+          const GasSel& e = stage[j][t];  // broadcast LDS reads, then SGPRs
+          int64_t cmp[Q], take[Q];
+#pragma unroll
+          for (int q = 0; q < Q; ++q) {
+            cmp[q] = uniform64(e.cmp[q]);
+            take[q] = uniform64(e.take[q]);
+          }
+          const int k = __builtin_amdgcn_readfirstlane(e.bad) ? -1 : first_fit<Q>(w, cmp);
+          fits = fits && k >= 0;
+          // per card taken by some lane of the wave (uniform branch), a per-lane select: a
+          // divergent branch around the update would make the compiler copy the array
+#pragma unroll
+          for (int kk = 0; kk < kMaxCards; ++kk)
+            if (__ballot(k == kk))
+#pragma unroll
+              for (int q = 0; q < Q; ++q) w[kk][q] -= k == kk ? take[q] : 0;
+          word |= (uint32_t)(k & 7) << (3 * t);
+        }
+        out = fits ? (node_ok | ((uint32_t)steps << 24) | word) : 0u;
       }
+      if (valid) res[p * N + n] = out;
     }
-    if (valid)
-      res[(int64_t)p * N + n] = fits ? (0x80000000u | ((uint32_t)nsel << 24) | word) : 0u;
+    __syncthreads();  // the next batch rewrites the stage
   }
 }
 
@@ -148,40 +331,53 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
   if (N == 0 || n_pods == 0) return PAS_OK;
-  const int32_t C = std::max(max_containers, 1);
-  const size_t table_bytes = sizeof(GasContainer) * (size_t)n_pods * C;
-  if (table_bytes > ctx->aux_bytes) {
+  // scratch: single-selection records | multi-selection pod words | their selection lists
+  // | 2 counts
+  if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
+  const size_t b_single = (sizeof(GasSingle) * (size_t)n_pods + 255) & ~size_t(255);
+  const size_t b_multi = (sizeof(int32_t) * (size_t)n_pods + 255) & ~size_t(255);
+  const size_t b_sels =
+      (sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS * (size_t)n_pods + 255) & ~size_t(255);
+  const size_t need = b_single + b_multi + b_sels + 256;
+  if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
       PAS_HIP(ctx, hipFree(ctx->aux));
       ctx->aux = nullptr;
       ctx->aux_bytes = 0;
     }
-    PAS_HIP(ctx, hipMalloc(&ctx->aux, table_bytes));
-    ctx->aux_bytes = table_bytes;
+    PAS_HIP(ctx, hipMalloc(&ctx->aux, need));
+    ctx->aux_bytes = need;
   }
-  GasContainer* table = static_cast<GasContainer*>(ctx->aux);
+  char* base = static_cast<char*>(ctx->aux);
+  GasSingle* single = reinterpret_cast<GasSingle*>(base);
+  int32_t* multi = reinterpret_cast<int32_t*>(base + b_single);
+  GasSel* sels = reinterpret_cast<GasSel*>(base + b_single + b_multi);
+  int32_t* counts = reinterpret_cast<int32_t*>(base + b_single + b_multi + b_sels);
   TimedLaunch tl;
-  const int32_t n_entries = n_pods * max_containers;
-  if (n_entries > 0) {
-    timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
-    gas_prep_kernel<<<(n_entries + kTpb - 1) / kTpb, kTpb, 0, s>>>(n_entries, Q, i915_index,
-                                                                  d_req, d_req_mask, table);
-    timing_end(ctx, s, &tl);
-    PAS_HIP(ctx, hipGetLastError());
-  }
+  timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
+  PAS_HIP(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int32_t), s));
+  gas_prep_kernel<<<(n_pods + kTpb - 1) / kTpb, kTpb, 0, s>>>(
+      n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, single, multi,
+      sels, counts);
+  timing_end(ctx, s, &tl);
+  PAS_HIP(ctx, hipGetLastError());
+  // grids: node blocks x pod chunks, ~4096 blocks for the whole batch; each kernel splits
+  // its device-counted list evenly over its chunks
   const int32_t node_blocks = (N + kTpb - 1) / kTpb;
-  const int32_t target_blocks = 4096;
-  int32_t chunks = std::max(1, std::min(n_pods, (target_blocks + node_blocks - 1) / node_blocks));
-  const int32_t ppb = (n_pods + chunks - 1) / chunks;
-  chunks = (n_pods + ppb - 1) / ppb;
+  const int32_t chunks = std::max(1, std::min(n_pods, (4096 + node_blocks - 1) / node_blocks));
   const dim3 grid((unsigned)node_blocks, (unsigned)chunks);
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   switch (Q) {
-    case 1: gas_fit_kernel<1><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, n_pods, ppb, C, max_containers, table, d_n_containers, d_res); break;
-    case 2: gas_fit_kernel<2><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, n_pods, ppb, C, max_containers, table, d_n_containers, d_res); break;
-    case 3: gas_fit_kernel<3><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, n_pods, ppb, C, max_containers, table, d_n_containers, d_res); break;
-    default: gas_fit_kernel<4><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, n_pods, ppb, C, max_containers, table, d_n_containers, d_res); break;
+#define PAS_GAS_CASE(QQ)                                                                        \
+  case QQ:                                                                                      \
+    gas_fit_single_kernel<QQ><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, single,   \
+                                                    counts, d_res);                             \
+    gas_fit_multi_kernel<QQ><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, multi,     \
+                                                   sels, counts, d_res);                       \
+    break;
+    PAS_GAS_CASE(1) PAS_GAS_CASE(2) PAS_GAS_CASE(3) default: PAS_GAS_CASE(4)
+#undef PAS_GAS_CASE
   }
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
