@@ -216,6 +216,42 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
                        int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
                        const int32_t* d_n_containers, uint32_t* d_res_out, void* hip_stream);
 
+/* GAS filter verdicts only, as node bitmaps fit_out[n_pods][W64(n_nodes)] (bit = bit 31 of
+ * the pas_gas_fit word).  Used to intersect GAS with TAS candidates (cand of the TAS calls)
+ * without materialising the per-(pod, node) words. */
+int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                              int32_t i915_index, const int64_t* d_req,
+                              const uint32_t* d_req_mask, const int32_t* d_n_containers,
+                              uint64_t* d_fit_out, void* hip_stream);
+
+/* ------------------------------------------------------------------------- */
+/* Node-sharded snapshots                                  */
+/* ------------------------------------------------------------------------- */
+
+/* A GPU holding nodes [node_base, node_base + n_nodes) of the cluster as its resident
+ * TAS snapshot evaluates every pod's filter + prioritize over that shard and keeps the
+ * first k entries of the shard's HostPriorityList (as pas_tas_eval_device with both flags
+ * would list them) as merge records:
+ *   top_node [n_pods][k]  global node index (node_base + shard index); INT32_MAX past len
+ *   top_key  [n_pods][k]  order key: ~value for GreaterThan, value for LessThan, 0 for any
+ *                         other operator (value = the node's v_milli of the prioritize
+ *                         metric); INT64_MAX past len
+ *   top_len  [n_pods]     min(k, entries)
+ * Ascending (key, node) is the HostPriorityList order, so the merge of all shards' records
+ * (pas_topk_merge_device) is exactly the first k entries over the whole cluster. */
+int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_rules,
+                        const pas_rule* d_rules, const int32_t* d_rule_off,
+                        const pas_rule* d_prio, const uint64_t* d_cand, int32_t k,
+                        int32_t node_base, int64_t* d_top_key, int32_t* d_top_node,
+                        int32_t* d_top_len, void* hip_stream);
+
+/* Merge of n_shards record sets laid out [n_shards][n_pods][k] (the layout of an
+ * all-gather of the per-shard top_key / top_node): out_node[n_pods][k] = the k smallest
+ * (key, node) records' nodes in order (-1 past out_len), out_len = min(k, records). */
+int pas_topk_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
+                          const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
+                          int32_t* d_out_len, void* hip_stream);
+
 /* ------------------------------------------------------------------------- */
 /* Instrumentation                                                           */
 /* ------------------------------------------------------------------------- */

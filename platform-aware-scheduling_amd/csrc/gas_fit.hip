@@ -181,6 +181,21 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
   return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// One (pod, node) result: the packed word, or (kBits) the fit bit in the pod's row of a
+// node bitmap, written per 64-node word by lane 0 of the wave (waves cover aligned
+// 64-node ranges).
+template <bool kBits>
+__device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t* __restrict__ fit,
+                                           int64_t p, int32_t N, int32_t n, bool valid,
+                                           uint32_t out) {
+  if (kBits) {
+    const uint64_t b = __ballot(valid && (out >> 31));
+    if ((threadIdx.x & 63) == 0 && n < N) fit[p * ((N + 63) / 64) + (n >> 6)] = b;
+  } else if (valid) {
+    res[p * N + n] = out;
+  }
+}
+
 // This block's share [*b, *e) of a device-counted list, split evenly over gridDim.y.
 __device__ __forceinline__ void list_share(const int32_t* count, int32_t* b, int32_t* e) {
   const int32_t cnt = __builtin_amdgcn_readfirstlane(*count);
@@ -190,11 +205,11 @@ __device__ __forceinline__ void list_share(const int32_t* count, int32_t* b, int
 }
 
 // Pods with at most one selection: a read-only first fit per (pod, node lane).
-template <int Q>
+template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
     int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
     const int64_t* __restrict__ used, const GasSingle* __restrict__ single,
-    const int32_t* __restrict__ counts, uint32_t* __restrict__ res) {
+    const int32_t* __restrict__ counts, uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
   __shared__ GasSingle stage[kPodBatch];
   const int32_t n = blockIdx.x * kTpb + threadIdx.x;
   const bool valid = n < N;
@@ -223,7 +238,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
         const int k = __builtin_amdgcn_readfirstlane(r.bad) ? -1 : first_fit<Q>(free, cmp);
         out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
       }
-      if (valid) res[pod * N + n] = out;
+      put_result<kBits>(res, fit, pod, N, n, valid, out);
     }
     __syncthreads();  // the next batch rewrites the stage
   }
@@ -233,12 +248,12 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
 // the first fitting card (free drops by the need for the following steps).  Two
 // selections need no state (the second sees the first take added to card c0's need);
 // more work on a copy of free.  Pod step lists are staged in LDS per batch.
-template <int Q>
+template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
     const int64_t* __restrict__ used, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts,
-    uint32_t* __restrict__ res) {
+    uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
   __shared__ GasSel stage[kMultiBatch][PAS_GAS_MAX_SELECTIONS];
   __shared__ int32_t stage_pod[kMultiBatch];
   const int32_t n = blockIdx.x * kTpb + threadIdx.x;
@@ -317,7 +332,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
         }
         out = fits ? (node_ok | ((uint32_t)steps << 24) | word) : 0u;
       }
-      if (valid) res[p * N + n] = out;
+      put_result<kBits>(res, fit, p, N, n, valid, out);
     }
     __syncthreads();  // the next batch rewrites the stage
   }
@@ -327,7 +342,8 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
 
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
-                   const int32_t* d_n_containers, uint32_t* d_res, hipStream_t s) {
+                   const int32_t* d_n_containers, uint32_t* d_res, uint64_t* d_fit,
+                   hipStream_t s) {
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
   if (N == 0 || n_pods == 0) return PAS_OK;
@@ -368,16 +384,19 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const int32_t chunks = std::max(1, std::min(n_pods, (4096 + node_blocks - 1) / node_blocks));
   const dim3 grid((unsigned)node_blocks, (unsigned)chunks);
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
-  switch (Q) {
-#define PAS_GAS_CASE(QQ)                                                                        \
-  case QQ:                                                                                      \
-    gas_fit_single_kernel<QQ><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, single,   \
-                                                    counts, d_res);                             \
-    gas_fit_multi_kernel<QQ><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, multi,     \
-                                                   sels, counts, d_res);                       \
+  const bool bits = d_fit != nullptr;
+  switch (Q * 2 + (bits ? 1 : 0)) {
+#define PAS_GAS_CASE(QQ, B)                                                                     \
+  case QQ * 2 + B:                                                                              \
+    gas_fit_single_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, single, \
+                                                       counts, d_res, d_fit);                   \
+    gas_fit_multi_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, multi,   \
+                                                      sels, counts, d_res, d_fit);              \
     break;
-    PAS_GAS_CASE(1) PAS_GAS_CASE(2) PAS_GAS_CASE(3) default: PAS_GAS_CASE(4)
+    PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
+    PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
 #undef PAS_GAS_CASE
+    default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   }
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());

@@ -442,7 +442,7 @@ int pas_tas_eval(pas_ctx* ctx, uint64_t gen, int32_t n_pods, const pas_rule* rul
   PAS_HIP(ctx, hipMemcpyAsync(d_prio, prio, b_prio, hipMemcpyHostToDevice, s));
   if (d_cand) PAS_HIP(ctx, hipMemcpyAsync(d_cand, cand, b_cand, hipMemcpyHostToDevice, s));
   rc = tas_eval_launch(ctx, n_pods, n_rules, d_rules, d_off, d_prio, d_cand, flags, d_pass,
-                       d_order, d_len, s);
+                       d_order, d_len, 0, s);
   if (rc) return rc;
   if (d_pass) PAS_HIP(ctx, hipMemcpyAsync(pass_out, d_pass, b_pass, hipMemcpyDeviceToHost, s));
   if (flags & PAS_TAS_PRIORITIZE) {
@@ -471,7 +471,7 @@ int pas_tas_eval_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
     return set_error(ctx, PAS_EINVAL, "pas_tas_eval_device: PRIORITIZE without outputs");
   if ((rc = activate(ctx))) return rc;
   return tas_eval_launch(ctx, n_pods, n_rules, d_rules, d_rule_off, d_prio, d_cand, flags,
-                         d_pass_out, d_order_out, d_order_len, pick_stream(ctx, hip_stream));
+                         d_pass_out, d_order_out, d_order_len, 0, pick_stream(ctx, hip_stream));
 }
 
 int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const pas_rule* rules,
@@ -661,7 +661,8 @@ int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containe
     PAS_HIP(ctx, hipMemcpyAsync(d_mask, req_mask, b_mask, hipMemcpyHostToDevice, s));
   }
   PAS_HIP(ctx, hipMemcpyAsync(d_nc, n_containers, b_nc, hipMemcpyHostToDevice, s));
-  rc = gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_mask, d_nc, d_res, s);
+  rc = gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_mask, d_nc, d_res,
+                      nullptr, s);
   if (rc) return rc;
   if (b_res) PAS_HIP(ctx, hipMemcpyAsync(res_out, d_res, b_res, hipMemcpyDeviceToHost, s));
   PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -681,7 +682,63 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_device: null input");
   if ((rc = activate(ctx))) return rc;
   return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                        d_n_containers, d_res_out, pick_stream(ctx, hip_stream));
+                        d_n_containers, d_res_out, nullptr, pick_stream(ctx, hip_stream));
+}
+
+int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                              int32_t i915_index, const int64_t* d_req,
+                              const uint32_t* d_req_mask, const int32_t* d_n_containers,
+                              uint64_t* d_fit_out, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_gas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_pods < 0 || max_containers < 0 || i915_index >= ctx->gas.n_res || i915_index < -1)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_bitmap_device: bad shape");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_n_containers || !d_fit_out || (max_containers > 0 && (!d_req || !d_req_mask)))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_bitmap_device: null input");
+  if ((rc = activate(ctx))) return rc;
+  return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                        d_n_containers, nullptr, d_fit_out, pick_stream(ctx, hip_stream));
+}
+
+// --------------------------------------------------------------------------- node shards
+
+int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_rules,
+                        const pas_rule* d_rules, const int32_t* d_rule_off,
+                        const pas_rule* d_prio, const uint64_t* d_cand, int32_t k,
+                        int32_t node_base, int64_t* d_top_key, int32_t* d_top_node,
+                        int32_t* d_top_len, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_pods < 0 || n_rules < 0 || k < 1 || node_base < 0)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_topk_device: bad shape");
+  if ((int64_t)node_base + ctx->tas.n_nodes > INT32_MAX)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_topk_device: node ids past int32");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_rule_off || !d_prio || (n_rules > 0 && !d_rules) || !d_top_key || !d_top_node ||
+      !d_top_len)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_topk_device: null argument");
+  if ((rc = activate(ctx))) return rc;
+  return tas_topk_launch(ctx, n_pods, n_rules, d_rules, d_rule_off, d_prio, d_cand, k,
+                         node_base, d_top_key, d_top_node, d_top_len,
+                         pick_stream(ctx, hip_stream));
+}
+
+int pas_topk_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
+                          const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
+                          int32_t* d_out_len, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_pods < 0 || k < 1 || n_shards < 1)
+    return set_error(ctx, PAS_EINVAL, "pas_topk_merge_device: bad shape");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_keys || !d_nodes || !d_out_node || !d_out_len)
+    return set_error(ctx, PAS_EINVAL, "pas_topk_merge_device: null argument");
+  int rc = activate(ctx);
+  if (rc) return rc;
+  return topk_merge_launch(ctx, n_pods, k, n_shards, d_keys, d_nodes, d_out_node, d_out_len,
+                           pick_stream(ctx, hip_stream));
 }
 
 // --------------------------------------------------------------------------- timing

@@ -298,12 +298,14 @@ __device__ __forceinline__ void lds_barrier() {
 // stores, the partial head and tail lines with one dword store each.  Every store is
 // unconditional and range-checked against a buffer descriptor of exactly its part of the
 // run (out-of-range lanes store nothing), so there are no per-lane predicates; a call with
-// no kept entries issues the same 7 stores and writes nothing.
+// no kept entries issues the same 7 stores and writes nothing.  kmax caps the entries
+// stored (top-k lists).
 template <int kAux>
 __device__ __forceinline__ void compact_store(int32_t* stage, uint32_t stage_off,
                                               const int32_t (&node)[kSegWords],
                                               const uint64_t (&keep)[kSegWords],
-                                              int32_t* order_out, int64_t gdst, int lane) {
+                                              int32_t* order_out, int64_t gdst, int lane,
+                                              int32_t kmax = kSegPos) {
   const int32_t a = (int32_t)(gdst & 31);  // stage offset: 128-B line alignment
   int32_t k = a;
 #pragma unroll
@@ -316,6 +318,7 @@ __device__ __forceinline__ void compact_store(int32_t* stage, uint32_t stage_off
     k += __popcll(keep[j]);
   }
   __builtin_amdgcn_wave_barrier();
+  k = min(k, a + kmax);  // top-k: only the first kmax kept entries are stored
   int32_t* const line0 = order_out + (gdst - a);  // 128-B aligned
   const int32_t full_lo = (a + 31) & ~31;         // first entry of the first whole line
   const int32_t full_hi = max(k & ~31, full_lo);  // end of the last whole line
@@ -356,8 +359,10 @@ struct EvalParams {
   const int32_t* perm;   // [3][M][R]
   const int4* desc;      // [2P] from the prep kernel
   uint64_t* pass_out;    // [P][W64]
-  int32_t* order_out;    // [P][N]
+  int32_t* order_out;    // [P][out_stride]
   int32_t* order_len;    // [P]
+  int32_t topk;          // 0: whole HostPriorityList; else its first topk entries
+  int32_t out_stride;    // N, or topk
 };
 
 // One workgroup of kW waves per pod, XCD-aware over the bucketed pod list (blocks b and b+8
@@ -494,7 +499,8 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
       for (int j = 0; j < kSegWords; ++j) none[j] = 0;
 #pragma unroll
       for (int i = 0; i < kS; ++i)
-        compact_store<kAux>(stage, stage_off, node[i], none, P.order_out, (int64_t)pod * N, lane);
+        compact_store<kAux>(stage, stage_off, node[i], none, P.order_out,
+                            (int64_t)pod * P.out_stride, lane);
     }
     for (int32_t r = 0; r < rounds; ++r) {
       uint64_t keep[kS][kSegWords];
@@ -538,11 +544,13 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
       // next round's first use of a segment wait for every store of this round
 #pragma unroll
       for (int i = 0; i < kS; ++i) {
+        const int32_t kmax = P.topk ? max(P.topk - base, 0) : kSegPos;
         if (!(kAblate & 1))
           compact_store<kAux>(stage, stage_off, node[i], keep[i], P.order_out,
-                        (int64_t)pod * N + base, lane);
+                              (int64_t)pod * P.out_stride + base, lane, kmax);
         base += cnt[i];
       }
+      if (P.topk && running >= P.topk) break;  // uniform: every wave has the same running
 #pragma unroll
       for (int i = 0; i < kS; ++i)
 #pragma unroll
@@ -551,12 +559,13 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
   }
 
   // ---- C. FilterResult row, HostPriorityList length ----
-  if (P.flags & PAS_TAS_FILTER) {
+  if ((P.flags & PAS_TAS_FILTER) && P.pass_out) {
     uint64_t* pass_row = P.pass_out + (int64_t)pod * W64;
     for (int32_t w = tid; w < W64; w += T) pass_row[w] = pass64[w];
   }
   // no list: no rule / ReadMetric error -> empty HostPriorityList (telemetryscheduler.go:92-96)
-  if (tid == 0 && (P.flags & PAS_TAS_PRIORITIZE)) P.order_len[pod] = running;
+  if (tid == 0 && (P.flags & PAS_TAS_PRIORITIZE))
+    P.order_len[pod] = P.topk ? min(running, P.topk) : running;
 }
 
 // ---------------------------------------------------------------------------- deschedule
@@ -635,7 +644,7 @@ const TasTuning& tas_tuning() {
 int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
                     uint32_t flags, uint64_t* d_pass, int32_t* d_order, int32_t* d_len,
-                    hipStream_t s) {
+                    int32_t topk, hipStream_t s) {
   const TasSnapshot& t = ctx->tas;
   const int32_t N = t.n_nodes, M = t.n_metrics;
   const int32_t W64 = (int32_t)w64(N);
@@ -704,6 +713,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   ep.pass_out = d_pass;
   ep.order_out = d_order;
   ep.order_len = d_len;
+  ep.topk = topk;
+  ep.out_stride = topk ? topk : N;
   using EvalFn = void (*)(EvalParams);
   EvalFn fn = &tas_eval_kernel<4, 1, 0>;
 #define PAS_EVAL_CASE(W, S, A) \

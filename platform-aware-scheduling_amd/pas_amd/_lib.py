@@ -103,6 +103,15 @@ SIGNATURES = {
         c_int,
         [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
     ),
+    "pas_gas_fit_bitmap_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
+    ),
+    "pas_tas_topk_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_int32, c_int32, _P, _P, _P, _P],
+    ),
+    "pas_topk_merge_device": (c_int, [_P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P]),
     "pas_set_timing": (c_int, [_P, c_int]),
     "pas_kernel_time": (c_int, [_P, c_int32, POINTER(c_double), POINTER(c_int64)]),
     "pas_reset_timing": (c_int, [_P]),

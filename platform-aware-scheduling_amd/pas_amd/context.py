@@ -253,3 +253,30 @@ class Context:
                                         _dptr(req_t), _dptr(mask_t), _dptr(ncont_t),
                                         _dptr(res_t), _stream(stream))
         self._check(rc, "pas_gas_fit_device")
+
+    def gas_fit_bitmap_device(self, gen: int, n_pods: int, max_containers: int, i915_index: int,
+                              req_t, mask_t, ncont_t, fit_t, stream=None):
+        """GAS fit verdicts as node bitmaps fit_t[n_pods][W64] (pas_gas_fit_bitmap_device)."""
+        rc = self._l.pas_gas_fit_bitmap_device(self._h, gen, n_pods, max_containers, i915_index,
+                                               _dptr(req_t), _dptr(mask_t), _dptr(ncont_t),
+                                               _dptr(fit_t), _stream(stream))
+        self._check(rc, "pas_gas_fit_bitmap_device")
+
+    # ------------------------------------------------------------------ node shards
+    def tas_topk_device(self, gen: int, n_pods: int, n_rules: int, rules_t, rule_off_t, prio_t,
+                        cand_t, k: int, node_base: int, key_t, node_t, len_t, stream=None):
+        """First k HostPriorityList entries of this node shard as merge records
+        (pas_tas_topk_device): key_t int64 [P][k], node_t int32 [P][k], len_t int32 [P]."""
+        rc = self._l.pas_tas_topk_device(self._h, gen, n_pods, n_rules, _dptr(rules_t),
+                                         _dptr(rule_off_t), _dptr(prio_t), _dptr(cand_t), k,
+                                         node_base, _dptr(key_t), _dptr(node_t), _dptr(len_t),
+                                         _stream(stream))
+        self._check(rc, "pas_tas_topk_device")
+
+    def topk_merge_device(self, n_pods: int, k: int, n_shards: int, keys_t, nodes_t, out_node_t,
+                          out_len_t, stream=None):
+        """Merge of [n_shards][P][k] records into the global first-k lists."""
+        rc = self._l.pas_topk_merge_device(self._h, n_pods, k, n_shards, _dptr(keys_t),
+                                           _dptr(nodes_t), _dptr(out_node_t), _dptr(out_len_t),
+                                           _stream(stream))
+        self._check(rc, "pas_topk_merge_device")

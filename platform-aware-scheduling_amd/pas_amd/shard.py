@@ -1,0 +1,106 @@
+"""Node-sharded evaluation across the GPUs of one node (BASELINE configs[3-4]).
+
+Every reference computation on the path is per node given the snapshot: the filter verdict
+(dontschedule.Violated, telemetryscheduler.go:184-225), the deschedule violations
+(deschedule/strategy.go:31-50) and the GAS fit (gpuscheduler/scheduler.go:280-338).  Only
+the prioritize order (core.OrderedList, operator.go:30-42) is global.  So each rank holds a
+contiguous node range of the cluster as its resident snapshot and:
+
+  * top-k prioritize: evaluates every pod against its shard, keeps the first k entries of
+    the shard's HostPriorityList as (key, global node) records (pas_tas_topk_device), the
+    records of all ranks are all-gathered over RCCL, and every rank merges them into the
+    exact global first k (pas_topk_merge_device);
+  * deschedule sweep: sweeps its shard's nodes and all-gathers the violation bitmaps
+    (S x W64 words per shard; shard ranges are multiples of 64 nodes so the words of all
+    ranks concatenate into the cluster bitmap).
+
+Collectives are torch.distributed all-gathers: RCCL ("nccl") over xGMI between GPUs; with
+the gloo backend (CPU tests, or several ranks sharing one GPU) the device buffers are staged
+through host memory.
+"""
+from typing import Tuple
+
+import torch
+
+
+def node_range(n_total: int, world: int, rank: int, align: int = 64) -> Tuple[int, int]:
+    """Contiguous node range [n0, n1) of `rank`: shards are multiples of `align` nodes (the
+    bitmap word), the last takes the remainder."""
+    units = (n_total + align - 1) // align
+    per = (units + world - 1) // world
+    n0 = min(n_total, rank * per * align)
+    n1 = min(n_total, (rank + 1) * per * align)
+    return n0, n1
+
+
+def _all_gather(t: torch.Tensor, world: int) -> torch.Tensor:
+    """[world * t.numel()] concatenation of every rank's `t` (same shape on all ranks)."""
+    if world == 1:
+        return t.reshape(-1)
+    import torch.distributed as dist
+    flat = t.contiguous().reshape(-1)
+    if dist.get_backend() == "nccl":
+        out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
+        dist.all_gather_into_tensor(out, flat)
+        return out
+    host = flat.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host)
+    return torch.cat(parts).to(flat.device)
+
+
+class ShardedTopK:
+    """Per-pod global top-k over a node-sharded TAS snapshot (one instance per rank).
+
+    The rank's Context holds the snapshot of nodes [node_base, node_base + n_local);
+    `run` returns (nodes [P][k] int32 global node ids, -1 past len; lens [P] int32), the
+    same on every rank."""
+
+    def __init__(self, ctx, k: int, world: int, rank: int, node_base: int, device="cuda"):
+        self.ctx, self.k, self.world, self.rank = ctx, k, world, rank
+        self.node_base = node_base
+        self.device = device
+        self._bufs = {}
+
+    def _buf(self, name, shape, dtype):
+        b = self._bufs.get(name)
+        if b is None or tuple(b.shape) != tuple(shape):
+            b = torch.empty(shape, dtype=dtype, device=self.device)
+            self._bufs[name] = b
+        return b
+
+    def run(self, gen: int, n_pods: int, n_rules: int, rules_t, rule_off_t, prio_t, cand_t=None,
+            stream=None):
+        k = self.k
+        key = self._buf("key", (n_pods, k), torch.int64)
+        node = self._buf("node", (n_pods, k), torch.int32)
+        ln = self._buf("len", (n_pods,), torch.int32)
+        self.ctx.tas_topk_device(gen, n_pods, n_rules, rules_t, rule_off_t, prio_t, cand_t, k,
+                                 self.node_base, key, node, ln, stream)
+        keys_all = _all_gather(key, self.world)
+        nodes_all = _all_gather(node, self.world)
+        out_node = self._buf("out_node", (n_pods, k), torch.int32)
+        out_len = self._buf("out_len", (n_pods,), torch.int32)
+        self.ctx.topk_merge_device(n_pods, k, self.world, keys_all, nodes_all, out_node, out_len,
+                                   stream)
+        return out_node, out_len
+
+
+def gather_violations(viol_local: torch.Tensor, world: int) -> torch.Tensor:
+    """Cluster violation bitmaps [S][W64_total] from every rank's [S][W64_shard] sweep
+    (shards from node_range: equal word counts except a shorter last shard, which is
+    padded here for the collective and trimmed by the caller's W64_total)."""
+    s, w = viol_local.shape
+    if world == 1:
+        return viol_local
+    import torch.distributed as dist
+    wmax = torch.tensor([w], dtype=torch.int64,
+                        device=viol_local.device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(wmax, op=dist.ReduceOp.MAX)
+    wmax = int(wmax.item())
+    padded = viol_local
+    if w < wmax:
+        padded = torch.zeros((s, wmax), dtype=viol_local.dtype, device=viol_local.device)
+        padded[:, :w] = viol_local
+    parts = _all_gather(padded, world).reshape(world, s, wmax)
+    return parts.permute(1, 0, 2).reshape(s, world * wmax)

@@ -1,0 +1,314 @@
+"""Node-sharded evaluation (pas_amd/shard.py).
+
+A rank holds a contiguous node range of the cluster; per pod it keeps the first k entries
+of its shard's HostPriorityList as (key, global node) records, the records are
+all-gathered and merged.  Parity: the merged lists equal the first k entries of the
+oracle's list over the whole cluster (telemetryscheduler.go:128-149 / operator.go:30-42),
+and gathered shard violation bitmaps equal the cluster sweep (deschedule/strategy.go:31-50).
+CPU tests run the collectives over gloo with the oracle as the per-shard evaluator; GPU
+tests run the HIP top-k and merge kernels.
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from helpers import pack_bits, unpack_bits
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GT, LT = 1, 0
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def shard_snapshot(v, pres, n0, n1):
+    n = v.shape[1]
+    pb = unpack_bits(pres, n)[:, n0:n1]
+    return np.ascontiguousarray(v[:, n0:n1]), pack_bits(pb)
+
+
+def shard_cand(cand, n, n0, n1):
+    if cand is None:
+        return None
+    return pack_bits(unpack_bits(cand, n)[:, n0:n1])
+
+
+def order_keys(v, prio, nodes, p):
+    """Merge keys of global node ids under pod p's prioritize operator (pas.h)."""
+    op = int(prio["op"][p])
+    if op == GT:
+        return np.invert(v[prio["metric"][p], nodes])
+    if op == LT:
+        return v[prio["metric"][p], nodes]
+    return np.zeros(len(nodes), np.int64)
+
+
+def records(oracle, v, pres, rules, off, prio, cand, n0, n1, k):
+    """Per-shard records (keys [P][k], nodes [P][k]) from the oracle's shard lists."""
+    n = v.shape[1]
+    sv, sp = shard_snapshot(v, pres, n0, n1)
+    _, order, lens = oracle.tas_eval(sv, sp, rules, off, prio, shard_cand(cand, n, n0, n1), 3)
+    P = len(prio)
+    keys = np.full((P, k), np.iinfo(np.int64).max, np.int64)
+    nodes = np.full((P, k), np.iinfo(np.int32).max, np.int32)
+    for p in range(P):
+        m = min(k, int(lens[p]))
+        g = order[p, :m].astype(np.int64) + n0
+        nodes[p, :m] = g
+        keys[p, :m] = order_keys(v, prio, g, p)
+    return keys, nodes
+
+
+def merge_records(keys_all, nodes_all, k):
+    """Reference merge: the k smallest (key, node) records per pod."""
+    S, P, _ = keys_all.shape
+    out = []
+    for p in range(P):
+        recs = [(int(keys_all[s, p, j]), int(nodes_all[s, p, j])) for s in range(S)
+                for j in range(k) if nodes_all[s, p, j] != np.iinfo(np.int32).max]
+        out.append([nd for _, nd in sorted(recs)[:k]])
+    return out
+
+
+def make_case(seed, n, m, p, r, cand_frac=None):
+    sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
+    from pas_amd import workload as wl
+    snap = wl.make_tas_snapshot(n, m, seed=seed)
+    batch = wl.make_tas_batch(snap, p, r, seed=seed, cand_frac=cand_frac)
+    rng = np.random.default_rng(seed)
+    # ties and the unsorted branch: some integer-valued entries, some Equals pods
+    batch.prio["op"][rng.random(p) < 0.15] = 2
+    return snap, batch
+
+
+# ------------------------------------------------------------------------------ CPU
+
+
+def test_node_range_partitions():
+    from pas_amd.shard import node_range
+    for n in (0, 1, 63, 64, 65, 1000, 100_003):
+        for world in (1, 2, 3, 8):
+            rs = [node_range(n, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (a0, a1), (b0, b1) in zip(rs, rs[1:]):
+                assert a1 == b0 and (a0 % 64 == 0 or a0 == n)
+            assert all(a0 <= a1 for a0, a1 in rs)
+
+
+def test_merge_of_shard_lists_is_global_list(oracle):
+    """Union-merge of shard top-k equals the global top-k (single process, oracle)."""
+    from pas_amd.shard import node_range
+    snap, batch = make_case(0xC5, 3000, 6, 40, 4, cand_frac=0.85)
+    v, pres = snap.v_milli, snap.present
+    _, order, lens = oracle.tas_eval(v, pres, batch.rules, batch.rule_off, batch.prio,
+                                     batch.cand, 3)
+    for world in (2, 3, 5):
+        for k in (1, 7, 16):
+            recs = [records(oracle, v, pres, batch.rules, batch.rule_off, batch.prio, batch.cand,
+                            *node_range(v.shape[1], world, r), k) for r in range(world)]
+            merged = merge_records(np.stack([a for a, _ in recs]),
+                                   np.stack([b for _, b in recs]), k)
+            for p in range(len(batch.prio)):
+                want = list(order[p, :min(k, int(lens[p]))])
+                assert merged[p] == want, (world, k, p)
+
+
+def _gloo_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    for p in (os.path.join(ROOT, "platform-aware-scheduling_amd"), os.path.join(ROOT, "oracle"),
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import oracle
+    from pas_amd import distrib
+    from pas_amd.shard import _all_gather, gather_violations, node_range
+    from pas_amd import workload as wl
+
+    distrib.setup("gloo")
+    snap, batch = make_case(0xC4, 2500, 5, 12, 3, cand_frac=0.9)
+    v, pres = snap.v_milli, snap.present
+    n = v.shape[1]
+    n0, n1 = node_range(n, world, rank)
+    k = 8
+    keys, nodes = records(oracle, v, pres, batch.rules, batch.rule_off, batch.prio, batch.cand,
+                          n0, n1, k)
+    P = len(batch.prio)
+    keys_all = _all_gather(torch.from_numpy(keys), world).numpy().reshape(world, P, k)
+    nodes_all = _all_gather(torch.from_numpy(nodes), world).numpy().reshape(world, P, k)
+    merged = merge_records(keys_all, nodes_all, k)
+    # deschedule: shard sweeps gathered into the cluster bitmap
+    drules, doff = wl.make_deschedule_rules(snap, 4, 3, seed=0xC4)
+    sv, sp = shard_snapshot(v, pres, n0, n1)
+    viol = oracle.tas_violations(sv, sp, drules, doff)
+    full = gather_violations(torch.from_numpy(viol.view(np.int64)), world).numpy()
+    padded = np.full((P, k), -1, np.int64)
+    for p, lst in enumerate(merged):
+        padded[p, :len(lst)] = lst
+    np.save(os.path.join(out_dir, f"merged{rank}.npy"), padded)
+    np.save(os.path.join(out_dir, f"viol{rank}.npy"), full[:, :(n + 63) // 64])
+    distrib.teardown(world)
+
+
+def test_sharded_records_over_gloo(tmp_path, oracle):
+    world = 2
+    mp.spawn(_gloo_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    snap, batch = make_case(0xC4, 2500, 5, 12, 3, cand_frac=0.9)
+    v, pres = snap.v_milli, snap.present
+    _, order, lens = oracle.tas_eval(v, pres, batch.rules, batch.rule_off, batch.prio,
+                                     batch.cand, 3)
+    sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
+    from pas_amd import workload as wl
+    drules, doff = wl.make_deschedule_rules(snap, 4, 3, seed=0xC4)
+    want_viol = oracle.tas_violations(v, pres, drules, doff)
+    for r in range(world):
+        merged = np.load(tmp_path / f"merged{r}.npy")
+        for p in range(len(batch.prio)):
+            m = min(8, int(lens[p]))
+            np.testing.assert_array_equal(merged[p, :m], order[p, :m])
+            assert (merged[p, m:] == -1).all()
+        viol = np.load(tmp_path / f"viol{r}.npy")
+        np.testing.assert_array_equal(viol.view(np.uint64), want_viol)
+
+
+# ------------------------------------------------------------------------------ GPU
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _rule_tensors(batch, cand):
+    rules_t = _dev(batch.rules.view(np.uint8))
+    off_t = _dev(batch.rule_off)
+    prio_t = _dev(batch.prio.view(np.uint8))
+    cand_t = None if cand is None else _dev(cand.view(np.int64))
+    return rules_t, off_t, prio_t, cand_t
+
+
+def _shard_records_gpu(v, pres, batch, cand, n0, n1, k, gen):
+    import pas_amd
+    n = v.shape[1]
+    sv, sp = shard_snapshot(v, pres, n0, n1)
+    with pas_amd.Context(0) as c:
+        c.tas_snapshot_set(gen, sv, sp)
+        rules_t, off_t, prio_t, cand_t = _rule_tensors(batch, shard_cand(cand, n, n0, n1))
+        P = len(batch.prio)
+        key = torch.empty((P, k), dtype=torch.int64, device="cuda")
+        node = torch.empty((P, k), dtype=torch.int32, device="cuda")
+        ln = torch.empty(P, dtype=torch.int32, device="cuda")
+        c.tas_topk_device(gen, P, len(batch.rules), rules_t, off_t, prio_t, cand_t, k, n0, key,
+                          node, ln)
+        c.synchronize()
+        return key, node, ln
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [1, 5, 16, 300])
+def test_topk_records_match_oracle(oracle, k):
+    from pas_amd.shard import node_range
+    snap, batch = make_case(0x51, 4100, 6, 48, 5, cand_frac=0.9)
+    v, pres = snap.v_milli, snap.present
+    for world, r in ((1, 0), (3, 1), (3, 2)):
+        n0, n1 = node_range(v.shape[1], world, r)
+        key, node, ln = _shard_records_gpu(v, pres, batch, batch.cand, n0, n1, k, 7)
+        want_k, want_n = records(oracle, v, pres, batch.rules, batch.rule_off, batch.prio,
+                                 batch.cand, n0, n1, k)
+        np.testing.assert_array_equal(node.cpu().numpy(), want_n)
+        np.testing.assert_array_equal(key.cpu().numpy(), want_k)
+        np.testing.assert_array_equal(ln.cpu().numpy(),
+                                      (want_n != np.iinfo(np.int32).max).sum(1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,k", [(2, 16), (3, 7), (8, 16), (4, 1)])
+def test_sharded_merge_equals_global_list(ctx, oracle, world, k):
+    """Device records of every shard, merged on device, equal the oracle's global lists."""
+    from pas_amd.shard import node_range
+    snap, batch = make_case(0x52 + world, 5000, 8, 64, 6, cand_frac=0.8)
+    v, pres = snap.v_milli, snap.present
+    recs = [_shard_records_gpu(v, pres, batch, batch.cand, *node_range(v.shape[1], world, r), k,
+                               9) for r in range(world)]
+    keys_all = torch.stack([a for a, _, _ in recs])
+    nodes_all = torch.stack([b for _, b, _ in recs])
+    P = len(batch.prio)
+    out_node = torch.empty((P, k), dtype=torch.int32, device="cuda")
+    out_len = torch.empty(P, dtype=torch.int32, device="cuda")
+    ctx.topk_merge_device(P, k, world, keys_all, nodes_all, out_node, out_len)
+    ctx.synchronize()
+    _, order, lens = oracle.tas_eval(v, pres, batch.rules, batch.rule_off, batch.prio,
+                                     batch.cand, 3)
+    got_n, got_l = out_node.cpu().numpy(), out_len.cpu().numpy()
+    for p in range(P):
+        m = min(k, int(lens[p]))
+        assert got_l[p] == m
+        np.testing.assert_array_equal(got_n[p, :m], order[p, :m])
+        assert (got_n[p, m:] == -1).all()
+
+
+@pytest.mark.gpu
+def test_gas_fit_bitmap_matches_words(ctx):
+    from pas_amd import workload as wl
+    gs = wl.make_gas_snapshot(3000, seed=0xC3)
+    gb = wl.make_gas_batch(70, seed=0xC3)
+    ctx.gas_snapshot_set(31, gs.n_cards, gs.cap, gs.used)
+    words = ctx.gas_fit(31, gb.req, gb.req_mask, gb.n_containers, wl.I915)
+    P, N = words.shape
+    fit_t = torch.full((P, (N + 63) // 64), -1, dtype=torch.int64, device="cuda")
+    ctx.gas_fit_bitmap_device(31, P, gb.req.shape[1], wl.I915, _dev(gb.req),
+                              _dev(gb.req_mask.view(np.int32)), _dev(gb.n_containers), fit_t)
+    ctx.synchronize()
+    got = unpack_bits(fit_t.cpu().numpy().view(np.uint64), N)
+    np.testing.assert_array_equal(got, (words >> 31).astype(bool))
+
+
+def _gpu_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK="0")
+    for p in (os.path.join(ROOT, "platform-aware-scheduling_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import pas_amd
+    from pas_amd import distrib
+    from pas_amd.shard import ShardedTopK, node_range
+
+    distrib.setup("gloo")  # ranks share the box's one GPU: collectives through host memory
+    torch.cuda.set_device(0)
+    snap, batch = make_case(0x53, 6000, 6, 50, 5, cand_frac=0.85)
+    v, pres = snap.v_milli, snap.present
+    n0, n1 = node_range(v.shape[1], world, rank)
+    sv, sp = shard_snapshot(v, pres, n0, n1)
+    with pas_amd.Context(0) as c:
+        c.tas_snapshot_set(3, sv, sp)
+        rules_t, off_t, prio_t, cand_t = _rule_tensors(batch, shard_cand(batch.cand, v.shape[1],
+                                                                         n0, n1))
+        st = ShardedTopK(c, 12, world, rank, n0)
+        out_node, out_len = st.run(3, len(batch.prio), len(batch.rules), rules_t, off_t, prio_t,
+                                   cand_t)
+        c.synchronize()
+        np.save(os.path.join(out_dir, f"nodes{rank}.npy"), out_node.cpu().numpy())
+        np.save(os.path.join(out_dir, f"lens{rank}.npy"), out_len.cpu().numpy())
+    distrib.teardown(world)
+
+
+@pytest.mark.gpu
+def test_sharded_topk_two_ranks_one_gpu(tmp_path, oracle):
+    """ShardedTopK end to end in two processes (gloo between them, one GPU)."""
+    world = 2
+    mp.spawn(_gpu_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    snap, batch = make_case(0x53, 6000, 6, 50, 5, cand_frac=0.85)
+    _, order, lens = oracle.tas_eval(snap.v_milli, snap.present, batch.rules, batch.rule_off,
+                                     batch.prio, batch.cand, 3)
+    for r in range(world):
+        nodes = np.load(tmp_path / f"nodes{r}.npy")
+        ln = np.load(tmp_path / f"lens{r}.npy")
+        for p in range(len(batch.prio)):
+            m = min(12, int(lens[p]))
+            assert ln[p] == m
+            np.testing.assert_array_equal(nodes[p, :m], order[p, :m])
