@@ -8,8 +8,9 @@ per second over the whole job.  With N GPUs every rank evaluates its own 4096-po
 batch against the same (replicated) snapshot — pending pods are independent, so the
 path shards by pod with no data-path collective ("scaling": "weak").
 
-Also: --workload gas (configs[2], 10k pods x 50k nodes x 8 cards) and
---workload deschedule (configs[3] per-GPU sweep, 1M nodes x 64 rules).
+Also: --workload gas (configs[2], 10k pods x 50k nodes x 8 cards), --workload deschedule
+(configs[3]: 1M nodes x 64 rules, node-sharded over the ranks, violations all-gathered) and
+--workload c5 (configs[4]: 64k pods x 1M nodes TAS+GAS, node-sharded, per-pod top-k merge).
 
 Prints ONE JSON line on rank 0.  See DESIGN.md §Measurement for the byte model.
 """
@@ -28,6 +29,7 @@ sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
 import pas_amd  # noqa: E402
 from pas_amd import _lib  # noqa: E402
 from pas_amd import distrib  # noqa: E402
+from pas_amd import shard  # noqa: E402
 from pas_amd.distrib import timed_steps, whole_job_rate  # noqa: E402
 from pas_amd import workload as wl  # noqa: E402
 
@@ -232,20 +234,33 @@ def bench_gas(args, world, rank):
 
 # ------------------------------------------------------------------------ deschedule
 
+def shard_tas(snap, n0, n1):
+    """Columns of nodes [n0, n1) (n0 a multiple of 64, as pas_amd.shard.node_range gives)."""
+    v = np.ascontiguousarray(snap.v_milli[:, n0:n1])
+    pres = np.ascontiguousarray(snap.present[:, n0 // 64:(n1 + 63) // 64])
+    return v, pres
+
+
 def bench_deschedule(args, world, rank):
+    """configs[3]: the sweep over N nodes, node-sharded over the ranks (strong scaling);
+    every rank ends the step with the cluster violation bitmaps (all-gather)."""
     N, M, S = args.nodes, args.metrics, 16
     ctx = pas_amd.Context(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
-    snap = wl.make_tas_snapshot(N, M, seed=0xC4 + rank)
+    snap = wl.make_tas_snapshot(N, M, seed=0xC4)
+    n0, n1 = shard.node_range(N, world, rank)
+    v, pres = shard_tas(snap, n0, n1)
+    n_local = n1 - n0
     rules, off = wl.make_deschedule_rules(snap, S, 4, seed=0xC4)
-    ctx.tas_snapshot_set_device(1, N, M, dev(snap.v_milli), dev(snap.present.view(np.int64)),
-                                stream)
+    ctx.tas_snapshot_set_device(1, n_local, M, dev(v), dev(pres.view(np.int64)), stream)
     rules_t, off_t = dev(rules.view(np.uint8)), dev(off)
-    viol_t = torch.empty((S, pas_amd.w64(N)), dtype=torch.int64, device="cuda")
+    viol_t = torch.empty((S, pas_amd.w64(n_local)), dtype=torch.int64, device="cuda")
+    gathered = {}
 
     def step():
         ctx.tas_violations_device(1, S, len(rules), rules_t, off_t, viol_t, stream)
+        gathered["v"] = shard.gather_violations(viol_t, world)
 
     for _ in range(args.warmup):
         step()
@@ -254,23 +269,84 @@ def bench_deschedule(args, world, rank):
     elapsed = timed_steps(step, args.steps, 0, world)
     ctx.set_timing(0)
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_VIOLATIONS)
-    w = pas_amd.w64(N)
-    alg_bytes = 8 * M * N + 8 * M * w + 8 * S * w
+    w = pas_amd.w64(n_local)
+    alg_bytes = 8 * M * n_local + 8 * M * w + 8 * S * w
     kernel_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = alg_bytes / kernel_s / 1e9
     out = {
-        "metric": "TAS deschedule sweep node-rule evals/sec, 1M nodes×64 rules per GPU",
-        "value": whole_job_rate(N * len(rules), world, args.steps, elapsed),
+        "metric": "TAS deschedule sweep node-rule evals/sec, 1M nodes×64 rules",
+        "value": N * len(rules) * args.steps / elapsed,
         "unit": "node-rule evals/s",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C4)",
-        "config": {"workload": "tas_deschedule_sweep (BASELINE configs[3], node-sharded)",
-                   "nodes_per_gpu": N, "metrics": M, "strategies": S, "rules": len(rules)},
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (SURVEY.md §8(d) C4)",
+        "config": {"workload": "tas_deschedule_sweep (BASELINE configs[3])", "nodes": N,
+                   "nodes_per_gpu": n_local, "metrics": M, "strategies": S, "rules": len(rules),
+                   "parallelism": f"node-sharded x{world}, violation bitmaps all-gathered"},
         "roofline": {"bound": "hbm", "kernel": "tas_violations_kernel", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic("tas_violations_kernel"),
                      "algorithmic_bytes": alg_bytes, "kernel_ms": kernel_s * 1e3},
+    }
+    ctx.close()
+    return out
+
+
+# ------------------------------------------------------------------------------- C5
+
+def bench_c5(args, world, rank):
+    """configs[4]: TAS+GAS over a node-sharded cluster: per rank, the GAS fit bitmaps of its
+    nodes become the TAS candidates, the TAS filter + prioritize keeps each pod's first k
+    nodes of the shard, and the records of all ranks are all-gathered (RCCL) and merged into
+    the cluster's first k per pod (strong scaling: the cluster is fixed)."""
+    P, N, M, R, K = args.pods, args.nodes, args.metrics, args.rules - 1, args.topk
+    ctx = pas_amd.Context(torch.cuda.current_device())
+    stream = torch.cuda.current_stream()
+    ctx.set_stream(stream)
+    n0, n1 = shard.node_range(N, world, rank)
+    n_local = n1 - n0
+    tsnap = wl.make_tas_snapshot(N, M, seed=0xC5)
+    v, pres = shard_tas(tsnap, n0, n1)
+    ctx.tas_snapshot_set_device(1, n_local, M, dev(v), dev(pres.view(np.int64)), stream)
+    tbatch = wl.make_tas_batch(tsnap, P, R, seed=0xC5)
+    del tsnap, v, pres
+    gsnap = wl.make_gas_snapshot(N, seed=0xC5)
+    ctx.gas_snapshot_set_device(2, n_local, gsnap.used.shape[1], gsnap.used.shape[2],
+                                dev(gsnap.n_cards[n0:n1]), dev(gsnap.cap[n0:n1]),
+                                dev(gsnap.used[n0:n1]), stream)
+    gbatch = wl.make_gas_batch(P, seed=0xC5)
+    del gsnap
+    rules_t, off_t = dev(tbatch.rules.view(np.uint8)), dev(tbatch.rule_off)
+    prio_t = dev(tbatch.prio.view(np.uint8))
+    req_t, mask_t = dev(gbatch.req), dev(gbatch.req_mask.view(np.int32))
+    nc_t = dev(gbatch.n_containers)
+    fit_t = torch.empty((P, pas_amd.w64(n_local)), dtype=torch.int64, device="cuda")
+    topk = shard.ShardedTopK(ctx, K, world, rank, n0)
+    result = {}
+
+    def step():
+        ctx.gas_fit_bitmap_device(2, P, gbatch.req.shape[1], wl.I915, req_t, mask_t, nc_t, fit_t,
+                                  stream)
+        result["nodes"], result["len"] = topk.run(1, P, len(tbatch.rules), rules_t, off_t,
+                                                  prio_t, fit_t, stream)
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed_steps(step, args.steps, 0, world)
+    out = {
+        "metric": "combined TAS+GAS pod-node evals/sec, node-sharded, per-pod top-k merge",
+        "value": P * N * args.steps / elapsed,
+        "unit": "pod-node evals/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "int64",
+        "data": "synthetic (SURVEY.md §8(d) C5)",
+        "config": {"workload": "tas_gas_topk_node_sharded (BASELINE configs[4])", "pods": P,
+                   "nodes": N, "nodes_per_gpu": n_local, "metrics": M, "rules_per_pod": R + 1,
+                   "topk": K, "parallelism": f"node-sharded x{world}, top-k records "
+                                             "all-gathered and merged",
+                   "mean_list_len": float(result["len"].float().mean().item())},
     }
     ctx.close()
     return out
@@ -281,20 +357,23 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["tas", "gas", "deschedule"], default="tas")
+    ap.add_argument("--workload", choices=["tas", "gas", "deschedule", "c5"], default="tas")
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--metrics", type=int, default=64)
     ap.add_argument("--rules", type=int, default=16)
+    ap.add_argument("--topk", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
-    defaults = {"tas": (4096, 100_000), "gas": (10_000, 50_000), "deschedule": (0, 1_000_000)}
+    defaults = {"tas": (4096, 100_000), "gas": (10_000, 50_000), "deschedule": (0, 1_000_000),
+                "c5": (65_536, 1_000_000)}
     dp, dn = defaults[args.workload]
     args.pods = args.pods or dp
     args.nodes = args.nodes or dn
     world, rank, _ = distrib.setup()
-    fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule}[args.workload]
+    fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule,
+          "c5": bench_c5}[args.workload]
     out = fn(args, world, rank)
     if rank == 0:
         print(json.dumps(out), flush=True)
