@@ -256,10 +256,18 @@ def bench_deschedule(args, world, rank):
     ctx.tas_snapshot_set_device(1, n_local, M, dev(v), dev(pres.view(np.int64)), stream)
     rules_t, off_t = dev(rules.view(np.uint8)), dev(off)
     viol_t = torch.empty((S, pas_amd.w64(n_local)), dtype=torch.int64, device="cuda")
+    # labels the nodes carry before Enforce (10 % of (node, strategy) pairs), and the per-node
+    # add / remove masks of updateNodeLabels (enforce.go:99-151) for the rank's shard
+    lab = wl.pack_bits(np.random.default_rng(0xC4 + rank).random((S, n_local)) < 0.1)
+    labels_t = dev(lab.view(np.int64))
+    add_t = torch.empty(n_local, dtype=torch.int64, device="cuda")
+    rem_t = torch.empty(n_local, dtype=torch.int64, device="cuda")
+    total_t = torch.empty(1, dtype=torch.int64, device="cuda")
     gathered = {}
 
     def step():
         ctx.tas_violations_device(1, S, len(rules), rules_t, off_t, viol_t, stream)
+        ctx.tas_label_plan_device(n_local, S, viol_t, labels_t, add_t, rem_t, total_t, stream)
         gathered["v"] = shard.gather_violations(viol_t, world)
 
     for _ in range(args.warmup):
@@ -269,6 +277,7 @@ def bench_deschedule(args, world, rank):
     elapsed = timed_steps(step, args.steps, 0, world)
     ctx.set_timing(0)
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_VIOLATIONS)
+    l_ms, l_n = ctx.kernel_time(_lib.PAS_K_TAS_LABELS)
     w = pas_amd.w64(n_local)
     alg_bytes = 8 * M * n_local + 8 * M * w + 8 * S * w
     kernel_s = (k_ms / max(k_n, 1)) / 1e3
@@ -283,7 +292,9 @@ def bench_deschedule(args, world, rank):
         "data": "synthetic (SURVEY.md §8(d) C4)",
         "config": {"workload": "tas_deschedule_sweep (BASELINE configs[3])", "nodes": N,
                    "nodes_per_gpu": n_local, "metrics": M, "strategies": S, "rules": len(rules),
+                   "step": "sweep + label plan (add/remove masks per node) + all-gather",
                    "parallelism": f"node-sharded x{world}, violation bitmaps all-gathered"},
+        "label_plan_ms": l_ms / max(l_n, 1),
         "roofline": {"bound": "hbm", "kernel": "tas_violations_kernel", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic("tas_violations_kernel"),

@@ -163,6 +163,31 @@ int pas_tas_violations_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
                               const int32_t* d_rule_off, uint64_t* d_viol_out,
                               void* hip_stream);
 
+/* Deschedule label plan (Deschedule.updateNodeLabels, deschedule/enforce.go:99-151) for
+ * n_strategies <= 64 strategies from a sweep's viol[s][W64(n_nodes)] and the nodes' labels:
+ *   labels       [s][W64] bit set = the node carries label <policy name of s> (any value);
+ *                NULL = no node carries any
+ *   add_out      [n_nodes] bit s = add "<policy>": "violating" (:108-117)
+ *   remove_out   [n_nodes] bit s = remove the label, then add it as "null" (:118-132)
+ *   total_out    the function's int result: the count of NON-violated (node, strategy)
+ *                pairs (totalViolations++ sits in the non-violated loop, :133)
+ * pas_label_patch_json renders one node's masks as the PATCH body. */
+int pas_tas_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strategies,
+                       const uint64_t* viol, const uint64_t* labels, uint64_t* add_out,
+                       uint64_t* remove_out, int64_t* total_out);
+int pas_tas_label_plan_device(pas_ctx* ctx, int32_t n_nodes, int32_t n_strategies,
+                              const uint64_t* d_viol, const uint64_t* d_labels,
+                              uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
+                              void* hip_stream);
+
+/* json.Marshal of the node's []patchValue (enforce.go:21-25, 74-86) for the masks of
+ * pas_tas_label_plan: adds in strategy order, then a remove + add "null" pair per removed
+ * label in strategy order (the reference emits these in Go-map order).  names[s] = policy
+ * name of strategy s.  Writes at most cap bytes (no terminator); *len = full length;
+ * PAS_ECAPACITY if it exceeds cap.  Host-only. */
+int pas_label_patch_json(int32_t n_strategies, const char* const* names, uint64_t add_mask,
+                         uint64_t remove_mask, char* buf, int64_t cap, int64_t* len);
+
 /* ------------------------------------------------------------------------- */
 /* GPU Aware Scheduling                                                      */
 /* ------------------------------------------------------------------------- */
@@ -263,6 +288,7 @@ int pas_topk_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_sha
 #define PAS_K_GAS_PREP 3       /* per-GPU container requests */
 #define PAS_K_GAS_FIT 4        /* per (pod, node) first fit */
 #define PAS_K_TAS_PREP 5       /* rule ranges + pods bucketed by prioritize order */
+#define PAS_K_TAS_LABELS 6     /* deschedule label plan */
 #define PAS_K_TAS_SPAN 7       /* whole pas_tas_eval path: first launch start to last launch end */
 #define PAS_K_COUNT 8
 #define PAS_TIMING_SPAN 1    /* whole paths: PAS_K_TAS_SPAN, the GAS fit and deschedule launches */

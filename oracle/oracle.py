@@ -54,6 +54,9 @@ def load():
         "or_check_resource_capacity": (c_int, [POINTER(OrRm), POINTER(OrRm), POINTER(OrRm)]),
         "or_gas_fit": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
                                P, P, P, P]),
+        "or_label_plan": (c_int, [c_int32, c_int32, P, P, P, P, P]),
+        "or_label_patch_json": (c_int64, [c_int32, P, ctypes.c_uint64, ctypes.c_uint64,
+                                          ctypes.c_char_p, c_int64]),
     }
     for name, (res, args) in sigs.items():
         fn = getattr(lib, name)
@@ -129,6 +132,31 @@ def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index):
     if rc != 0:
         raise ValueError(f"oracle gas_fit failed: {rc}")
     return out
+
+
+def label_plan(viol, labels, n_nodes):
+    """updateNodeLabels per node: (add masks, remove masks, totalViolations)."""
+    viol = np.ascontiguousarray(viol, np.uint64)
+    s = viol.shape[0]
+    labels = None if labels is None else np.ascontiguousarray(labels, np.uint64)
+    add = np.zeros(n_nodes, np.uint64)
+    rem = np.zeros(n_nodes, np.uint64)
+    total = c_int64(0)
+    rc = load().or_label_plan(n_nodes, s, _p(viol), _p(labels), _p(add), _p(rem),
+                              ctypes.byref(total))
+    if rc != 0:
+        raise ValueError("oracle label_plan: more than 64 strategies")
+    return add, rem, total.value
+
+
+def label_patch_json(names, add, rem) -> bytes:
+    arr = (ctypes.c_char_p * len(names))(*[n.encode() for n in names])
+    buf = ctypes.create_string_buffer(1 << 16)
+    n = load().or_label_patch_json(len(names), ctypes.cast(arr, c_void_p), int(add), int(rem),
+                                   buf, len(buf))
+    if n < 0:
+        raise ValueError("oracle label_patch_json: buffer too small")
+    return buf.raw[:n]
 
 
 def rm(d: dict, keys: list) -> OrRm:

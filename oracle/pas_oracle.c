@@ -9,6 +9,7 @@
 #include "pas_oracle.h"
 
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 
 static inline int has_bit(const uint64_t* bits, int64_t i) {
@@ -199,6 +200,92 @@ int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli
   }
   free(viol);
   return rc;
+}
+
+/* ---- deschedule label payloads ------------------------------------------- */
+
+int or_label_plan(int32_t n_nodes, int32_t n_strat, const uint64_t* viol, const uint64_t* labels,
+                  uint64_t* add, uint64_t* rem, int64_t* total_violations) {
+  if (n_strat < 0 || n_strat > 64) return -1;
+  const int64_t w = w64(n_nodes);
+  int64_t total = 0;
+  for (int32_t n = 0; n < n_nodes; ++n) {          /* for _, node := range allNodes.Items */
+    uint64_t a = 0, r = 0;
+    for (int32_t s = 0; s < n_strat; ++s) {
+      if (has_bit(viol + s * w, n)) {                /* viols[node.Name] (:108-117) */
+        a |= 1ull << s;
+      } else {                                       /* nonViolatedPolicies (:118-134) */
+        if (labels && has_bit(labels + s * w, n)) r |= 1ull << s;
+        ++total;                                     /* totalViolations++ for every one */
+      }
+    }
+    add[n] = a;
+    rem[n] = r;
+  }
+  *total_violations = total;
+  return 0;
+}
+
+/* Go encoding/json string: ", \, control characters, and the HTML-safe <, >, &. */
+static int64_t json_str(const char* s, char* buf, int64_t pos, int64_t cap) {
+  static const char hex[] = "0123456789abcdef";
+  char tmp[8];
+  if (pos < cap) buf[pos] = '"';
+  ++pos;
+  for (const unsigned char* c = (const unsigned char*)s; *c; ++c) {
+    int len = 0;
+    if (*c == '"' || *c == '\\') { tmp[0] = '\\'; tmp[1] = (char)*c; len = 2; }
+    else if (*c == '\n') { tmp[0] = '\\'; tmp[1] = 'n'; len = 2; }
+    else if (*c == '\r') { tmp[0] = '\\'; tmp[1] = 'r'; len = 2; }
+    else if (*c == '\t') { tmp[0] = '\\'; tmp[1] = 't'; len = 2; }
+    else if (*c < 0x20 || *c == '<' || *c == '>' || *c == '&') {
+      tmp[0] = '\\'; tmp[1] = 'u'; tmp[2] = '0'; tmp[3] = '0';
+      tmp[4] = hex[*c >> 4]; tmp[5] = hex[*c & 15]; len = 6;
+    } else { tmp[0] = (char)*c; len = 1; }
+    for (int i = 0; i < len; ++i, ++pos)
+      if (pos < cap) buf[pos] = tmp[i];
+  }
+  if (pos < cap) buf[pos] = '"';
+  return pos + 1;
+}
+
+static int64_t json_lit(const char* s, char* buf, int64_t pos, int64_t cap) {
+  for (; *s; ++s, ++pos)
+    if (pos < cap) buf[pos] = *s;
+  return pos;
+}
+
+static int64_t json_patch(const char* op, const char* name, const char* value, char* buf,
+                          int64_t pos, int64_t cap, int first) {
+  char path[1024];
+  snprintf(path, sizeof path, "/metadata/labels/%s", name);
+  if (!first) pos = json_lit(",", buf, pos, cap);
+  pos = json_lit("{\"op\":", buf, pos, cap);
+  pos = json_str(op, buf, pos, cap);
+  pos = json_lit(",\"path\":", buf, pos, cap);
+  pos = json_str(path, buf, pos, cap);
+  pos = json_lit(",\"value\":", buf, pos, cap);
+  pos = json_str(value, buf, pos, cap);
+  return json_lit("}", buf, pos, cap);
+}
+
+int64_t or_label_patch_json(int32_t n_strat, const char* const* names, uint64_t add, uint64_t rem,
+                            char* buf, int64_t cap) {
+  int64_t pos = json_lit("[", buf, 0, cap);
+  int first = 1;
+  for (int32_t s = 0; s < n_strat; ++s)
+    if (add >> s & 1) {
+      pos = json_patch("add", names[s], "violating", buf, pos, cap, first);
+      first = 0;
+    }
+  for (int32_t s = 0; s < n_strat; ++s)
+    if (rem >> s & 1) {
+      pos = json_patch("remove", names[s], "", buf, pos, cap, first);
+      pos = json_patch("add", names[s], "null", buf, pos, cap, 0);
+      first = 0;
+    }
+  pos = json_lit("]", buf, pos, cap);
+  return pos <= cap ? pos : -1;
 }
 
 /* ---- GAS resourceMap ------------------------------------------------------ */

@@ -64,6 +64,19 @@ int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli
                       const uint64_t* present, int32_t n_strategies, const or_rule* rules,
                       const int32_t* rule_off, uint64_t* viol_out);
 
+/* Deschedule.updateNodeLabels (deschedule/enforce.go:99-151) per node, for S <= 64
+ * registered strategies: add[n] = strategies violated at node n (their label is added as
+ * "violating"), rem[n] = not violated but labelled (label removed, then added as "null").
+ * *total_violations counts, as the reference does, the NON-violated (node, strategy)
+ * pairs (enforce.go:118-134). */
+int or_label_plan(int32_t n_nodes, int32_t n_strat, const uint64_t* viol, const uint64_t* labels,
+                  uint64_t* add, uint64_t* rem, int64_t* total_violations);
+/* json.Marshal of the node's []patchValue (enforce.go:20-24, 76-83): adds in strategy
+ * order, then remove + add-null pairs in strategy order (the reference's order is map
+ * iteration).  Returns the length, or -1 if cap is too small. */
+int64_t or_label_patch_json(int32_t n_strat, const char* const* names, uint64_t add, uint64_t rem,
+                            char* buf, int64_t cap);
+
 /* ---- GAS ---------------------------------------------------------------- */
 
 /* A resourceMap (gpuscheduler/resource_map.go:20) restated over small integer key

@@ -60,7 +60,8 @@ void timing_begin(pas_ctx* ctx, hipStream_t s, int kernel, TimedLaunch* tl) {
   // span-level timing brackets whole paths only: events between the launches of a path
   // would add gaps to the span they measure
   if (!ctx->timing || (ctx->timing == PAS_TIMING_SPAN && kernel != PAS_K_TAS_SPAN &&
-                       kernel != PAS_K_GAS_FIT && kernel != PAS_K_TAS_VIOLATIONS))
+                       kernel != PAS_K_GAS_FIT && kernel != PAS_K_TAS_VIOLATIONS &&
+                       kernel != PAS_K_TAS_LABELS))
     return;
   tl->start = take_event(ctx);
   tl->stop = take_event(ctx);
@@ -271,6 +272,7 @@ void pas_destroy(pas_ctx* ctx) {
   free_gas(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->aux) (void)hipFree(ctx->aux);
+  if (ctx->label_part) (void)hipFree(ctx->label_part);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -700,6 +702,67 @@ int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_
   if ((rc = activate(ctx))) return rc;
   return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
                         d_n_containers, nullptr, d_fit_out, pick_stream(ctx, hip_stream));
+}
+
+// --------------------------------------------------------------------------- deschedule labels
+
+static int check_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const void* viol,
+                            const void* add, const void* rem, const void* total,
+                            const char* fn) {
+  if (n_nodes < 0 || n_strat < 0 || n_strat > 64)
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad shape (0 <= n_strat <= 64)");
+  if (!total || (n_nodes > 0 && (!add || !rem || (n_strat > 0 && !viol))))
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null argument");
+  return PAS_OK;
+}
+
+int pas_tas_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* viol,
+                       const uint64_t* labels, uint64_t* add_out, uint64_t* remove_out,
+                       int64_t* total_out) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_label_plan(ctx, n_nodes, n_strat, viol, add_out, remove_out, total_out,
+                            "pas_tas_label_plan");
+  if (rc) return rc;
+  if ((rc = activate(ctx))) return rc;
+  const size_t W = ((size_t)n_nodes + 63) / 64;
+  const size_t b_bits = sizeof(uint64_t) * (size_t)n_strat * W;
+  const size_t b_mask = sizeof(uint64_t) * (size_t)n_nodes;
+  if ((rc = ensure_scratch(ctx, carve_size({b_bits, b_bits, b_mask, b_mask, sizeof(int64_t)}))))
+    return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  uint64_t* d_viol = cv.take<uint64_t>((size_t)n_strat * W);
+  uint64_t* d_labels = cv.take<uint64_t>((size_t)n_strat * W);
+  uint64_t* d_add = cv.take<uint64_t>(n_nodes);
+  uint64_t* d_rem = cv.take<uint64_t>(n_nodes);
+  int64_t* d_total = cv.take<int64_t>(1);
+  hipStream_t s = ctx->stream;
+  if (b_bits) {
+    PAS_HIP(ctx, hipMemcpyAsync(d_viol, viol, b_bits, hipMemcpyHostToDevice, s));
+    if (labels) PAS_HIP(ctx, hipMemcpyAsync(d_labels, labels, b_bits, hipMemcpyHostToDevice, s));
+  }
+  rc = label_plan_launch(ctx, n_nodes, n_strat, d_viol, labels ? d_labels : nullptr, d_add,
+                         d_rem, d_total, s);
+  if (rc) return rc;
+  if (b_mask) {
+    PAS_HIP(ctx, hipMemcpyAsync(add_out, d_add, b_mask, hipMemcpyDeviceToHost, s));
+    PAS_HIP(ctx, hipMemcpyAsync(remove_out, d_rem, b_mask, hipMemcpyDeviceToHost, s));
+  }
+  PAS_HIP(ctx, hipMemcpyAsync(total_out, d_total, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  return PAS_OK;
+}
+
+int pas_tas_label_plan_device(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat,
+                              const uint64_t* d_viol, const uint64_t* d_labels,
+                              uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
+                              void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_label_plan(ctx, n_nodes, n_strat, d_viol, d_add_out, d_remove_out,
+                            d_total_out, "pas_tas_label_plan_device");
+  if (rc) return rc;
+  if ((rc = activate(ctx))) return rc;
+  return label_plan_launch(ctx, n_nodes, n_strat, d_viol, d_labels, d_add_out, d_remove_out,
+                           d_total_out, pick_stream(ctx, hip_stream));
 }
 
 // --------------------------------------------------------------------------- node shards

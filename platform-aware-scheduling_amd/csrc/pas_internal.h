@@ -92,6 +92,7 @@ struct pas_ctx {
   size_t scratch_bytes = 0;
   void* aux = nullptr;  // per-call device table: TAS rule ranges / GAS container steps
   size_t aux_bytes = 0;
+  int64_t* label_part = nullptr;  // per-workgroup partial counts of the label plan
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;
@@ -141,5 +142,8 @@ int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
 int topk_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
                       const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
                       int32_t* d_out_len, hipStream_t s);
+int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
+                      const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
+                      int64_t* d_total, hipStream_t s);
 
 }  // namespace pas

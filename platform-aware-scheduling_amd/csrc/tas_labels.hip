@@ -1,0 +1,204 @@
+// tas_labels.hip — deschedule label plan: which strategy labels each node's patch adds and
+// removes, from the violation bitmaps of a sweep and the labels the nodes carry.
+//
+// Deschedule.updateNodeLabels (deschedule/enforce.go:99-151) walks every node: for each
+// strategy whose violation list holds the node it adds the strategy's label with value
+// "violating" (:108-117); for every other registered strategy it counts a "violation"
+// (totalViolations++, :118-134 — the reference counts the non-violated pairs) and, when the
+// node carries that label, removes it and re-adds it as "null" (:119-132).  Per node that is
+// two 64-bit masks over <= 64 strategies.  The sweep's output is [S][W64] bitmaps (a word =
+// 64 nodes of one strategy), so the plan is a 64 x S bit transpose per word: one wave per
+// word, lane s loads word w of strategy row s (violations and labels), the S words are
+// broadcast with readlane and each lane (node) collects bit s of each.  HBM-bound byte work:
+// 2 * S * 8 bytes read per 64 nodes, 16 bytes written per node.
+//
+// totalViolations is a count over the whole node list, so the kernel writes one partial
+// count of violated pairs per workgroup and a one-workgroup kernel finishes the sum (device-
+// scope atomics on one address serialise across the 8 XCDs).
+//
+// The JSON body of one node's patch (enforce.go:21-25, 74-86) is host work on the two masks:
+// pas_label_patch_json below.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+
+#include "pas_internal.h"
+
+namespace pas {
+namespace {
+
+constexpr int kTpb = 256;
+constexpr int kWaves = kTpb / 64;
+constexpr int kMaxBlocks = 2048;  // grid-stride beyond; also the partial-count buffer size
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, int s) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, s);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), s);
+  return (uint64_t)hi << 32 | lo;
+}
+
+__global__ __launch_bounds__(kTpb) void label_plan_kernel(int32_t n_nodes, int32_t n_strat,
+                                                          int64_t W,
+                                                          const uint64_t* __restrict__ viol,
+                                                          const uint64_t* __restrict__ labels,
+                                                          uint64_t* __restrict__ add,
+                                                          uint64_t* __restrict__ rem,
+                                                          int64_t* __restrict__ part) {
+  __shared__ int64_t red[kWaves];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t stride = (int64_t)gridDim.x * kWaves;
+  int64_t violated = 0;  // violated pairs of this lane's strategy row
+  for (int64_t w = (int64_t)blockIdx.x * kWaves + wave; w < W; w += stride) {
+    uint64_t vw = 0, lw = 0;
+    if (lane < n_strat) {
+      vw = viol[lane * W + w];
+      if (labels) lw = labels[lane * W + w];
+    }
+    const int64_t valid = min((int64_t)64, (int64_t)n_nodes - w * 64);
+    vw &= valid == 64 ? ~0ull : ((1ull << valid) - 1);
+    violated += __popcll(vw);
+    uint64_t a = 0, r = 0;
+    for (int s = 0; s < n_strat; ++s) a |= ((readlane64(vw, s) >> lane) & 1ull) << s;
+    if (labels)
+      for (int s = 0; s < n_strat; ++s) r |= ((readlane64(lw, s) >> lane) & 1ull) << s;
+    if (lane < valid) {
+      add[w * 64 + lane] = a;
+      rem[w * 64 + lane] = r & ~a;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) violated += __shfl_xor(violated, off, 64);
+  if (lane == 0) red[wave] = violated;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int i = 0; i < kWaves; ++i) t += red[i];
+    part[blockIdx.x] = t;
+  }
+}
+
+// totalViolations = the non-violated pairs = n_nodes * S - violated pairs.
+__global__ __launch_bounds__(kTpb) void label_total_kernel(int32_t n_parts, int64_t pairs,
+                                                           const int64_t* __restrict__ part,
+                                                           int64_t* __restrict__ total) {
+  __shared__ int64_t red[kWaves];
+  int64_t t = 0;
+  for (int i = threadIdx.x; i < n_parts; i += kTpb) t += part[i];
+  for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t v = 0;
+    for (int i = 0; i < kWaves; ++i) v += red[i];
+    *total = pairs - v;
+  }
+}
+
+// Go encoding/json string encoding: '"', '\\', \n \r \t, and other control bytes and the
+// HTML-unsafe <, >, & as \u00XX (json.Marshal escapes HTML by default).
+// Label names are Kubernetes label keys (ASCII), so the UTF-8 rules of the encoder
+// (U+2028/U+2029, invalid sequences) do not arise.
+struct JsonOut {
+  char* buf;
+  int64_t cap;
+  int64_t pos = 0;
+  void put(char c) {
+    if (pos < cap) buf[pos] = c;
+    ++pos;
+  }
+  void lit(const char* s) {
+    for (; *s; ++s) put(*s);
+  }
+  void str(const char* prefix, const char* s) {
+    static const char hex[] = "0123456789abcdef";
+    put('"');
+    for (int part = 0; part < 2; ++part) {
+      for (const unsigned char* c = (const unsigned char*)(part ? s : prefix); *c; ++c) {
+        switch (*c) {
+          case '"': put('\\'); put('"'); break;
+          case '\\': put('\\'); put('\\'); break;
+          case '\n': put('\\'); put('n'); break;
+          case '\r': put('\\'); put('r'); break;
+          case '\t': put('\\'); put('t'); break;
+          default:
+            if (*c < 0x20 || *c == '<' || *c == '>' || *c == '&') {
+              lit("\\u00");
+              put(hex[*c >> 4]);
+              put(hex[*c & 15]);
+            } else {
+              put((char)*c);
+            }
+        }
+      }
+    }
+    put('"');
+  }
+  // {"op":<op>,"path":"/metadata/labels/<name>","value":<value>} (patchValue, enforce.go:21-25)
+  void patch(const char* op, const char* name, const char* value) {
+    lit("{\"op\":");
+    str("", op);
+    lit(",\"path\":");
+    str("/metadata/labels/", name);
+    lit(",\"value\":");
+    str("", value);
+    put('}');
+  }
+};
+
+}  // namespace
+
+int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
+                      const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
+                      int64_t* d_total, hipStream_t s) {
+  if (!ctx->label_part)
+    PAS_HIP(ctx, hipMalloc(&ctx->label_part, sizeof(int64_t) * kMaxBlocks));
+  const int64_t W = ((int64_t)n_nodes + 63) / 64;
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((W + kWaves - 1) / kWaves,
+                                                                   kMaxBlocks));
+  TimedLaunch tl;
+  timing_begin(ctx, s, PAS_K_TAS_LABELS, &tl);
+  label_plan_kernel<<<blocks, kTpb, 0, s>>>(n_nodes, n_strat, W, d_viol, d_labels, d_add, d_rem,
+                                            ctx->label_part);
+  label_total_kernel<<<1, kTpb, 0, s>>>(blocks, (int64_t)n_nodes * n_strat, ctx->label_part,
+                                        d_total);
+  timing_end(ctx, s, &tl);
+  PAS_HIP(ctx, hipGetLastError());
+  return PAS_OK;
+}
+
+}  // namespace pas
+
+// json.Marshal([]patchValue) of one node's label patch: the adds in strategy order, then a
+// remove + add-"null" pair per removed label in strategy order (the reference iterates a
+// Go map there, whose order is unspecified; the set of operations is the same).
+extern "C" int pas_label_patch_json(int32_t n_strat, const char* const* names, uint64_t add_mask,
+                                    uint64_t remove_mask, char* buf, int64_t cap, int64_t* len) {
+  if (n_strat < 0 || n_strat > 64 || !names || !len || cap < 0 || (cap > 0 && !buf))
+    return PAS_EINVAL;
+  const uint64_t live = n_strat == 64 ? ~0ull : ((1ull << n_strat) - 1);
+  if ((add_mask | remove_mask) & ~live) return PAS_EINVAL;
+  for (int32_t s = 0; s < n_strat; ++s)
+    if (((add_mask | remove_mask) >> s & 1) && !names[s]) return PAS_EINVAL;
+  pas::JsonOut o{buf, cap};
+  o.put('[');
+  bool first = true;
+  for (int32_t s = 0; s < n_strat; ++s)
+    if (add_mask >> s & 1) {
+      if (!first) o.put(',');
+      o.patch("add", names[s], "violating");
+      first = false;
+    }
+  for (int32_t s = 0; s < n_strat; ++s)
+    if (remove_mask >> s & 1) {
+      if (!first) o.put(',');
+      o.patch("remove", names[s], "");
+      o.put(',');
+      o.patch("add", names[s], "null");
+      first = false;
+    }
+  o.put(']');
+  *len = o.pos;
+  return o.pos <= cap ? PAS_OK : PAS_ECAPACITY;
+}

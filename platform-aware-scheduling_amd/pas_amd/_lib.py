@@ -50,8 +50,10 @@ PAS_K_TAS_VIOLATIONS = 2
 PAS_K_GAS_PREP = 3
 PAS_K_GAS_FIT = 4
 PAS_K_TAS_PREP = 5
+PAS_K_TAS_LABELS = 6
 PAS_K_TAS_SPAN = 7
 KERNEL_NAMES = {
+    PAS_K_TAS_LABELS: "label_plan_kernel",
     PAS_K_TAS_EVAL: "tas_eval_kernel",
     PAS_K_TAS_VIOLATIONS: "tas_violations_kernel",
     PAS_K_GAS_PREP: "gas_prep_kernel",
@@ -93,6 +95,12 @@ SIGNATURES = {
     ),
     "pas_tas_violations": (c_int, [_P, c_uint64, c_int32, _P, _P, _P]),
     "pas_tas_violations_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P]),
+    "pas_tas_label_plan": (c_int, [_P, c_int32, c_int32, _P, _P, _P, _P, _P]),
+    "pas_tas_label_plan_device": (c_int, [_P, c_int32, c_int32, _P, _P, _P, _P, _P, _P]),
+    "pas_label_patch_json": (
+        c_int,
+        [c_int32, POINTER(c_char_p), c_uint64, c_uint64, c_char_p, c_int64, POINTER(c_int64)],
+    ),
     "pas_gas_snapshot_set": (c_int, [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P]),
     "pas_gas_snapshot_set_device": (
         c_int,

@@ -77,6 +77,22 @@ def quantity_as_int64(q: str) -> int:
     return out.value
 
 
+def label_patch_json(names, add_mask: int, remove_mask: int) -> bytes:
+    """JSON PATCH body of one node's label update (deschedule/enforce.go:74-86, 104-135)."""
+    l = _lib.load()
+    arr = (ctypes.c_char_p * max(len(names), 1))(*[n.encode() for n in names])
+    n = c_int64()
+    cap = 256
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        rc = l.pas_label_patch_json(len(names), arr, add_mask, remove_mask, buf, cap, byref(n))
+        if rc == _lib.PAS_OK:
+            return buf.raw[:n.value]
+        if rc != _lib.PAS_ECAPACITY:
+            raise PasError(rc, "pas_label_patch_json")
+        cap = n.value
+
+
 class Context:
     """One pas_ctx bound to a HIP device."""
 
@@ -212,6 +228,30 @@ class Context:
                                                _dptr(rule_off_t), _dptr(viol_t),
                                                _stream(stream))
         self._check(rc, "pas_tas_violations_device")
+
+    def tas_label_plan(self, n_nodes: int, viol: np.ndarray, labels: Optional[np.ndarray] = None):
+        """(add [n_nodes] u64, remove [n_nodes] u64, total) of updateNodeLabels
+        (deschedule/enforce.go:99-151) from viol[S][W64] and labels[S][W64] (or None)."""
+        viol = np.ascontiguousarray(viol, dtype=np.uint64)
+        s = viol.shape[0]
+        if labels is not None:
+            labels = np.ascontiguousarray(labels, dtype=np.uint64)
+            assert labels.shape == viol.shape, "labels must have the shape of viol"
+        add = np.zeros(n_nodes, np.uint64)
+        rem = np.zeros(n_nodes, np.uint64)
+        total = c_int64()
+        rc = self._l.pas_tas_label_plan(self._h, n_nodes, s, _ptr(viol) if viol.size else None,
+                                        _ptr(labels) if labels is not None and labels.size
+                                        else None, _ptr(add), _ptr(rem), byref(total))
+        self._check(rc, "pas_tas_label_plan")
+        return add, rem, total.value
+
+    def tas_label_plan_device(self, n_nodes: int, n_strat: int, viol_t, labels_t, add_t, rem_t,
+                              total_t, stream=None):
+        rc = self._l.pas_tas_label_plan_device(self._h, n_nodes, n_strat, _dptr(viol_t),
+                                               _dptr(labels_t), _dptr(add_t), _dptr(rem_t),
+                                               _dptr(total_t), _stream(stream))
+        self._check(rc, "pas_tas_label_plan_device")
 
     # ------------------------------------------------------------------ GAS
     def gas_snapshot_set(self, gen: int, n_cards: np.ndarray, cap_per_gpu: np.ndarray,

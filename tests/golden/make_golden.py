@@ -57,11 +57,22 @@ V["G4_deschedule_enforce"] = {
     "metrics": {"memory": {"node-1": 100}},
     "nodes": ["node-1"],
     "policy": "deschedule-test",
+    # "labels": node-1's labels before Enforce (enforce_test.go:40, :46); "want" = nodes
+    # listed by deschedule-test=violating afterwards (:68-84).  The label plan and patch body
+    # are derived (the test does not inspect them): updateNodeLabels (enforce.go:99-151) and
+    # json.Marshal of patchValue (enforce.go:21-25, 74-86).
     "cases": [
-        {"name": "node label test",
-         "rules": [["memory", "GreaterThan", 1], ["cpu", "LessThan", 10]], "want": ["node-1"]},
-        {"name": "node unlabel test",
-         "rules": [["memory", "GreaterThan", 1000], ["cpu", "LessThan", 10]], "want": []},
+        {"name": "node label test", "labels": {"deschedule-test": ""},
+         "rules": [["memory", "GreaterThan", 1], ["cpu", "LessThan", 10]], "want": ["node-1"],
+         "derived": {"add": ["deschedule-test"], "remove": [], "total": 0,
+                     "patch": '[{"op":"add","path":"/metadata/labels/deschedule-test",'
+                              '"value":"violating"}]'}},
+        {"name": "node unlabel test", "labels": {"deschedule-test": "violating"},
+         "rules": [["memory", "GreaterThan", 1000], ["cpu", "LessThan", 10]], "want": [],
+         "derived": {"add": [], "remove": ["deschedule-test"], "total": 1,
+                     "patch": '[{"op":"remove","path":"/metadata/labels/deschedule-test",'
+                              '"value":""},{"op":"add","path":"/metadata/labels/'
+                              'deschedule-test","value":"null"}]'}},
     ],
 }
 

@@ -1,0 +1,161 @@
+"""Deschedule label plan and patch body (Deschedule.updateNodeLabels / patchNode,
+deschedule/enforce.go:74-151).  The JSON encoder is host code in libpas.so and runs on CPU;
+the plan kernel is checked on the GPU, bit-exact against the oracle, end to end from the
+sweep (pas_tas_violations) through the plan to the patched labels."""
+import json
+
+import numpy as np
+import pytest
+
+import pas_amd
+from pas_amd import workload as wl
+from helpers import golden, unpack_bits
+from test_oracle_golden import apply_label_patch
+
+G = golden()
+
+
+def random_names(rng, s):
+    alphabet = list("abcdefghij-.") + ["<", ">", "&", '"', "\\", "\n", "\t", "\x01", "/"]
+    return ["p%d-" % i + "".join(rng.choice(alphabet, size=rng.integers(0, 12))) for i in range(s)]
+
+
+# ---------------------------------------------------------------- host JSON (CPU)
+
+def test_patch_json_matches_oracle(oracle):
+    rng = np.random.default_rng(11)
+    for s in (0, 1, 2, 7, 63, 64):
+        names = random_names(rng, s)
+        live = (1 << s) - 1
+        for _ in range(20):
+            add = int(rng.integers(0, 1 << 62, dtype=np.int64)) & live
+            rem = int(rng.integers(0, 1 << 62, dtype=np.int64)) & live & ~add
+            got = pas_amd.label_patch_json(names, add, rem)
+            assert got == oracle.label_patch_json(names, add, rem)
+            ops = json.loads(got)  # valid JSON whose strings decode to the names
+            n_add = bin(add).count("1")
+            assert len(ops) == n_add + 2 * bin(rem).count("1")
+            want = [("add", names[i], "violating") for i in range(s) if add >> i & 1]
+            for i in range(s):
+                if rem >> i & 1:
+                    want += [("remove", names[i], ""), ("add", names[i], "null")]
+            assert [(o["op"], o["path"][len("/metadata/labels/"):], o["value"]) for o in ops] \
+                == want
+
+
+def test_patch_json_go_encoding():
+    # encoding/json escapes <, >, & and control bytes as \u00XX (HTML-safe by default)
+    got = pas_amd.label_patch_json(["a<b>&c\x1f"], 1, 0)
+    assert got == (b'[{"op":"add","path":"/metadata/labels/a\\u003cb\\u003e\\u0026c\\u001f",'
+                   b'"value":"violating"}]')
+    assert pas_amd.label_patch_json(["x"], 0, 0) == b"[]"  # payload := []patchValue{}
+
+
+def test_patch_json_capacity_and_errors():
+    lib = pas_amd.LIB
+    import ctypes
+    names = (ctypes.c_char_p * 2)(b"alpha", b"beta")
+    n = ctypes.c_int64()
+    buf = ctypes.create_string_buffer(8)
+    assert lib.pas_label_patch_json(2, names, 3, 0, buf, 8, ctypes.byref(n)) == \
+        pas_amd._lib.PAS_ECAPACITY
+    full = n.value
+    buf = ctypes.create_string_buffer(full)
+    assert lib.pas_label_patch_json(2, names, 3, 0, buf, full, ctypes.byref(n)) == 0
+    assert n.value == full and json.loads(buf.raw)[1]["path"] == "/metadata/labels/beta"
+    # mask bits past n_strategies, n_strategies > 64
+    assert lib.pas_label_patch_json(2, names, 4, 0, buf, full, ctypes.byref(n)) == \
+        pas_amd._lib.PAS_EINVAL
+    assert lib.pas_label_patch_json(65, names, 0, 0, buf, full, ctypes.byref(n)) == \
+        pas_amd._lib.PAS_EINVAL
+
+
+# ---------------------------------------------------------------- plan kernel (GPU)
+
+def _plan_case(rng, n, s, density=0.3):
+    w = (n + 63) // 64
+    if n == 0 or s == 0:
+        return np.zeros((s, w), np.uint64), np.zeros((s, w), np.uint64)
+    viol = wl.pack_bits(rng.random((s, n)) < density)
+    labels = wl.pack_bits(rng.random((s, n)) < 0.5)
+    assert viol.shape == (s, w)
+    return viol, labels
+
+
+@pytest.mark.gpu
+def test_label_plan_parity(ctx, oracle):
+    rng = np.random.default_rng(12)
+    for n in (0, 1, 63, 64, 65, 1000, 4097):
+        for s in (0, 1, 5, 64):
+            viol, labels = _plan_case(rng, n, s)
+            for lab in (labels, None):
+                got = ctx.tas_label_plan(n, viol, lab)
+                want = oracle.label_plan(viol, lab, n)
+                np.testing.assert_array_equal(got[0], want[0], err_msg=f"add n={n} s={s}")
+                np.testing.assert_array_equal(got[1], want[1], err_msg=f"rem n={n} s={s}")
+                assert got[2] == want[2], (n, s)
+
+
+@pytest.mark.gpu
+def test_label_plan_golden_g4(ctx, oracle):
+    # the reference's own Enforce test (enforce_test.go:38-52): sweep on the GPU, plan on
+    # the GPU, patch body from libpas.so, applied to node-1's labels
+    from helpers import NamedSnapshot
+    g = G["G4_deschedule_enforce"]
+    snap = NamedSnapshot(g["metrics"], g["nodes"])
+    policy = g["policy"]
+    for gen, c in enumerate(g["cases"], start=7000):
+        ctx.tas_snapshot_set(gen, snap.v_milli, snap.present)
+        rules = snap.rules(c["rules"])
+        viol = ctx.tas_violations(gen, rules, np.array([0, len(rules)], np.int32))
+        labels = np.zeros_like(viol)
+        if policy in c["labels"]:
+            labels[0, 0] = 1
+        add, rem, total = ctx.tas_label_plan(len(g["nodes"]), viol, labels)
+        assert total == c["derived"]["total"], c["name"]
+        body = pas_amd.label_patch_json([policy], int(add[0]), int(rem[0]))
+        assert body.decode() == c["derived"]["patch"], c["name"]
+        after = apply_label_patch(c["labels"], body)
+        assert [n for n in g["nodes"] if after.get(policy) == "violating"] == c["want"]
+
+
+@pytest.mark.gpu
+def test_label_plan_device_after_sweep(ctx, oracle):
+    # device chain at configs[3] shape (1M nodes x 16 strategies): sweep -> plan, resident
+    import torch
+    n, s = 1_000_000, 16
+    snap = wl.make_tas_snapshot(n, 64, seed=0xC4)
+    rules, off = wl.make_deschedule_rules(snap, s, 4, seed=0xC4)
+    gen = 7100
+    ctx.tas_snapshot_set(gen, snap.v_milli, snap.present)
+    dev = torch.device("cuda", 0)
+    rules_t = torch.from_numpy(rules.view(np.uint8).copy()).to(dev)
+    off_t = torch.from_numpy(off).to(dev)
+    w = (n + 63) // 64
+    viol_t = torch.empty((s, w), dtype=torch.int64, device=dev)
+    ctx.tas_violations_device(gen, s, len(rules), rules_t, off_t, viol_t)
+    rng = np.random.default_rng(13)
+    labels = wl.pack_bits(rng.random((s, n)) < 0.1)
+    labels_t = torch.from_numpy(labels.view(np.int64)).to(dev)
+    add_t = torch.empty(n, dtype=torch.int64, device=dev)
+    rem_t = torch.empty(n, dtype=torch.int64, device=dev)
+    total_t = torch.empty(1, dtype=torch.int64, device=dev)
+    ctx.tas_label_plan_device(n, s, viol_t, labels_t, add_t, rem_t, total_t)
+    torch.cuda.synchronize()
+    viol = viol_t.cpu().numpy().view(np.uint64)
+    want = oracle.label_plan(viol, labels, n)
+    np.testing.assert_array_equal(add_t.cpu().numpy().view(np.uint64), want[0])
+    np.testing.assert_array_equal(rem_t.cpu().numpy().view(np.uint64), want[1])
+    assert int(total_t.item()) == want[2]
+    # size-independent properties: add is the column of the sweep; add & remove disjoint;
+    # total = n * s - violated pairs
+    a = add_t.cpu().numpy().view(np.uint64)
+    assert not np.any(a & rem_t.cpu().numpy().view(np.uint64))
+    assert want[2] == n * s - int(unpack_bits(viol, n).sum())
+
+
+@pytest.mark.gpu
+def test_label_plan_errors(ctx):
+    with pytest.raises(pas_amd.PasError) as e:
+        ctx.tas_label_plan(10, np.zeros((65, 1), np.uint64))
+    assert e.value.code == pas_amd._lib.PAS_EINVAL

@@ -62,11 +62,47 @@ def test_g3_violated(oracle):
         assert _violated(oracle, snap, c["rules"]) == sorted(c["want"]), c["name"]
 
 
+def apply_label_patch(labels: dict, body: bytes) -> dict:
+    """JSON PATCH (RFC 6902) add/remove on /metadata/labels/<key>, as the API server applies
+    the body of Deschedule.patchNode (enforce.go:74-86)."""
+    import json
+    out = dict(labels)
+    for op in json.loads(body):
+        prefix = "/metadata/labels/"
+        assert op["path"].startswith(prefix)
+        key = op["path"][len(prefix):]
+        if op["op"] == "remove":
+            assert key in out, "remove of a missing label fails the whole patch"
+            del out[key]
+        else:
+            assert op["op"] == "add"
+            out[key] = op["value"]
+    return out
+
+
 def test_g4_deschedule_enforce(oracle):
     g = G["G4_deschedule_enforce"]
     snap = NamedSnapshot(g["metrics"], g["nodes"])
+    policy = g["policy"]
     for c in g["cases"]:
         assert _violated(oracle, snap, c["rules"]) == sorted(c["want"]), c["name"]
+        rules = snap.rules(c["rules"])
+        viol = oracle.tas_violations(snap.v_milli, snap.present, rules,
+                                     np.array([0, len(rules)], np.int32))
+        labels = np.zeros_like(viol)
+        for i, node in enumerate(g["nodes"]):
+            if policy in c["labels"]:  # every node of this fixture carries c["labels"]
+                labels[0, i >> 6] |= np.uint64(1 << (i & 63))
+        add, rem, total = oracle.label_plan(viol, labels, len(g["nodes"]))
+        d = c["derived"]
+        assert [policy] * int(add[0]) == d["add"] and [policy] * int(rem[0]) == d["remove"]
+        assert total == d["total"], c["name"]
+        body = oracle.label_patch_json([policy], add[0], rem[0])
+        assert body.decode() == d["patch"], c["name"]
+        # the reference's assertion: nodes listed by <policy>=violating after the patch
+        after = apply_label_patch(c["labels"], body)
+        got = [n for n in g["nodes"] if after.get(policy) == "violating"]
+        assert got == c["want"], c["name"]
 
 
 def _filter(oracle, snap, named_rules, nodes):
