@@ -20,6 +20,7 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles")
 TAS_PATH = ("tas_prep_kernel", "tas_eval_kernel")
+GAS_PATH = ("gas_prep_kernel", "gas_fit_single_kernel", "gas_fit_multi_kernel")
 
 
 def short(name):
@@ -86,9 +87,13 @@ def main():
             traffic["tas_path"] = round(sum(hbm(k) for k in TAS_PATH))
             traffic["tas_path_by_kernel"] = {k: round(hbm(k)) for k in TAS_PATH}
         elif w == "gas":
-            traffic["gas_fit_kernel"] = round(hbm("gas_fit_kernel") + hbm("gas_prep_kernel"))
+            traffic["gas_fit_kernel"] = round(sum(hbm(k) for k in GAS_PATH))
+            traffic["gas_fit_by_kernel"] = {k: round(hbm(k)) for k in GAS_PATH}
         elif w == "deschedule":
             traffic["tas_violations_kernel"] = round(hbm("tas_violations_kernel"))
+            traffic["label_plan_kernel"] = round(hbm("label_plan_kernel"))
+        elif w == "c5":
+            traffic["c5_by_kernel"] = {k: round(hbm(k)) for k in kernels}
         print(w, "->", [r["kernel"] + f" {r['avg_us']:.1f}us x{r['calls']}" for r in rows[:8]])
     traffic["_source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, round {rnd}; "
                           "bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB->B)")
