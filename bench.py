@@ -53,6 +53,28 @@ def load_traffic(name):
 
 # ------------------------------------------------------------------------------- TAS
 
+def snapshot_refresh_ms(ctx, N, M, v_t, p_t, stream, gen=1):
+    """Wall time of a full re-upload of the resident snapshot (buffers already allocated)
+    and of one- and eight-column refreshes (AutoUpdatingCache.updateMetric).  The contents
+    are re-uploaded unchanged and the snapshot ends at generation `gen`."""
+    out = {}
+    eight = list(range(0, M, max(M // 8, 1)))[:8]
+    cases = [("full", None, None, None), ("1_column", [0], v_t[:1], p_t[:1]),
+             ("8_columns", eight, v_t[eight].contiguous(), p_t[eight].contiguous())]
+    for name, cols, cv, cp in cases:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if cols is None:
+            ctx.tas_snapshot_set_device(gen + 1, N, M, v_t, p_t, stream)
+        else:
+            ctx.tas_snapshot_update_device(gen, gen + 1, cols, cv, cp, stream)
+        torch.cuda.synchronize()
+        out[name] = (time.perf_counter() - t0) * 1e3
+        ctx.tas_snapshot_update_device(gen + 1, gen, [], None, None, stream)
+    torch.cuda.synchronize()
+    return out
+
+
 def bench_tas(args, world, rank):
     P, N, M, R = args.pods, args.nodes, args.metrics, args.rules - 1
     ctx = pas_amd.Context(torch.cuda.current_device())
@@ -66,6 +88,7 @@ def bench_tas(args, world, rank):
     ctx.tas_snapshot_set_device(1, N, M, v_t, p_t, stream)
     torch.cuda.synchronize()
     snapshot_ms = (time.perf_counter() - t0) * 1e3
+    refresh = snapshot_refresh_ms(ctx, N, M, v_t, p_t, stream)
     rules_t = dev(batch.rules.view(np.uint8))
     off_t = dev(batch.rule_off)
     prio_t = dev(batch.prio.view(np.uint8))
@@ -126,7 +149,7 @@ def bench_tas(args, world, rank):
             "pods_per_gpu": P, "nodes": N, "metrics": M, "rules_per_pod": R + 1,
             "parallelism": f"pod-sharded x{world} (independent batches, replicated snapshot)",
             "prioritize_entries_per_step": sum_len * world,
-            "snapshot_build_ms": snapshot_ms,
+            "snapshot_build_ms": snapshot_ms, "snapshot_refresh_ms": refresh,
             "kernel_ms_per_step": kern,
             "launches_per_step": launches,
         },
@@ -253,7 +276,14 @@ def bench_deschedule(args, world, rank):
     v, pres = shard_tas(snap, n0, n1)
     n_local = n1 - n0
     rules, off = wl.make_deschedule_rules(snap, S, 4, seed=0xC4)
-    ctx.tas_snapshot_set_device(1, n_local, M, dev(v), dev(pres.view(np.int64)), stream)
+    v_t, p_t = dev(v), dev(pres.view(np.int64))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ctx.tas_snapshot_set_device(1, n_local, M, v_t, p_t, stream)
+    torch.cuda.synchronize()
+    snapshot_ms = (time.perf_counter() - t0) * 1e3
+    refresh = snapshot_refresh_ms(ctx, n_local, M, v_t, p_t, stream)
+    del v_t, p_t
     rules_t, off_t = dev(rules.view(np.uint8)), dev(off)
     viol_t = torch.empty((S, pas_amd.w64(n_local)), dtype=torch.int64, device="cuda")
     # labels the nodes carry before Enforce (10 % of (node, strategy) pairs), and the per-node
@@ -293,6 +323,7 @@ def bench_deschedule(args, world, rank):
         "config": {"workload": "tas_deschedule_sweep (BASELINE configs[3])", "nodes": N,
                    "nodes_per_gpu": n_local, "metrics": M, "strategies": S, "rules": len(rules),
                    "step": "sweep + label plan (add/remove masks per node) + all-gather",
+                   "snapshot_build_ms": snapshot_ms, "snapshot_refresh_ms": refresh,
                    "parallelism": f"node-sharded x{world}, violation bitmaps all-gathered"},
         "label_plan_ms": l_ms / max(l_n, 1),
         "roofline": {"bound": "hbm", "kernel": "tas_violations_kernel", "achieved": achieved,

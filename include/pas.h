@@ -116,6 +116,20 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
                           int32_t* n_metrics);
 
+/* Column refresh: AutoUpdatingCache.updateMetric replaces one metric's whole node map
+ * (cache/autoupdating.go:45-73, WriteMetric :100-112).  Replaces the resident snapshot's
+ * columns cols[0 .. n_cols) (distinct metric indices, host array) with
+ * v_milli[n_cols][n_nodes] / present[n_cols][W64] and rebuilds only their orders; the
+ * snapshot moves from generation gen_from (PAS_ESTALE otherwise) to gen_to.  Node count and
+ * metric count are unchanged (a new node or metric column needs pas_tas_snapshot_set).
+ * The _device form is asynchronous on hip_stream except for the copy of cols. */
+int pas_tas_snapshot_update(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_cols,
+                            const int32_t* cols, const int64_t* v_milli,
+                            const uint64_t* present);
+int pas_tas_snapshot_update_device(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to,
+                                   int32_t n_cols, const int32_t* cols, const int64_t* d_v_milli,
+                                   const uint64_t* d_present, void* hip_stream);
+
 #define PAS_TAS_FILTER 1u      /* produce pass_out (MetricsExtender.filterNodes) */
 #define PAS_TAS_PRIORITIZE 2u  /* produce order_out/order_len (prioritizeNodesForRule) */
 

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "pas.h"
 #include "pas_internal.h"
@@ -104,10 +105,13 @@ void free_tas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(t.perm));
   free_ptr(reinterpret_cast<void*&>(t.f1k));
   free_ptr(reinterpret_cast<void*&>(t.f32));
-  free_ptr(reinterpret_cast<void*&>(t.vals_c));
+  free_ptr(t.keys_a);
+  free_ptr(t.keys_b);
+  free_ptr(reinterpret_cast<void*&>(t.ids_a));
+  free_ptr(reinterpret_cast<void*&>(t.ids_b));
+  free_ptr(reinterpret_cast<void*&>(t.popc));
   free_ptr(reinterpret_cast<void*&>(t.word_scan));
-  free_ptr(reinterpret_cast<void*&>(t.seg_begin));
-  free_ptr(reinterpret_cast<void*&>(t.seg_end));
+  free_ptr(reinterpret_cast<void*&>(t.rows));
   free_ptr(t.sort_tmp);
   free_ptr(t.scan_tmp);
   t = TasSnapshot{};
@@ -347,6 +351,61 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
   if (rc) return rc;
   return tas_snapshot_build(ctx, gen, n_nodes, n_metrics, d_v_milli, d_present,
                             pick_stream(ctx, hip_stream));
+}
+
+static int check_update(pas_ctx* ctx, uint64_t gen_from, int32_t n_cols, const int32_t* cols,
+                        const void* vals, const void* present, const char* fn) {
+  if (!ctx->tas.valid) return set_error(ctx, PAS_ENOSNAP, std::string(fn) + ": no TAS snapshot");
+  if (ctx->tas.gen != gen_from)
+    return set_error(ctx, PAS_ESTALE, std::string(fn) + ": resident generation " +
+                                          std::to_string(ctx->tas.gen) + ", update from " +
+                                          std::to_string(gen_from));
+  const int32_t M = ctx->tas.n_metrics;
+  if (n_cols < 0 || n_cols > M)
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad column count");
+  if (n_cols > 0 && (!cols || (ctx->tas.n_nodes > 0 && (!vals || !present))))
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
+  std::vector<char> seen((size_t)M, 0);
+  for (int32_t c = 0; c < n_cols; ++c) {
+    if (cols[c] < 0 || cols[c] >= M || seen[(size_t)cols[c]]++)
+      return set_error(ctx, PAS_EINVAL,
+                       std::string(fn) + ": columns must be distinct metric indices < n_metrics");
+  }
+  return PAS_OK;
+}
+
+int pas_tas_snapshot_update(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_cols,
+                            const int32_t* cols, const int64_t* v_milli,
+                            const uint64_t* present) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_update(ctx, gen_from, n_cols, cols, v_milli, present, "pas_tas_snapshot_update");
+  if (rc) return rc;
+  if ((rc = activate(ctx))) return rc;
+  const int32_t N = ctx->tas.n_nodes;
+  const size_t vb = sizeof(int64_t) * (size_t)n_cols * N;
+  const size_t pb = sizeof(uint64_t) * (size_t)n_cols * w64(N);
+  if ((rc = ensure_scratch(ctx, carve_size({vb, pb})))) return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  int64_t* d_v = cv.take<int64_t>((size_t)n_cols * N);
+  uint64_t* d_p = cv.take<uint64_t>((size_t)n_cols * w64(N));
+  hipStream_t s = ctx->stream;
+  if (vb) PAS_HIP(ctx, hipMemcpyAsync(d_v, v_milli, vb, hipMemcpyHostToDevice, s));
+  if (pb) PAS_HIP(ctx, hipMemcpyAsync(d_p, present, pb, hipMemcpyHostToDevice, s));
+  if ((rc = tas_snapshot_update(ctx, gen_to, n_cols, cols, d_v, d_p, s))) return rc;
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  return PAS_OK;
+}
+
+int pas_tas_snapshot_update_device(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to,
+                                   int32_t n_cols, const int32_t* cols, const int64_t* d_v_milli,
+                                   const uint64_t* d_present, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_update(ctx, gen_from, n_cols, cols, d_v_milli, d_present,
+                        "pas_tas_snapshot_update_device");
+  if (rc) return rc;
+  if ((rc = activate(ctx))) return rc;
+  return tas_snapshot_update(ctx, gen_to, n_cols, cols, d_v_milli, d_present,
+                             pick_stream(ctx, hip_stream));
 }
 
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,

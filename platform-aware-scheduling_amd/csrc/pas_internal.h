@@ -47,11 +47,15 @@ struct TasSnapshot {
   int32_t* perm = nullptr;
   int64_t* f1k = nullptr;  // [M][R / 1024] sorted[m][1024 a]: fences of the range search
   int64_t* f32 = nullptr;  // [M][R / 32]   sorted[m][32 b]
-  // build scratch
-  int64_t* vals_c = nullptr;       // [M][R] compacted values in index order
+  // build scratch (kept for column updates): sort keys {value, row} and node ids, two
+  // buffers each, [M][R]; per-word popcounts and their scan; the updated rows
+  void* keys_a = nullptr;
+  void* keys_b = nullptr;
+  int32_t* ids_a = nullptr;
+  int32_t* ids_b = nullptr;
+  uint32_t* popc = nullptr;        // [M*W64 + 1]
   uint32_t* word_scan = nullptr;   // [M*W64 + 1]
-  int32_t* seg_begin = nullptr;    // [M]
-  int32_t* seg_end = nullptr;      // [M]
+  int32_t* rows = nullptr;         // [M]
   void* sort_tmp = nullptr;
   size_t sort_tmp_bytes = 0;
   void* scan_tmp = nullptr;
@@ -125,6 +129,10 @@ void free_gas(pas_ctx* ctx);
 // Per-translation-unit entry points used by the C-ABI layer.
 int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t n_metrics,
                        const int64_t* d_vals, const uint64_t* d_present, hipStream_t s);
+// Replace metric columns cols[0..n_cols) (host array, distinct, < n_metrics) with
+// d_vals [n_cols][N] / d_present [n_cols][W64] and rebuild their orders.
+int tas_snapshot_update(pas_ctx* ctx, uint64_t gen, int32_t n_cols, const int32_t* cols,
+                        const int64_t* d_vals, const uint64_t* d_present, hipStream_t s);
 int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
                     uint32_t flags, uint64_t* d_pass, int32_t* d_order, int32_t* d_len,

@@ -174,6 +174,23 @@ class Context:
                     "pas_tas_snapshot_set_device")
         self.n_nodes, self.n_metrics = n_nodes, n_metrics
 
+    def tas_snapshot_update(self, gen_from: int, gen_to: int, cols, v_milli: np.ndarray,
+                            present: np.ndarray):
+        """Replace metric columns `cols` (AutoUpdatingCache.updateMetric) and re-sort them."""
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        v = np.ascontiguousarray(v_milli, dtype=np.int64).reshape(len(cols), self.n_nodes)
+        p = np.ascontiguousarray(present, dtype=np.uint64).reshape(len(cols), w64(self.n_nodes))
+        self._check(self._l.pas_tas_snapshot_update(
+            self._h, gen_from, gen_to, len(cols), _ptr(cols) if cols.size else None,
+            _ptr(v) if v.size else None, _ptr(p) if p.size else None), "pas_tas_snapshot_update")
+
+    def tas_snapshot_update_device(self, gen_from: int, gen_to: int, cols, v_t, p_t,
+                                   stream=None):
+        cols = np.ascontiguousarray(cols, dtype=np.int32)
+        self._check(self._l.pas_tas_snapshot_update_device(
+            self._h, gen_from, gen_to, len(cols), _ptr(cols) if cols.size else None, _dptr(v_t),
+            _dptr(p_t), _stream(stream)), "pas_tas_snapshot_update_device")
+
     def tas_snapshot_info(self):
         g = c_uint64()
         n = c_int32()
