@@ -263,6 +263,41 @@ int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_
                               const uint32_t* d_req_mask, const int32_t* d_n_containers,
                               uint64_t* d_fit_out, void* hip_stream);
 
+/* Bind-time commit (GASExtender.bindNode, scheduler.go:385-445): for binds b in call order,
+ * pod bind_pod[b] (an index into the req / req_mask / n_containers batch, as pas_gas_fit)
+ * onto node bind_node[b]: runSchedulingLogic on the node's CURRENT resident usage, then
+ * Cache.adjustPodResources(add) with the resulting annotation (node_resource_cache.go:
+ * 240-287), applied to the resident used[N][K][Q] in place.  Binds to the same node see
+ * each other in call order.  res_out[b] = the pas_gas_fit word for that (pod, node) at bind
+ * time, status_out[b] = PAS_GAS_OK or PAS_GAS_WONT_FIT (then nothing changes).  The
+ * snapshot moves from generation gen_from (PAS_ESTALE otherwise) to gen_to. */
+#define PAS_GAS_OK 0
+#define PAS_GAS_WONT_FIT 1
+#define PAS_GAS_ERR_INPUT 2    /* resource_map.go errInput: nothing changes */
+#define PAS_GAS_ERR_OVERFLOW 3 /* resource_map.go errOverflow: nothing changes */
+int pas_gas_bind(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
+                 const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
+                 int32_t max_containers, int32_t i915_index, const int64_t* req,
+                 const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
+                 int32_t* status_out);
+
+/* Pods leaving nodes: Cache.adjustPodResources(remove) (node_resource_cache.go:240-287) with
+ * each pod's annotation, in call order.  Container c of release r has cards_per_container
+ * [r][c] cards (its "gas-container-cards" segment), listed in container order in
+ * cards[r][8] as ranks into the node's cards; request / count is subtracted from each card
+ * (subtractRM, resource_map.go:55-73,103-127: clamp at 0; a negative amount, or a card the
+ * node's label does not list, is an input error and nothing changes).  The snapshot keeps
+ * no "key absent" state: a label card has every kind, so subtracting from a kind that was
+ * never added clamps at 0 where the reference reports errInput. */
+int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
+                    const int32_t* rel_pod, const int32_t* rel_node, int32_t n_pods,
+                    int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
+                    const int32_t* n_containers, const int32_t* cards_per_container,
+                    const int32_t* cards, int32_t* status_out);
+
+/* Read back the resident usage used[N][K][Q] and its generation. */
+int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out);
+
 /* ------------------------------------------------------------------------- */
 /* Node-sharded snapshots                                  */
 /* ------------------------------------------------------------------------- */

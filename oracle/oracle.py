@@ -54,6 +54,10 @@ def load():
         "or_check_resource_capacity": (c_int, [POINTER(OrRm), POINTER(OrRm), POINTER(OrRm)]),
         "or_gas_fit": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
                                P, P, P, P]),
+        "or_gas_bind": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, P, P, c_int32,
+                                c_int32, P, P, P, P, P]),
+        "or_gas_release": (c_int, [c_int32, c_int32, c_int32, P, P, c_int32, P, P, c_int32,
+                                   P, P, P, P, P, P]),
         "or_label_plan": (c_int, [c_int32, c_int32, P, P, P, P, P]),
         "or_label_patch_json": (c_int64, [c_int32, P, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_char_p, c_int64]),
@@ -132,6 +136,54 @@ def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index):
     if rc != 0:
         raise ValueError(f"oracle gas_fit failed: {rc}")
     return out
+
+
+def gas_bind(n_cards, cap, used, req, req_mask, n_containers, i915_index, pods, nodes):
+    """Binds in order (bindNode: runSchedulingLogic + adjustPodResources(add)).
+    Returns (used after, result words, statuses)."""
+    n_cards = np.ascontiguousarray(n_cards, np.int32)
+    cap = np.ascontiguousarray(cap, np.int64)
+    used = np.array(used, np.int64, copy=True, order="C")
+    req = np.ascontiguousarray(req, np.int64)
+    req_mask = np.ascontiguousarray(req_mask, np.uint32)
+    n_containers = np.ascontiguousarray(n_containers, np.int32)
+    pods = np.ascontiguousarray(pods, np.int32)
+    nodes = np.ascontiguousarray(nodes, np.int32)
+    n, k, q = used.shape
+    c = req.shape[1]
+    b = len(pods)
+    res = np.zeros(b, np.uint32)
+    st = np.zeros(b, np.int32)
+    rc = load().or_gas_bind(n, k, q, _p(n_cards), _p(cap), _p(used), b, _p(pods), _p(nodes), c,
+                            i915_index, _p(req), _p(req_mask), _p(n_containers), _p(res),
+                            _p(st))
+    if rc != 0:
+        raise ValueError(f"oracle gas_bind failed: {rc}")
+    return used, res, st
+
+
+def gas_release(n_cards, used, req, req_mask, n_containers, pods, nodes, cards_per_container,
+                cards):
+    """Pods leaving nodes (adjustPodResources(remove)).  Returns (used after, statuses)."""
+    n_cards = np.ascontiguousarray(n_cards, np.int32)
+    used = np.array(used, np.int64, copy=True, order="C")
+    req = np.ascontiguousarray(req, np.int64)
+    req_mask = np.ascontiguousarray(req_mask, np.uint32)
+    n_containers = np.ascontiguousarray(n_containers, np.int32)
+    pods = np.ascontiguousarray(pods, np.int32)
+    nodes = np.ascontiguousarray(nodes, np.int32)
+    cpc = np.ascontiguousarray(cards_per_container, np.int32)
+    cards = np.ascontiguousarray(cards, np.int32)
+    n, k, q = used.shape
+    c = req.shape[1]
+    r = len(pods)
+    st = np.zeros(r, np.int32)
+    rc = load().or_gas_release(n, k, q, _p(n_cards), _p(used), r, _p(pods), _p(nodes), c,
+                               _p(req), _p(req_mask), _p(n_containers), _p(cpc), _p(cards),
+                               _p(st))
+    if rc != 0:
+        raise ValueError(f"oracle gas_release failed: {rc}")
+    return used, st
 
 
 def label_plan(viol, labels, n_nodes):

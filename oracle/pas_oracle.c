@@ -428,3 +428,110 @@ int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t*
   }
   return 0;
 }
+
+/* ---- GAS bind-time commit ------------------------------------------------- */
+
+/* The node's usage as resourceMaps (every kind of a labelled card is a key). */
+static void node_maps(int32_t max_cards, int32_t n_res, int32_t ncard, const int64_t* u,
+                      or_rm* out) {
+  for (int32_t k = 0; k < max_cards; ++k) {
+    memset(&out[k], 0, sizeof(or_rm));
+    if (k >= ncard) continue;
+    for (int32_t q = 0; q < n_res; ++q) {
+      out[k].has[q] = 1;
+      out[k].val[q] = u[(int64_t)k * n_res + q];
+    }
+  }
+}
+
+static void container_map(int32_t n_res, const int64_t* req, uint32_t mask, or_rm* out) {
+  memset(out, 0, sizeof(or_rm));                    /* containerRequests (utils.go:14-32) */
+  for (int32_t q = 0; q < n_res; ++q)
+    if (mask & (1u << q)) { out->has[q] = 1; out->val[q] = req[q]; }
+}
+
+int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+                const int64_t* cap_per_gpu, int64_t* used, int32_t n_binds,
+                const int32_t* bind_pod, const int32_t* bind_node, int32_t max_containers,
+                int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                const int32_t* n_containers, uint32_t* res_out, int32_t* status) {
+  if (max_cards > 8 || n_res > OR_RM_MAX_KEYS) return -1;
+  for (int32_t b = 0; b < n_binds; ++b) {
+    const int32_t p = bind_pod[b], n = bind_node[b];
+    if (n < 0 || n >= n_nodes) return -1;
+    int64_t* u = used + (int64_t)n * max_cards * n_res;
+    uint32_t word = 0;
+    /* runSchedulingLogic(pod, node) on the current usage */
+    if (or_gas_fit(1, max_cards, n_res, n_cards + n, cap_per_gpu + (int64_t)n * n_res, u, 1,
+                   max_containers, i915_index, req + (int64_t)p * max_containers * n_res,
+                   req_mask + (int64_t)p * max_containers, n_containers + p, &word) != 0)
+      return -2;
+    res_out[b] = word;
+    if (!(word >> 31)) { status[b] = OR_GAS_WONT_FIT; continue; }
+    /* adjustPodResources(add): the annotation lists, per container, the cards of its
+     * selections (numCards = numI915); checked on a copy, then applied */
+    or_rm maps[8];
+    node_maps(max_cards, n_res, n_cards[n], u, maps);
+    int32_t sel = 0, err = OR_RM_OK;
+    for (int32_t c = 0; c < n_containers[p] && !err; ++c) {
+      const int64_t base = (int64_t)p * max_containers + c;
+      or_rm r;
+      container_map(n_res, req + base * n_res, req_mask[base], &r);
+      int64_t k_c = 0;
+      if (req_mask[base] && i915_index >= 0 && r.has[i915_index] && r.val[i915_index] > 0)
+        k_c = r.val[i915_index];
+      if (k_c <= 0) continue;                       /* empty segment: skipped */
+      or_rm_divide(&r, (int32_t)k_c);
+      for (int64_t g = 0; g < k_c && !err; ++g, ++sel)
+        err = or_rm_add_rm(&maps[(word >> (3 * sel)) & 7], &r);
+    }
+    if (err) {                                       /* nothing changes */
+      status[b] = err == OR_RM_ERR_OVERFLOW ? OR_GAS_ERR_OVERFLOW : OR_GAS_ERR_INPUT;
+      continue;
+    }
+    for (int32_t k = 0; k < n_cards[n]; ++k)
+      for (int32_t q = 0; q < n_res; ++q) u[(int64_t)k * n_res + q] = maps[k].val[q];
+    status[b] = OR_GAS_OK;
+  }
+  return 0;
+}
+
+int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+                   int64_t* used, int32_t n_rel, const int32_t* rel_pod,
+                   const int32_t* rel_node, int32_t max_containers, const int64_t* req,
+                   const uint32_t* req_mask, const int32_t* n_containers,
+                   const int32_t* cards_per_container, const int32_t* cards, int32_t* status) {
+  if (max_cards > 8 || n_res > OR_RM_MAX_KEYS) return -1;
+  for (int32_t r = 0; r < n_rel; ++r) {
+    const int32_t p = rel_pod[r], n = rel_node[r];
+    if (n < 0 || n >= n_nodes) return -1;
+    int64_t* u = used + (int64_t)n * max_cards * n_res;
+    const int32_t ncard = n_cards[n] > 0 ? n_cards[n] : 0;
+    or_rm maps[8], stale;
+    node_maps(max_cards, n_res, ncard, u, maps);
+    int32_t off = 0, err = OR_RM_OK;
+    for (int32_t c = 0; c < n_containers[p] && !err; ++c) {
+      const int64_t base = (int64_t)p * max_containers + c;
+      const int32_t k_c = cards_per_container[(int64_t)r * max_containers + c];
+      if (k_c <= 0) continue;                        /* empty segment */
+      or_rm q;
+      container_map(n_res, req + base * n_res, req_mask[base], &q);
+      or_rm_divide(&q, k_c);
+      for (int32_t j = 0; j < k_c && !err; ++j) {
+        const int32_t k = cards[(int64_t)r * 8 + off + j];
+        if (k >= 0 && k < ncard) {
+          err = or_rm_subtract_rm(&maps[k], &q);
+        } else {                                     /* new empty map for the card */
+          memset(&stale, 0, sizeof stale);
+          err = or_rm_subtract_rm(&stale, &q);
+        }
+      }
+      off += k_c;
+    }
+    if (err) { status[r] = OR_GAS_ERR_INPUT; continue; }
+    for (int32_t k = 0; k < ncard; ++k)
+      for (int32_t q = 0; q < n_res; ++q) u[(int64_t)k * n_res + q] = maps[k].val[q];
+    status[r] = OR_GAS_OK;
+  }
+  return 0;
+}

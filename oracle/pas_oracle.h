@@ -104,6 +104,30 @@ int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t*
                int32_t max_containers, int32_t i915_index, const int64_t* req,
                const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out);
 
+/* GASExtender.bindNode (scheduler.go:385-445) for binds b = 0 .. n_binds-1 in order: pod
+ * bind_pod[b] onto node bind_node[b] — runSchedulingLogic on the node's current usage
+ * (:280-338), then Cache.adjustPodResources(add) with the resulting annotation
+ * (node_resource_cache.go:240-287: per container, request / numCards added to each of its
+ * cards, all or nothing).  used is updated in place.  res_out[b] = the packed result word
+ * (as or_gas_fit; 0 when it does not fit), status[b] = OR_GAS_* below. */
+enum { OR_GAS_OK = 0, OR_GAS_WONT_FIT = 1, OR_GAS_ERR_INPUT = 2, OR_GAS_ERR_OVERFLOW = 3 };
+int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+                const int64_t* cap_per_gpu, int64_t* used, int32_t n_binds,
+                const int32_t* bind_pod, const int32_t* bind_node, int32_t max_containers,
+                int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                const int32_t* n_containers, uint32_t* res_out, int32_t* status);
+/* Cache.adjustPodResources(remove) (node_resource_cache.go:240-287) for pods leaving nodes,
+ * in order: container c's cards are cards[r][off .. off + n_cc[r][c]) (off = sum of the
+ * earlier containers' counts; ranks into the node's cards); its request / n_cc is
+ * subtracted from each (subtractRM: clamp at 0; a negative amount or a key the card does
+ * not have -> input error, nothing changes).  A card rank outside the node's cards is a
+ * card without usage keys. */
+int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+                   int64_t* used, int32_t n_rel, const int32_t* rel_pod,
+                   const int32_t* rel_node, int32_t max_containers, const int64_t* req,
+                   const uint32_t* req_mask, const int32_t* n_containers,
+                   const int32_t* cards_per_container, const int32_t* cards, int32_t* status);
+
 #ifdef __cplusplus
 }
 #endif

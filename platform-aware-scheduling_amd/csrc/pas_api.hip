@@ -674,6 +674,149 @@ static int check_gas_gen(pas_ctx* ctx, uint64_t gen) {
   return PAS_OK;
 }
 
+// Shared host path of pas_gas_bind / pas_gas_release: validates, groups the operations by
+// node (stable), uploads everything in one scratch carve and runs the commit kernel.
+static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t gen_to,
+                      int32_t n_ops, const int32_t* op_pod, const int32_t* op_node,
+                      int32_t n_pods, int32_t max_containers, int32_t i915_index,
+                      const int64_t* req, const uint32_t* req_mask, const int32_t* n_containers,
+                      const int32_t* cpc, const int32_t* cards, uint32_t* res_out,
+                      int32_t* status_out, const char* fn) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_gas_gen(ctx, gen_from);
+  if (rc) return rc;
+  const GasSnapshot& g = ctx->gas;
+  const int32_t Q = g.n_res, N = g.n_nodes;
+  if (n_ops < 0 || n_pods < 0 || max_containers < 0 || i915_index >= Q || i915_index < -1)
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad shape");
+  if (n_ops > 0 && (!op_pod || !op_node || !status_out || !n_containers ||
+                    (max_containers > 0 && (!req || !req_mask)) ||
+                    (release ? (!cpc || !cards) : !res_out)))
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
+  std::vector<int32_t> order((size_t)n_ops);
+  for (int32_t i = 0; i < n_ops; ++i) {
+    order[(size_t)i] = i;
+    if (op_node[i] < 0 || op_node[i] >= N || op_pod[i] < 0 || op_pod[i] >= n_pods)
+      return set_error(ctx, PAS_EINVAL, std::string(fn) + ": node or pod index out of range");
+    const int32_t p = op_pod[i];
+    if (n_containers[p] < 0 || n_containers[p] > max_containers)
+      return set_error(ctx, PAS_EINVAL, std::string(fn) + ": n_containers out of range");
+    int64_t sel = 0;
+    for (int32_t c = 0; c < n_containers[p]; ++c) {
+      const int64_t b = (int64_t)p * max_containers + c;
+      if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
+      if (release) {
+        const int32_t k = cpc[(int64_t)i * max_containers + c];
+        if (k < 0) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": negative card count");
+        sel += k;
+      } else if (i915_index >= 0 && req_mask[b] && (req_mask[b] >> i915_index & 1u)) {
+        const int64_t v = req[b * Q + i915_index];
+        if (v > 0) sel += v;
+      }
+    }
+    if (sel > PAS_GAS_MAX_SELECTIONS)
+      return set_error(ctx, release ? PAS_EINVAL : PAS_ECAPACITY,
+                       std::string(fn) + ": more than 8 cards for one pod");
+  }
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int32_t a, int32_t b) { return op_node[a] < op_node[b]; });
+  std::vector<int32_t> seg_off;
+  for (int32_t i = 0; i < n_ops; ++i)
+    if (i == 0 || op_node[order[(size_t)i]] != op_node[order[(size_t)i - 1]])
+      seg_off.push_back(i);
+  const int32_t n_seg = (int32_t)seg_off.size();
+  seg_off.push_back(n_ops);
+  if ((rc = activate(ctx))) return rc;
+  const size_t C = (size_t)std::max(max_containers, 1);
+  const size_t ops = (size_t)std::max(n_ops, 1);
+  const size_t pods = (size_t)std::max(n_pods, 1);
+  const size_t b_req = sizeof(int64_t) * pods * C * Q, b_mask = sizeof(uint32_t) * pods * C;
+  const size_t b_nc = sizeof(int32_t) * pods, b_op = sizeof(int32_t) * ops;
+  const size_t b_seg = sizeof(int32_t) * (size_t)(n_seg + 1);
+  const size_t b_cpc = sizeof(int32_t) * ops * C, b_cards = sizeof(int32_t) * ops * 8;
+  if ((rc = ensure_scratch(ctx, carve_size({b_req, b_mask, b_nc, b_op, b_op, b_op, b_seg, b_cpc,
+                                            b_cards, b_op, b_op}))))
+    return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  int64_t* d_req = cv.take<int64_t>(pods * C * Q);
+  uint32_t* d_mask = cv.take<uint32_t>(pods * C);
+  int32_t* d_nc = cv.take<int32_t>(pods);
+  int32_t* d_pod = cv.take<int32_t>(ops);
+  int32_t* d_node = cv.take<int32_t>(ops);
+  int32_t* d_order = cv.take<int32_t>(ops);
+  int32_t* d_seg = cv.take<int32_t>((size_t)n_seg + 1);
+  int32_t* d_cpc = cv.take<int32_t>(ops * C);
+  int32_t* d_cards = cv.take<int32_t>(ops * 8);
+  uint32_t* d_res = cv.take<uint32_t>(ops);
+  int32_t* d_status = cv.take<int32_t>(ops);
+  hipStream_t s = ctx->stream;
+  if (n_ops > 0) {
+    if (max_containers > 0 && n_pods > 0) {
+      PAS_HIP(ctx, hipMemcpyAsync(d_req, req, sizeof(int64_t) * n_pods * max_containers * Q,
+                                  hipMemcpyHostToDevice, s));
+      PAS_HIP(ctx, hipMemcpyAsync(d_mask, req_mask, sizeof(uint32_t) * n_pods * max_containers,
+                                  hipMemcpyHostToDevice, s));
+    }
+    PAS_HIP(ctx, hipMemcpyAsync(d_nc, n_containers, sizeof(int32_t) * n_pods,
+                                hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(d_pod, op_pod, b_op, hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(d_node, op_node, b_op, hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(d_order, order.data(), b_op, hipMemcpyHostToDevice, s));
+    PAS_HIP(ctx, hipMemcpyAsync(d_seg, seg_off.data(), b_seg, hipMemcpyHostToDevice, s));
+    if (release) {
+      if (max_containers > 0)
+        PAS_HIP(ctx, hipMemcpyAsync(d_cpc, cpc, sizeof(int32_t) * n_ops * max_containers,
+                                    hipMemcpyHostToDevice, s));
+      PAS_HIP(ctx, hipMemcpyAsync(d_cards, cards, sizeof(int32_t) * n_ops * 8,
+                                  hipMemcpyHostToDevice, s));
+    }
+    if ((rc = gas_commit_launch(ctx, release, n_seg, max_containers, i915_index, d_order, d_seg,
+                                d_pod, d_node, d_req, d_mask, d_nc, d_cpc, d_cards, d_res,
+                                d_status, s)))
+      return rc;
+    if (!release)
+      PAS_HIP(ctx, hipMemcpyAsync(res_out, d_res, b_op, hipMemcpyDeviceToHost, s));
+    PAS_HIP(ctx, hipMemcpyAsync(status_out, d_status, b_op, hipMemcpyDeviceToHost, s));
+  }
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  ctx->gas.gen = gen_to;
+  return PAS_OK;
+}
+
+int pas_gas_bind(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
+                 const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
+                 int32_t max_containers, int32_t i915_index, const int64_t* req,
+                 const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
+                 int32_t* status_out) {
+  return gas_commit(ctx, false, gen_from, gen_to, n_binds, bind_pod, bind_node, n_pods,
+                    max_containers, i915_index, req, req_mask, n_containers, nullptr, nullptr,
+                    res_out, status_out, "pas_gas_bind");
+}
+
+int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
+                    const int32_t* rel_pod, const int32_t* rel_node, int32_t n_pods,
+                    int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
+                    const int32_t* n_containers, const int32_t* cards_per_container,
+                    const int32_t* cards, int32_t* status_out) {
+  return gas_commit(ctx, true, gen_from, gen_to, n_releases, rel_pod, rel_node, n_pods,
+                    max_containers, -1, req, req_mask, n_containers, cards_per_container, cards,
+                    nullptr, status_out, "pas_gas_release");
+}
+
+int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out) {
+  if (!ctx) return PAS_EINVAL;
+  if (!ctx->gas.valid) return set_error(ctx, PAS_ENOSNAP, "no GAS snapshot uploaded");
+  const GasSnapshot& g = ctx->gas;
+  const size_t b = sizeof(int64_t) * (size_t)g.n_nodes * g.max_cards * g.n_res;
+  if (b && !used_out) return set_error(ctx, PAS_EINVAL, "pas_gas_snapshot_get: null output");
+  int rc = activate(ctx);
+  if (rc) return rc;
+  if (b) PAS_HIP(ctx, hipMemcpyAsync(used_out, g.used, b, hipMemcpyDeviceToHost, ctx->stream));
+  PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (gen) *gen = g.gen;
+  return PAS_OK;
+}
+
 int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out) {

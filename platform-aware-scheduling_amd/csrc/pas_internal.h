@@ -150,6 +150,14 @@ int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
 int topk_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
                       const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
                       int32_t* d_out_len, hipStream_t s);
+// Bind (fit + commit, release = false) or release of operations grouped by node: order =
+// operation indices sorted by node (stable), seg_off [n_seg + 1] the node segments.
+int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_containers,
+                      int32_t i915_index, const int32_t* d_order, const int32_t* d_seg_off,
+                      const int32_t* d_pod, const int32_t* d_node, const int64_t* d_req,
+                      const uint32_t* d_mask, const int32_t* d_ncont, const int32_t* d_cpc,
+                      const int32_t* d_cards, uint32_t* d_res, int32_t* d_status,
+                      hipStream_t s);
 int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
                       const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                       int64_t* d_total, hipStream_t s);

@@ -45,6 +45,11 @@ PAS_GAS_MAX_CARDS = 8
 PAS_GAS_MAX_RES = 4
 PAS_GAS_MAX_SELECTIONS = 8
 
+PAS_GAS_OK = 0
+PAS_GAS_WONT_FIT = 1
+PAS_GAS_ERR_INPUT = 2
+PAS_GAS_ERR_OVERFLOW = 3
+
 PAS_K_TAS_EVAL = 1
 PAS_K_TAS_VIOLATIONS = 2
 PAS_K_GAS_PREP = 3
@@ -118,6 +123,15 @@ SIGNATURES = {
         c_int,
         [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
     ),
+    "pas_gas_bind": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
+    ),
+    "pas_gas_release": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, _P, _P, _P, _P, _P, _P],
+    ),
+    "pas_gas_snapshot_get": (c_int, [_P, POINTER(c_uint64), _P]),
     "pas_tas_topk_device": (
         c_int,
         [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_int32, c_int32, _P, _P, _P, _P],

@@ -304,6 +304,52 @@ class Context:
         self._check(rc, "pas_gas_fit")
         return out
 
+    def gas_bind(self, gen_from: int, gen_to: int, pods, nodes, req: np.ndarray,
+                 req_mask: np.ndarray, n_containers: np.ndarray, i915_index: int):
+        """GASExtender.bindNode for binds (pods[b] -> nodes[b]) in order, committed into the
+        resident usage.  Returns (result words, statuses)."""
+        req = np.ascontiguousarray(req, dtype=np.int64)
+        p, c, q = req.shape
+        req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
+        n_containers = np.ascontiguousarray(n_containers, dtype=np.int32)
+        pods = np.ascontiguousarray(pods, dtype=np.int32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        res = np.zeros(len(pods), np.uint32)
+        st = np.zeros(len(pods), np.int32)
+        rc = self._l.pas_gas_bind(self._h, gen_from, gen_to, len(pods), _ptr(pods), _ptr(nodes),
+                                  p, c, i915_index, _ptr(req), _ptr(req_mask),
+                                  _ptr(n_containers), _ptr(res), _ptr(st))
+        self._check(rc, "pas_gas_bind")
+        return res, st
+
+    def gas_release(self, gen_from: int, gen_to: int, pods, nodes, req: np.ndarray,
+                    req_mask: np.ndarray, n_containers: np.ndarray, cards_per_container,
+                    cards) -> np.ndarray:
+        """adjustPodResources(remove) for pods leaving nodes; returns statuses."""
+        req = np.ascontiguousarray(req, dtype=np.int64)
+        p, c, q = req.shape
+        req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
+        n_containers = np.ascontiguousarray(n_containers, dtype=np.int32)
+        pods = np.ascontiguousarray(pods, dtype=np.int32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        cpc = np.ascontiguousarray(cards_per_container, dtype=np.int32).reshape(len(pods), c)
+        cards = np.ascontiguousarray(cards, dtype=np.int32).reshape(len(pods), 8)
+        st = np.zeros(len(pods), np.int32)
+        rc = self._l.pas_gas_release(self._h, gen_from, gen_to, len(pods), _ptr(pods),
+                                     _ptr(nodes), p, c, _ptr(req), _ptr(req_mask),
+                                     _ptr(n_containers), _ptr(cpc), _ptr(cards), _ptr(st))
+        self._check(rc, "pas_gas_release")
+        return st
+
+    def gas_snapshot_get(self):
+        """(generation, used [N][K][Q]) of the resident GAS snapshot."""
+        n, k, q = self.gas_shape
+        used = np.zeros((n, k, q), np.int64)
+        g = c_uint64()
+        self._check(self._l.pas_gas_snapshot_get(self._h, byref(g), _ptr(used)),
+                    "pas_gas_snapshot_get")
+        return g.value, used
+
     def gas_fit_device(self, gen: int, n_pods: int, max_containers: int, i915_index: int, req_t,
                        mask_t, ncont_t, res_t, stream=None):
         rc = self._l.pas_gas_fit_device(self._h, gen, n_pods, max_containers, i915_index,
