@@ -327,6 +327,39 @@ int pas_topk_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_sha
                           int32_t* d_out_len, void* hip_stream);
 
 /* ------------------------------------------------------------------------- */
+/* Wire encoders, host only                                */
+/* ------------------------------------------------------------------------- */
+
+/* Response bodies exactly as the reference's handlers write them with
+ * json.NewEncoder(w).Encode (encoding/json of Go 1.16, HTML-safe escaping, trailing "\n").
+ * Each writes at most cap bytes (no terminator), sets *out_len to the full length, and
+ * returns PAS_ECAPACITY when it exceeds cap.  names[i] / node_json[i] are indexed by
+ * snapshot node id.
+ *
+ * HostPriorityList of one pod (WritePrioritizeResponse, telemetryscheduler.go:152-158):
+ * order[0 .. len) from pas_tas_eval's order_out row -> [{"Host":..,"Score":10-i},...]. */
+int pas_encode_host_priority_list(int32_t len, const int32_t* order, const char* const* names,
+                                  char* buf, int64_t cap, int64_t* out_len);
+
+/* TAS FilterResult of one pod (filterNodes + WriteFilterResponse, telemetryscheduler.go:
+ * 184-225, 238-244): the request's nodes req_node[0 .. n_req) in request order, the pod's
+ * pass_out row; node_json[i] (node_json_len[i] bytes) = the JSON of node i as the Go shim
+ * encodes a v1.Node (spliced into "items").  The nil results (no policy label, policy not
+ * cached, no dontschedule rules, no nodes: :189-203) are the body "null\n", written by
+ * the shim. */
+int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const uint64_t* pass,
+                                 const char* const* names, const char* const* node_json,
+                                 const int64_t* node_json_len, char* buf, int64_t cap,
+                                 int64_t* out_len);
+
+/* GAS FilterResult of one pod (GASExtender.filterNodes, gpuscheduler/scheduler.go:449-482):
+ * request node names in order, fit = the pod's row of pas_gas_fit_bitmap_device (or bit 31
+ * of the pas_gas_fit words, packed); n_req == 0 gives the reference's error result. */
+int pas_encode_gas_filter_result(int32_t n_req, const int32_t* req_node, const uint64_t* fit,
+                                 const char* const* names, char* buf, int64_t cap,
+                                 int64_t* out_len);
+
+/* ------------------------------------------------------------------------- */
 /* Instrumentation                                                           */
 /* ------------------------------------------------------------------------- */
 

@@ -24,6 +24,7 @@
 #include <cstdint>
 #include <cstring>
 
+#include "json_out.h"
 #include "pas_internal.h"
 
 namespace pas {
@@ -96,56 +97,17 @@ __global__ __launch_bounds__(kTpb) void label_total_kernel(int32_t n_parts, int6
   }
 }
 
-// Go encoding/json string encoding: '"', '\\', \n \r \t, and other control bytes and the
-// HTML-unsafe <, >, & as \u00XX (json.Marshal escapes HTML by default).
-// Label names are Kubernetes label keys (ASCII), so the UTF-8 rules of the encoder
-// (U+2028/U+2029, invalid sequences) do not arise.
-struct JsonOut {
-  char* buf;
-  int64_t cap;
-  int64_t pos = 0;
-  void put(char c) {
-    if (pos < cap) buf[pos] = c;
-    ++pos;
-  }
-  void lit(const char* s) {
-    for (; *s; ++s) put(*s);
-  }
-  void str(const char* prefix, const char* s) {
-    static const char hex[] = "0123456789abcdef";
-    put('"');
-    for (int part = 0; part < 2; ++part) {
-      for (const unsigned char* c = (const unsigned char*)(part ? s : prefix); *c; ++c) {
-        switch (*c) {
-          case '"': put('\\'); put('"'); break;
-          case '\\': put('\\'); put('\\'); break;
-          case '\n': put('\\'); put('n'); break;
-          case '\r': put('\\'); put('r'); break;
-          case '\t': put('\\'); put('t'); break;
-          default:
-            if (*c < 0x20 || *c == '<' || *c == '>' || *c == '&') {
-              lit("\\u00");
-              put(hex[*c >> 4]);
-              put(hex[*c & 15]);
-            } else {
-              put((char)*c);
-            }
-        }
-      }
-    }
-    put('"');
-  }
-  // {"op":<op>,"path":"/metadata/labels/<name>","value":<value>} (patchValue, enforce.go:21-25)
-  void patch(const char* op, const char* name, const char* value) {
-    lit("{\"op\":");
-    str("", op);
-    lit(",\"path\":");
-    str("/metadata/labels/", name);
-    lit(",\"value\":");
-    str("", value);
-    put('}');
-  }
-};
+// One patchValue (enforce.go:21-25): {"op":<op>,"path":"/metadata/labels/<name>","value":<v>}
+void put_patch(JsonOut& o, const char* op, const char* name, const char* value) {
+  o.lit("{\"op\":");
+  o.str(op);
+  o.lit(",\"path\":\"");
+  o.str_body("/metadata/labels/");
+  o.str_body(name);
+  o.lit("\",\"value\":");
+  o.str(value);
+  o.put('}');
+}
 
 }  // namespace
 
@@ -187,15 +149,15 @@ extern "C" int pas_label_patch_json(int32_t n_strat, const char* const* names, u
   for (int32_t s = 0; s < n_strat; ++s)
     if (add_mask >> s & 1) {
       if (!first) o.put(',');
-      o.patch("add", names[s], "violating");
+      pas::put_patch(o, "add", names[s], "violating");
       first = false;
     }
   for (int32_t s = 0; s < n_strat; ++s)
     if (remove_mask >> s & 1) {
       if (!first) o.put(',');
-      o.patch("remove", names[s], "");
+      pas::put_patch(o, "remove", names[s], "");
       o.put(',');
-      o.patch("add", names[s], "null");
+      pas::put_patch(o, "add", names[s], "null");
       first = false;
     }
   o.put(']');

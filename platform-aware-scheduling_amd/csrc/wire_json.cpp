@@ -1,0 +1,184 @@
+// wire_json.cpp — extender response bodies from the evaluator's index outputs (SURVEY.md
+// §8 f2), byte for byte what the reference's handlers write with
+// json.NewEncoder(w).Encode(result) (a trailing newline included):
+//
+//   HostPriorityList (extender/types.go:25-33), WritePrioritizeResponse
+//     (telemetryscheduler.go:152-158):  [{"Host":"<name>","Score":<10-i>},...]
+//   TAS FilterResult (types.go:56-66), filterNodes + WriteFilterResponse
+//     (telemetryscheduler.go:184-225, 238-244):
+//     {"Nodes":{"metadata":{},"items":[<node>,...]},"NodeNames":["a","b",""],
+//      "FailedNodes":{"<name>":"Node violates",...},"Error":""}
+//     items is null when no node passes (a nil []v1.Node); NodeNames is
+//     strings.Split("<name> <name> ... ", " ") (:209-212): a trailing "", and a name with
+//     spaces split into pieces; map keys are sorted, as encoding/json does.
+//   GAS FilterResult, filterNodes (gpuscheduler/scheduler.go:449-482):
+//     {"Nodes":null,"NodeNames":[...] or null,"FailedNodes":{...},"Error":""}
+//     and the misconfiguration error result for an empty NodeNames (:455-461).
+//
+// The struct fields carry no json tags, so keys are the Go field names; v1.NodeList has
+// TypeMeta inline (kind / apiVersion omitempty, absent here) and ListMeta under "metadata"
+// (all fields omitempty: {}).  Node objects are spliced in as the caller's JSON text of each
+// node (the shim keeps json.Marshal(node) per snapshot node: nodes do not change between
+// requests).  Names are Kubernetes node names; the string encoder is nevertheless the
+// general one (json_out.h).
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "json_out.h"
+#include "pas.h"
+
+namespace {
+
+bool passed(const uint64_t* bits, int32_t n) { return (bits[n >> 6] >> (n & 63)) & 1ull; }
+
+// FailedNodes: distinct names sorted bytewise (Go sorts map keys by their string).
+void failed_nodes(pas::JsonOut& o, std::vector<const char*>& names, const char* reason) {
+  std::sort(names.begin(), names.end(), [](const char* a, const char* b) {
+    return std::strcmp(a, b) < 0;
+  });
+  names.erase(std::unique(names.begin(), names.end(),
+                          [](const char* a, const char* b) { return std::strcmp(a, b) == 0; }),
+              names.end());
+  o.put('{');
+  for (size_t i = 0; i < names.size(); ++i) {
+    if (i) o.put(',');
+    o.str(names[i]);
+    o.put(':');
+    o.str(reason);
+  }
+  o.put('}');
+}
+
+int finish(pas::JsonOut& o, int64_t* out_len) {
+  o.put('\n');  // json.Encoder terminates each value with a newline
+  *out_len = o.pos;
+  return o.pos <= o.cap ? PAS_OK : PAS_ECAPACITY;
+}
+
+bool out_ok(char* buf, int64_t cap, int64_t* out_len) {
+  return out_len && cap >= 0 && (cap == 0 || buf);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pas_encode_host_priority_list(int32_t len, const int32_t* order, const char* const* names,
+                                  char* buf, int64_t cap, int64_t* out_len) {
+  if (len < 0 || (len > 0 && (!order || !names)) || !out_ok(buf, cap, out_len))
+    return PAS_EINVAL;
+  for (int32_t i = 0; i < len; ++i)
+    if (order[i] < 0 || !names[order[i]]) return PAS_EINVAL;
+  pas::JsonOut o{buf, cap};
+  o.put('[');
+  for (int32_t i = 0; i < len; ++i) {
+    if (i) o.put(',');
+    o.lit("{\"Host\":");
+    o.str(names[order[i]]);
+    o.lit(",\"Score\":");
+    o.integer(10 - (int64_t)i);  // Score: 10 - i (telemetryscheduler.go:145-147)
+    o.put('}');
+  }
+  o.put(']');
+  return finish(o, out_len);
+}
+
+int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const uint64_t* pass,
+                                 const char* const* names, const char* const* node_json,
+                                 const int64_t* node_json_len, char* buf, int64_t cap,
+                                 int64_t* out_len) {
+  if (n_req < 0 || (n_req > 0 && (!req_node || !pass || !names || !node_json || !node_json_len)) ||
+      !out_ok(buf, cap, out_len))
+    return PAS_EINVAL;
+  for (int32_t i = 0; i < n_req; ++i)
+    if (req_node[i] < 0 || !names[req_node[i]] || !node_json[req_node[i]] ||
+        node_json_len[req_node[i]] < 0)
+      return PAS_EINVAL;
+  pas::JsonOut o{buf, cap};
+  bool any = false;
+  for (int32_t i = 0; i < n_req && !any; ++i) any = passed(pass, req_node[i]);
+  o.lit("{\"Nodes\":{\"metadata\":{},\"items\":");
+  if (!any) {
+    o.lit("null");
+  } else {
+    o.put('[');
+    bool first = true;
+    for (int32_t i = 0; i < n_req; ++i) {
+      const int32_t n = req_node[i];
+      if (!passed(pass, n)) continue;
+      if (!first) o.put(',');
+      first = false;
+      o.raw(node_json[n], node_json_len[n]);
+    }
+    o.put(']');
+  }
+  o.lit("},\"NodeNames\":[");
+  std::vector<const char*> failed;
+  for (int32_t i = 0; i < n_req; ++i) {
+    const int32_t n = req_node[i];
+    if (!passed(pass, n)) {
+      failed.push_back(names[n]);
+      continue;
+    }
+    // availableNodeNames += node.Name + " ", later split on " ": a name with spaces
+    // becomes several entries
+    const char* p = names[n];
+    for (;;) {
+      const char* sp = std::strchr(p, ' ');
+      const int64_t len = sp ? sp - p : (int64_t)std::strlen(p);
+      std::string piece(p, (size_t)len);
+      o.str(piece.c_str());
+      o.put(',');
+      if (!sp) break;
+      p = sp + 1;
+    }
+  }
+  o.lit("\"\"],\"FailedNodes\":");
+  // strings.Join([]string{"Node violates"}, policy.Name) is "Node violates" (:206)
+  failed_nodes(o, failed, "Node violates");
+  o.lit(",\"Error\":\"\"}");
+  return finish(o, out_len);
+}
+
+int pas_encode_gas_filter_result(int32_t n_req, const int32_t* req_node, const uint64_t* fit,
+                                 const char* const* names, char* buf, int64_t cap,
+                                 int64_t* out_len) {
+  if (n_req < 0 || (n_req > 0 && (!req_node || !fit || !names)) || !out_ok(buf, cap, out_len))
+    return PAS_EINVAL;
+  for (int32_t i = 0; i < n_req; ++i)
+    if (req_node[i] < 0 || !names[req_node[i]]) return PAS_EINVAL;
+  pas::JsonOut o{buf, cap};
+  if (n_req == 0) {  // args.NodeNames nil or empty (:455-461)
+    o.lit("{\"Nodes\":null,\"NodeNames\":null,\"FailedNodes\":null,\"Error\":");
+    o.str("No nodes to compare. This should not happen, perhaps the extender is "
+          "misconfigured with NodeCacheCapable == false.");
+    o.put('}');
+    return finish(o, out_len);
+  }
+  o.lit("{\"Nodes\":null,\"NodeNames\":");
+  bool first = true;
+  std::vector<const char*> failed;
+  for (int32_t i = 0; i < n_req; ++i) {
+    const int32_t n = req_node[i];
+    if (!passed(fit, n)) {
+      failed.push_back(names[n]);
+      continue;
+    }
+    o.put(first ? '[' : ',');
+    first = false;
+    o.str(names[n]);
+  }
+  if (first)
+    o.lit("null");  // var nodeNames []string stays nil
+  else
+    o.put(']');
+  o.lit(",\"FailedNodes\":");
+  failed_nodes(o, failed, "Not enough GPU-resources for deployment");
+  o.lit(",\"Error\":\"\"}");
+  return finish(o, out_len);
+}
+
+}  // extern "C"

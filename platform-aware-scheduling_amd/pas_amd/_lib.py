@@ -137,6 +137,13 @@ SIGNATURES = {
         [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_int32, c_int32, _P, _P, _P, _P],
     ),
     "pas_topk_merge_device": (c_int, [_P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P]),
+    "pas_encode_host_priority_list": (
+        c_int, [c_int32, _P, POINTER(c_char_p), c_char_p, c_int64, POINTER(c_int64)]),
+    "pas_encode_tas_filter_result": (
+        c_int, [c_int32, _P, _P, POINTER(c_char_p), POINTER(c_char_p), _P, c_char_p, c_int64,
+                POINTER(c_int64)]),
+    "pas_encode_gas_filter_result": (
+        c_int, [c_int32, _P, _P, POINTER(c_char_p), c_char_p, c_int64, POINTER(c_int64)]),
     "pas_set_timing": (c_int, [_P, c_int]),
     "pas_kernel_time": (c_int, [_P, c_int32, POINTER(c_double), POINTER(c_int64)]),
     "pas_reset_timing": (c_int, [_P]),

@@ -114,11 +114,15 @@ V["G7_filter"] = {
     "source": "telemetry-aware-scheduling/pkg/telemetryscheduler/scheduler_test.go:277-292",
     "policy": TEST_POLICY1,
     "nodes": ["node A", "node B"],
+    # The test asserts FailedNodes only (:321-337).  Derived: the nodes kept, and NodeNames =
+    # strings.Split(availableNodeNames, " ") (telemetryscheduler.go:209-212), which splits the
+    # test's space-containing names.
     "cases": [
         {"name": "get and return node test", "metrics": {"dummyMetric1": {"node A": 10, "node B": 30}},
-         "want_failed": [], "want_node_names": ["node A", "node B", ""]},
+         "want_failed": [], "want_passed": ["node A", "node B"],
+         "want_node_names": ["node", "A", "node", "B", ""]},
         {"name": "filter out one node", "metrics": {"dummyMetric1": {"node A": 50, "node B": 30}},
-         "want_failed": ["node A"], "want_node_names": ["node B", ""]},
+         "want_failed": ["node A"], "want_passed": ["node B"], "want_node_names": ["node", "B", ""]},
     ],
 }
 

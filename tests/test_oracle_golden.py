@@ -138,8 +138,9 @@ def test_g7_filter(oracle):
         passed = _filter(oracle, snap, g["policy"]["dontschedule"], g["nodes"])
         failed = [n for n in g["nodes"] if n not in passed]
         assert failed == c["want_failed"], c["name"]
-        # NodeNames = strings.Split(names + " ", " ") keeps a trailing "" (:209-212)
-        assert passed + [""] == c["want_node_names"], c["name"]
+        assert passed == c["want_passed"], c["name"]
+        # NodeNames = strings.Split("<passed names, each + ' '>", " ") (:209-212)
+        assert "".join(n + " " for n in passed).split(" ") == c["want_node_names"], c["name"]
 
 
 def test_g8_e2e(oracle):
