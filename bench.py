@@ -172,25 +172,52 @@ def bench_tas(args, world, rank):
     return out
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the box's CPU share for one GPU (16), at most."""
+    return max(1, min(16, os.cpu_count() or 1))
+
+
+def threaded_rate(run_range, n_items, per_item_s, budget_s, threads):
+    """Items/s of run_range(lo, hi) over a bounded sample split across `threads` Python
+    threads (the oracle's ctypes calls release the GIL).  Returns (rate, items, seconds)."""
+    from concurrent.futures import ThreadPoolExecutor
+    items = int(max(threads, min(n_items, budget_s * threads / max(per_item_s, 1e-6))))
+    # small chunks handed out dynamically (pods differ in cost)
+    chunk = max(1, items // (threads * 8))
+    bounds = [(lo, min(items, lo + chunk)) for lo in range(0, items, chunk)]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        list(ex.map(lambda b: run_range(*b), bounds))
+    t = time.perf_counter() - t0
+    return items / t, items, t
+
+
 def cpu_baseline_tas(snap, batch, budget_s):
-    """The C restatement of the reference (oracle/, 1 thread) on a bounded pod sample."""
+    """The C restatement of the reference (oracle/) on a bounded pod sample: one thread, and
+    pods partitioned over the host threads (SURVEY.md §8(d) Plan B)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle
     N = snap.v_milli.shape[1]
 
-    def run(pods):
-        off = batch.rule_off[: pods + 1]
-        t0 = time.perf_counter()
-        oracle.tas_eval(snap.v_milli, snap.present, batch.rules[: off[-1]], off,
-                        batch.prio[:pods], None, 3)
-        return time.perf_counter() - t0
+    def run_range(lo, hi):
+        if hi <= lo:
+            return
+        off = batch.rule_off[lo: hi + 1] - batch.rule_off[lo]
+        oracle.tas_eval(snap.v_milli, snap.present,
+                        batch.rules[batch.rule_off[lo]: batch.rule_off[hi]], off,
+                        batch.prio[lo:hi], None, 3)
 
-    one = run(1)
-    pods = int(max(1, min(len(batch.prio), budget_s / max(one, 1e-6))))
-    t = run(pods)
-    return {"value": pods * N / t, "unit": "pod-node evals/s", "cores": 1, "kind": "port",
-            "sample": f"{pods} pods x {N} nodes x 16 rules (first pods of the rank-0 batch), "
-                      f"{t:.1f} s, oracle/pas_oracle.c single thread"}
+    t0 = time.perf_counter()
+    run_range(0, 1)
+    one = time.perf_counter() - t0
+    single, pods1, t1 = threaded_rate(run_range, len(batch.prio), one, budget_s / 2, 1)
+    threads = cpu_threads()
+    multi, pods_t, tt = threaded_rate(run_range, len(batch.prio), one, budget_s / 2, threads)
+    return {"value": multi * N, "unit": "pod-node evals/s", "cores": threads, "kind": "port",
+            "single_thread_value": single * N,
+            "sample": f"{pods_t} pods x {N} nodes x 16 rules over {threads} threads in "
+                      f"{tt:.1f} s (1 thread: {pods1} pods in {t1:.1f} s); first pods of the "
+                      "rank-0 batch; oracle/pas_oracle.c, C restatement of the reference"}
 
 
 # ------------------------------------------------------------------------------- GAS
@@ -240,17 +267,22 @@ def bench_gas(args, world, rank):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
+
+        def run_range(lo, hi):
+            if hi > lo:
+                oracle.gas_fit(snap.n_cards, snap.cap, snap.used, batch.req[lo:hi],
+                               batch.req_mask[lo:hi], batch.n_containers[lo:hi], wl.I915)
+
         t0 = time.perf_counter()
-        oracle.gas_fit(snap.n_cards, snap.cap, snap.used, batch.req[:1], batch.req_mask[:1],
-                       batch.n_containers[:1], wl.I915)
+        run_range(0, 1)
         one = time.perf_counter() - t0
-        pods = int(max(1, min(P, args.cpu_seconds / max(one, 1e-6))))
-        t0 = time.perf_counter()
-        oracle.gas_fit(snap.n_cards, snap.cap, snap.used, batch.req[:pods],
-                       batch.req_mask[:pods], batch.n_containers[:pods], wl.I915)
-        t = time.perf_counter() - t0
-        out["cpu_baseline"] = {"value": pods * N / t, "unit": "pod-node fits/s", "cores": 1,
-                               "kind": "port", "sample": f"{pods} pods x {N} nodes, {t:.1f} s"}
+        single, pods1, t1 = threaded_rate(run_range, P, one, args.cpu_seconds / 2, 1)
+        threads = cpu_threads()
+        multi, pods_t, tt = threaded_rate(run_range, P, one, args.cpu_seconds / 2, threads)
+        out["cpu_baseline"] = {"value": multi * N, "unit": "pod-node fits/s", "cores": threads,
+                               "kind": "port", "single_thread_value": single * N,
+                               "sample": f"{pods_t} pods x {N} nodes over {threads} threads in "
+                                         f"{tt:.1f} s (1 thread: {pods1} pods in {t1:.1f} s)"}
     ctx.close()
     return out
 
