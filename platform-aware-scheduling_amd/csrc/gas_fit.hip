@@ -159,6 +159,8 @@ __device__ __forceinline__ void load_free(int32_t n, bool valid, int32_t ncard, 
     }
 }
 
+typedef unsigned long long lane_mask;  // one bit per lane of the wave (ballot)
+
 // First card (lexicographic rank) passing checkResourceCapacity, or -1: cmp[q] <= free[k][q]
 // for every kind (cmp is INT64_MIN for kinds the container does not request).
 template <int Q>
@@ -173,6 +175,15 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
     chosen = ok ? k : chosen;
   }
   return chosen;
+}
+
+// A wave-uniform value copied into a VGPR pair, so that selects against the condition mask
+// (VCC, one scalar operand) do not re-materialise it per use.
+__device__ __forceinline__ int64_t to_vgpr64(int64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)((uint64_t)x >> 32);
+  asm volatile("v_mov_b32 %0, %0" : "+v"(lo));
+  asm volatile("v_mov_b32 %0, %0" : "+v"(hi));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
@@ -283,21 +294,36 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
         const GasSel& e0 = stage[j][0];
         const GasSel& e1 = stage[j][1];
         int64_t cmp0[Q], cmp1[Q], cmp1t[Q];
+        bool ovf = false;  // need1 + take0 beyond int64: card c0 cannot take the second
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
           cmp0[q] = uniform64(e0.cmp[q]);
           cmp1[q] = uniform64(e1.cmp[q]);
-          cmp1t[q] = cmp1[q] + uniform64(e0.take[q]);  // INT64_MIN + 0 stays unrequested
+          // INT64_MIN + 0 stays unrequested
+          ovf |= __builtin_add_overflow(cmp1[q], uniform64(e0.take[q]), &cmp1t[q]);
         }
         const int c0 = __builtin_amdgcn_readfirstlane(e0.bad) ? -1 : first_fit<Q>(free, cmp0);
         int c1 = -1;
         if (!__builtin_amdgcn_readfirstlane(e1.bad)) {
+          // card k fits the second selection: cmp1 <= free (k != c0) or cmp1t <= free
+          // (k == c0; never when need1 + take0 overflows, a uniform and rare case)
+          if (!ovf) {
 #pragma unroll
-          for (int k = kMaxCards - 1; k >= 0; --k) {
-            bool ok = true;
+            for (int k = kMaxCards - 1; k >= 0; --k) {
+              bool ok = true;
 #pragma unroll
-            for (int q = 0; q < Q; ++q) ok = ok && (c0 == k ? cmp1t[q] : cmp1[q]) <= free[k][q];
-            c1 = ok ? k : c1;
+              for (int q = 0; q < Q; ++q)
+                ok = ok && (c0 == k ? cmp1t[q] : cmp1[q]) <= free[k][q];
+              c1 = ok ? k : c1;
+            }
+          } else {
+#pragma unroll
+            for (int k = kMaxCards - 1; k >= 0; --k) {
+              bool ok = c0 != k;
+#pragma unroll
+              for (int q = 0; q < Q; ++q) ok = ok && cmp1[q] <= free[k][q];
+              c1 = ok ? k : c1;
+            }
           }
         }
         out = (c0 >= 0 && c1 >= 0) ? (node_ok | (2u << 24) | (uint32_t)c0 | ((uint32_t)c1 << 3))
@@ -323,11 +349,14 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
           fits = fits && k >= 0;
           // per card taken by some lane of the wave (uniform branch), a per-lane select: a
           // divergent branch around the update would make the compiler copy the array
+          int64_t tv[Q];  // the takes in VGPRs once per step (a select may read one SGPR)
+#pragma unroll
+          for (int q = 0; q < Q; ++q) tv[q] = to_vgpr64(take[q]);
 #pragma unroll
           for (int kk = 0; kk < kMaxCards; ++kk)
             if (__ballot(k == kk))
 #pragma unroll
-              for (int q = 0; q < Q; ++q) w[kk][q] -= k == kk ? take[q] : 0;
+              for (int q = 0; q < Q; ++q) w[kk][q] -= k == kk ? tv[q] : 0;
           word |= (uint32_t)(k & 7) << (3 * t);
         }
         out = fits ? (node_ok | ((uint32_t)steps << 24) | word) : 0u;

@@ -116,3 +116,20 @@ def test_same_card_reuse_and_container_accumulation(ctx, oracle):
     assert decode_gas_word(got[0, 0]) == (True, [0, 0, 1])
     np.testing.assert_array_equal(got, oracle.gas_fit(n_cards, cap, used, req, mask,
                                                       np.array([2], np.int32), 0))
+
+
+def test_two_selection_take_overflow(ctx, oracle):
+    # two containers, one card each; the first takes INT64_MAX of a kind on card 0, so the
+    # second's check on card 0 overflows (used + need < 0 -> false, scheduler.go:367-371) and
+    # it must go to card 1
+    big = np.int64(2**63 - 1)
+    n_cards = np.array([2], np.int32)
+    cap = np.array([[10, big]], np.int64)
+    used = np.zeros((1, 2, 2), np.int64)
+    req = np.array([[[1, big], [1, 5]]], np.int64)
+    mask = np.array([[3, 3]], np.uint32)
+    ncont = np.array([2], np.int32)
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    assert decode_gas_word(want[0, 0]) == (True, [0, 1])
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
+    np.testing.assert_array_equal(got, want)
