@@ -133,3 +133,27 @@ def test_two_selection_take_overflow(ctx, oracle):
     assert decode_gas_word(want[0, 0]) == (True, [0, 1])
     got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_extreme_multi_selection_fuzz(ctx, oracle, seed):
+    # near-int64 capacities, usages and requests across several selections per pod: every
+    # overflow branch of checkResourceCapacity / addRM (scheduler.go:341-383,
+    # resource_map.go:77-98) through the single, two-selection and multi-selection paths
+    rng = np.random.default_rng(seed)
+    big = 2**63 - 1
+    n, k, q, p, c = 300, 3, 2, 64, 4
+    n_cards = rng.integers(0, k + 1, size=n).astype(np.int32)
+    cap = rng.choice(np.array([big, big - 1, 2**62, 2**61, 10], np.int64), size=(n, q))
+    used = rng.choice(np.array([0, 1, 2**62, 2**61, big - 5], np.int64), size=(n, k, q))
+    req = rng.choice(np.array([1, 2, 2**60, 2**61, 2**62, big - 1, big], np.int64),
+                     size=(p, c, q))
+    req[:, :, 0] = rng.integers(1, 3, size=(p, c))  # i915 selections per container
+    mask = np.full((p, c), 3, np.uint32)
+    ncont = rng.integers(1, c + 1, size=p).astype(np.int32)
+    for pi in range(p):  # at most 8 selections per pod
+        while int(req[pi, :ncont[pi], 0].sum()) > 8:
+            ncont[pi] -= 1
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
+    np.testing.assert_array_equal(got, want)
