@@ -1,0 +1,119 @@
+"""Host-side snapshot builders: the reference's cache contents in the
+layouts of pas_tas_snapshot_set / pas_gas_snapshot_set.  This is the work the Go shim does once
+per cache refresh; it is restated here so the whole path can be exercised from the
+reference's own data shapes (metric maps of Quantity strings, node labels, usage maps).
+
+TAS (cache/autoupdating.go:76-85, metrics/client.go:25-32): one column per metric name, one
+row bit per node that has the metric, value * 1000 exact (pas_quantity_to_milli); values
+that are not milli-exact are reported and keep that metric on the CPU path.
+
+GAS (gpuscheduler/scheduler.go:132-178, 269-275; node_resource_cache.go:474-491):
+  cards      strings.Split(label "gpu.intel.com/cards", ".") -- duplicates and empty names
+             included -- gives gpuCount; the cards a selection walks are the node's usage map
+             keys plus the label cards (addEmptyResourceMaps), in sort.Strings order, minus
+             cards not in the label (skipped as "vanished"): the sorted distinct label cards
+  capacity   AsInt64 of every allocatable "gpu.intel.com/*" resource, divided by gpuCount
+             (truncating); a kind the node does not advertise has capacity 0 (fails as missing)
+  used       the usage map of each of those cards (a missing kind is 0)
+  n_cards    number of those cards; 0 without the label (errWontFit, :290-298); -1 for a node
+             the lister does not know (FetchNode error, :282-288)
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .context import quantity_as_int64, quantity_to_milli, w64
+
+GPU_LIST_LABEL = "gpu.intel.com/cards"
+RESOURCE_PREFIX = "gpu.intel.com/"
+
+
+def tas_snapshot_from_metrics(metrics: Mapping[str, Mapping[str, str]],
+                              node_names: Sequence[str],
+                              metric_names: Optional[Sequence[str]] = None):
+    """(v_milli [M][N] int64, present [M][W64] uint64, inexact [(metric, node)]) from
+    {metric: {node: quantity string}}.  Nodes not in node_names are ignored."""
+    metric_names = list(metrics) if metric_names is None else list(metric_names)
+    index = {n: i for i, n in enumerate(node_names)}
+    n, m = len(node_names), len(metric_names)
+    v = np.zeros((m, n), np.int64)
+    present = np.zeros((m, w64(n)), np.uint64)
+    inexact: List[Tuple[str, str]] = []
+    for j, name in enumerate(metric_names):
+        for node, q in metrics.get(name, {}).items():
+            i = index.get(node)
+            if i is None:
+                continue
+            try:
+                v[j, i] = quantity_to_milli(q)
+            except _lib.PasError as e:
+                if e.code != _lib.PAS_ENOTEXACT:
+                    raise
+                inexact.append((name, node))
+                continue
+            present[j, i >> 6] |= np.uint64(1 << (i & 63))
+    return v, present, inexact
+
+
+def go_sort_strings(names):
+    """sort.Strings: bytewise order of the UTF-8 encodings ("card10" < "card2")."""
+    return sorted(names, key=lambda s: s.encode())
+
+
+def gas_snapshot_from_nodes(nodes: Sequence[Optional[dict]], kinds: Sequence[str],
+                            max_cards: int = _lib.PAS_GAS_MAX_CARDS):
+    """(n_cards [N] int32, cap_per_gpu [N][Q] int64, used [N][K][Q] int64, card_names) from
+    per-node dicts {"labels": {...}, "allocatable": {resource: quantity}, "usage":
+    {card: {resource: int}}}, or None for a node the lister does not know.  card_names[n]
+    lists the node's cards in rank order (rank = the 3-bit index in a pas_gas_fit word)."""
+    q = len(kinds)
+    k_max = max_cards
+    n = len(nodes)
+    n_cards = np.zeros(n, np.int32)
+    cap = np.zeros((n, q), np.int64)
+    used = np.zeros((n, k_max, q), np.int64)
+    card_names: List[List[str]] = []
+    for i, node in enumerate(nodes):
+        if node is None:
+            n_cards[i] = -1
+            card_names.append([])
+            continue
+        labels = node.get("labels") or {}
+        if GPU_LIST_LABEL not in labels:
+            card_names.append([])
+            continue
+        gpus = labels[GPU_LIST_LABEL].split(".")
+        gpu_count = len(gpus)
+        cards = go_sort_strings(set(gpus))
+        if len(cards) > k_max:
+            raise _lib.PasError(_lib.PAS_ECAPACITY,
+                                f"node {i}: {len(cards)} cards > {k_max} (PAS_GAS_MAX_CARDS)")
+        n_cards[i] = len(cards)
+        card_names.append(cards)
+        alloc = node.get("allocatable") or {}
+        for j, kind in enumerate(kinds):
+            if kind in alloc and kind.startswith(RESOURCE_PREFIX):
+                # resourceMap.divide: Go integer division truncates toward zero
+                value = quantity_as_int64(alloc[kind])
+                share = abs(value) // gpu_count
+                cap[i, j] = -share if value < 0 else share
+        usage: Dict[str, Dict[str, int]] = node.get("usage") or {}
+        for r, card in enumerate(cards):
+            for j, kind in enumerate(kinds):
+                used[i, r, j] = int(usage.get(card, {}).get(kind, 0))
+    return n_cards, cap, used, card_names
+
+
+def annotation(word: int, container_i915: Sequence[int], card_names: Sequence[str]) -> str:
+    """The "gas-container-cards" annotation (scheduler.go:317-335) of a pas_gas_fit word:
+    container c takes its next container_i915[c] selections; cards joined by ",", containers
+    by "|"."""
+    ranks = [(int(word) >> (3 * s)) & 7 for s in range((int(word) >> 24) & 15)]
+    out, pos = [], 0
+    for n in container_i915:
+        out.append(",".join(card_names[r] for r in ranks[pos:pos + n]))
+        pos += n
+    return "|".join(out)
