@@ -359,6 +359,10 @@ int pas_encode_gas_filter_result(int32_t n_req, const int32_t* req_node, const u
                                  const char* const* names, char* buf, int64_t cap,
                                  int64_t* out_len);
 
+/* BindingResult of GASExtender.bindNode (scheduler.go:385-445): {"Error":"<error>"}; NULL or
+ * "" for success. */
+int pas_encode_binding_result(const char* error, char* buf, int64_t cap, int64_t* out_len);
+
 /* ------------------------------------------------------------------------- */
 /* Instrumentation                                                           */
 /* ------------------------------------------------------------------------- */

@@ -181,4 +181,15 @@ int pas_encode_gas_filter_result(int32_t n_req, const int32_t* req_node, const u
   return finish(o, out_len);
 }
 
+// BindingResult (extender/types.go:79-82) of GASExtender.bindNode (scheduler.go:385-445):
+// {"Error":"<err.Error()>"} or {"Error":""} on success.
+int pas_encode_binding_result(const char* error, char* buf, int64_t cap, int64_t* out_len) {
+  if (!out_ok(buf, cap, out_len)) return PAS_EINVAL;
+  pas::JsonOut o{buf, cap};
+  o.lit("{\"Error\":");
+  o.str(error ? error : "");
+  o.put('}');
+  return finish(o, out_len);
+}
+
 }  // extern "C"

@@ -144,6 +144,7 @@ SIGNATURES = {
                 POINTER(c_int64)]),
     "pas_encode_gas_filter_result": (
         c_int, [c_int32, _P, _P, POINTER(c_char_p), c_char_p, c_int64, POINTER(c_int64)]),
+    "pas_encode_binding_result": (c_int, [c_char_p, c_char_p, c_int64, POINTER(c_int64)]),
     "pas_set_timing": (c_int, [_P, c_int]),
     "pas_kernel_time": (c_int, [_P, c_int32, POINTER(c_double), POINTER(c_int64)]),
     "pas_reset_timing": (c_int, [_P]),

@@ -1,0 +1,261 @@
+"""The reference's extender handlers over the C-ABI (BASELINE north_star: "drops in behind
+the existing scheduler/filter and scheduler/prioritize HTTP verbs").
+
+MetricsExtender mirrors telemetry-aware-scheduling/pkg/telemetryscheduler/telemetryscheduler.go
+and GASExtender mirrors gpu-aware-scheduling/pkg/gpuscheduler/scheduler.go: same verbs, same
+request decoding (extender.Args, BindingArgs), same status codes and bodies, same early
+returns.  The evaluation goes through libpas.so (pas_tas_eval, pas_gas_fit, pas_gas_bind) and
+the bodies through its wire encoders.  A verb takes the request body and returns
+(HTTP status, response body), as an http.ResponseWriter would have received them.
+
+The Go shim is the production host; this module is its restatement for the
+tests, with the same names and error behaviour.
+"""
+from __future__ import annotations
+
+import json
+from typing import Dict, Mapping, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib, wire
+from .context import Context, make_rules, parse_operator, quantity_as_int64, w64
+
+TAS_POLICY_LABEL = "telemetry-policy"  # telemetryscheduler.go: tasPolicy
+I915 = "gpu.intel.com/i915"
+
+
+def _field(obj, name):
+    """encoding/json field lookup: exact key first, then case-insensitive (Args has no json
+    tags; the kube-scheduler sends "pod", "nodes", "nodenames")."""
+    if not isinstance(obj, dict):
+        return None
+    if name in obj:
+        return obj[name]
+    low = name.lower()
+    for k, v in obj.items():
+        if k.lower() == low:
+            return v
+    return None
+
+
+def _decode(body: bytes):
+    if not body:
+        raise ValueError("request body empty")
+    return json.loads(body)
+
+
+def _node_name(item) -> str:
+    return ((item or {}).get("metadata") or {}).get("name", "")
+
+
+class MetricsExtender:
+    """TAS extender: Filter / Prioritize / Bind (telemetryscheduler.go:36-244).
+
+    policies: {(namespace, name): {"dontschedule": [(metric, op, target)],
+                                   "scheduleonmetric": [(metric, op, target)]}}
+    The context holds the TAS snapshot of generation `gen` over `node_names` x `metric_names`.
+    """
+
+    def __init__(self, ctx: Context, gen: int, node_names: Sequence[str],
+                 metric_names: Sequence[str], policies: Mapping[Tuple[str, str], dict]):
+        self.ctx, self.gen = ctx, gen
+        self.node_index = {n: i for i, n in enumerate(node_names)}
+        self.metric_index = {m: i for i, m in enumerate(metric_names)}
+        self.policies = policies
+        self.table = wire.NodeTable(node_names)
+
+    # -- helpers ------------------------------------------------------------------
+    def _policy(self, pod) -> Optional[dict]:
+        """getPolicyFromPod (:103-112)."""
+        meta = (pod or {}).get("metadata") or {}
+        name = (meta.get("labels") or {}).get(TAS_POLICY_LABEL)
+        if name is None:
+            return None
+        return self.policies.get((meta.get("namespace", ""), name))
+
+    def _rules(self, triples):
+        metric, op, target = [], [], []
+        for m, o, t in triples:
+            metric.append(self.metric_index.get(m, -1))  # not cached: skipped (strategy.go:28-32)
+            code = parse_operator(o)
+            if code < 0:
+                raise ValueError(f"unknown operator {o!r}")  # the reference panics
+            op.append(code)
+            target.append(int(t))
+        return make_rules(metric, op, target)
+
+    def _request_nodes(self, nodes):
+        items = nodes.get("items") if isinstance(nodes, dict) else None
+        items = items or []
+        return items, np.array([self.node_index.get(_node_name(it), -1) for it in items],
+                               np.int32)
+
+    def _cand(self, idx):
+        cand = np.zeros((1, w64(len(self.node_index))), np.uint64)
+        for i in idx:
+            if i >= 0:
+                cand[0, i >> 6] |= np.uint64(1 << (int(i) & 63))
+        return cand
+
+    # -- verbs --------------------------------------------------------------------
+    def filter(self, body: bytes) -> Tuple[int, bytes]:
+        """Filter + filterNodes + WriteFilterResponse (:162-244)."""
+        try:
+            args = _decode(body)
+            nodes = _field(args, "Nodes")
+            if nodes is None:
+                raise ValueError("no nodes in list")
+        except ValueError:
+            return 200, b""  # decode error: nothing written (:164-168)
+        pod = _field(args, "Pod")
+        policy = self._policy(pod)
+        rules = (policy or {}).get("dontschedule") or []
+        items, idx = self._request_nodes(nodes)
+        if policy is None or not rules or len(items) == 0:
+            return 404, b"null\n"  # nil FilterResult (:189-203)
+        if (idx < 0).any():
+            raise KeyError("request node not in the snapshot")
+        r = self._rules(rules)
+        pass_out, _, _ = self.ctx.tas_eval(self.gen, r, np.array([0, len(r)], np.int32),
+                                           make_rules([-1], [0], [0]), self._cand(idx),
+                                           _lib.PAS_TAS_FILTER)
+        blobs = [json.dumps(it, separators=(",", ":")).encode() for it in items]
+        table = wire.NodeTable([_node_name(it) for it in items], blobs)
+        order = np.arange(len(items), dtype=np.int32)
+        # the pass row re-indexed to the request's own order (duplicates keep their verdict)
+        row = np.zeros(w64(len(items)), np.uint64)
+        for j, i in enumerate(idx):
+            if (int(pass_out[0, i >> 6]) >> (int(i) & 63)) & 1:
+                row[j >> 6] |= np.uint64(1 << (j & 63))
+        return 200, wire.tas_filter_result(order, row, table)
+
+    def prioritize(self, body: bytes) -> Tuple[int, bytes]:
+        """Prioritize + prioritizeNodes + WritePrioritizeResponse (:36-158)."""
+        try:
+            args = _decode(body)
+            nodes = _field(args, "Nodes")
+            if nodes is None:
+                raise ValueError("no nodes in list")
+        except ValueError:
+            return 200, b""
+        items, idx = self._request_nodes(nodes)
+        if len(items) == 0:
+            return 200, b""  # no nodes: nothing written (:46-49)
+        pod = _field(args, "Pod")
+        status = 200
+        labels = (((pod or {}).get("metadata") or {}).get("labels") or {})
+        if TAS_POLICY_LABEL not in labels:
+            status = 400  # (:50-53), then the (empty) list is still written
+        policy = self._policy(pod)
+        prio = (policy or {}).get("scheduleonmetric") or []
+        # getSchedulingRule (:115-124): first rule with a metric name; errors -> []
+        if policy is None or not prio or not prio[0][0]:
+            return status, b"[]\n"
+        if prio[0][0] not in self.metric_index:  # ReadMetric error -> [] (:130-133)
+            return status, b"[]\n"
+        if (idx < 0).any():
+            raise KeyError("request node not in the snapshot")
+        code = parse_operator(prio[0][1])
+        p = make_rules([self.metric_index[prio[0][0]]], [code if code >= 0 else 3],
+                       [int(prio[0][2])])
+        _, order, lens = self.ctx.tas_eval(self.gen, make_rules([], [], []),
+                                           np.zeros(2, np.int32), p, self._cand(idx),
+                                           _lib.PAS_TAS_PRIORITIZE)
+        return status, wire.host_priority_list(order[0, : lens[0]], self.table)
+
+    def bind(self, body: bytes) -> Tuple[int, bytes]:
+        return 404, b""  # not implemented by TAS (:178-181)
+
+
+class GASExtender:
+    """GAS extender: Filter / Bind / Prioritize (gpuscheduler/scheduler.go:385-573).
+
+    The context holds the GAS snapshot (generation `gen`) built by
+    pas_amd.snapshot.gas_snapshot_from_nodes over `node_names` with `card_names` and `kinds`;
+    `pods` resolves BindingArgs to pods ({(namespace, name): v1.Pod JSON object})."""
+
+    def __init__(self, ctx: Context, gen: int, node_names: Sequence[str],
+                 card_names: Sequence[Sequence[str]], kinds: Sequence[str],
+                 pods: Optional[Dict[Tuple[str, str], dict]] = None):
+        self.ctx, self.gen = ctx, gen
+        self.node_index = {n: i for i, n in enumerate(node_names)}
+        self.card_names = card_names
+        self.kinds = list(kinds)
+        self.pods = pods if pods is not None else {}
+        self.i915 = self.kinds.index(I915) if I915 in self.kinds else -1
+
+    def _requests(self, pod):
+        """containerRequests (utils.go:14-32): gpu.intel.com/ requests, AsInt64 (ok ignored)."""
+        containers = (((pod or {}).get("spec") or {}).get("containers") or [])
+        c = max(1, len(containers))
+        req = np.zeros((1, c, len(self.kinds)), np.int64)
+        mask = np.zeros((1, c), np.uint32)
+        per_container = []
+        for ci, cont in enumerate(containers):
+            reqs = (((cont or {}).get("resources") or {}).get("requests") or {})
+            i915 = 0
+            for name, q in reqs.items():
+                if not name.startswith("gpu.intel.com/"):
+                    continue
+                if name not in self.kinds:
+                    raise KeyError(f"resource kind {name} not in the snapshot")
+                j = self.kinds.index(name)
+                req[0, ci, j] = quantity_as_int64(q)
+                mask[0, ci] |= 1 << j
+                if name == I915:
+                    i915 = max(int(req[0, ci, j]), 0)
+            per_container.append(i915 if mask[0, ci] else 0)
+        return req, mask, np.array([len(containers)], np.int32), per_container
+
+    def filter(self, body: bytes) -> Tuple[int, bytes]:
+        """Filter + filterNodes (:449-482, 523-543)."""
+        try:
+            args = _decode(body)
+        except ValueError:
+            return 404, b""
+        names = _field(args, "NodeNames") or []
+        table = wire.NodeTable(names)
+        if not names:
+            return 404, wire.gas_filter_result([], np.zeros(1, np.uint64), table)
+        req, mask, ncont, _ = self._requests(_field(args, "Pod"))
+        res = self.ctx.gas_fit(self.gen, req, mask, ncont, self.i915)
+        fit = np.zeros(w64(len(names)), np.uint64)
+        for j, name in enumerate(names):
+            i = self.node_index.get(name)
+            if i is not None and int(res[0, i]) >> 31:  # unknown node: FetchNode error
+                fit[j >> 6] |= np.uint64(1 << (j & 63))
+        return 200, wire.gas_filter_result(np.arange(len(names), dtype=np.int32), fit, table)
+
+    def bind(self, body: bytes) -> Tuple[int, bytes]:
+        """Bind + bindNode (:385-445, 546-566): fit on the current usage, commit, annotate."""
+        try:
+            args = _decode(body)
+        except ValueError:
+            return 404, b""
+        key = (_field(args, "PodNamespace") or "", _field(args, "PodName") or "")
+        pod = self.pods.get(key)
+        if pod is None:  # fetchPod: the lister's NotFound error (node_resource_cache.go:460-471)
+            return 404, self._error(f'pod "{key[1]}" not found')
+        node_name = _field(args, "Node") or ""
+        node = self.node_index.get(node_name)
+        req, mask, ncont, per_container = self._requests(pod)
+        if node is None:  # runSchedulingLogic -> FetchNode error (:282-288)
+            return 404, self._error(f'node "{node_name}" not found')
+        res, st = self.ctx.gas_bind(self.gen, self.gen + 1, [0], [node], req, mask, ncont,
+                                    self.i915)
+        self.gen += 1
+        if st[0] != _lib.PAS_GAS_OK:
+            return 404, self._error("will not fit")  # errWontFit (:49)
+        from .snapshot import annotation
+        pod.setdefault("metadata", {}).setdefault("annotations", {})[
+            "gas-container-cards"] = annotation(int(res[0]), per_container, self.card_names[node])
+        return 200, wire.binding_result("")
+
+    def prioritize(self, body: bytes) -> Tuple[int, bytes]:
+        return 404, b""  # not implemented by GAS (:517-519)
+
+    @staticmethod
+    def _error(msg: str) -> bytes:
+        """BindingResult{Error: msg} through json.NewEncoder (:508-513)."""
+        return wire.binding_result(msg)

@@ -77,3 +77,8 @@ def gas_filter_result(req_nodes, fit_row, table: NodeTable) -> bytes:
     fit_row = np.ascontiguousarray(fit_row, dtype=np.uint64)
     return _call(_lib.load().pas_encode_gas_filter_result, len(req_nodes), _ptr(req_nodes),
                  _ptr(fit_row), table.names)
+
+
+def binding_result(error: str = "") -> bytes:
+    """BindingResult {"Error": ...} of a GAS bind."""
+    return _call(_lib.load().pas_encode_binding_result, error.encode())

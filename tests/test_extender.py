@@ -1,0 +1,140 @@
+"""The extender verbs end to end, as the reference's handler tests drive them
+(telemetryscheduler/scheduler_test.go: JSON requests built from twoNodeArgument / noPolicyPod,
+responses decoded and compared), through pas_amd.extender over libpas.so.  Marked gpu."""
+import json
+
+import numpy as np
+import pytest
+
+import pas_amd
+from pas_amd import extender as ext
+from pas_amd import snapshot as sn
+from helpers import golden
+
+pytestmark = pytest.mark.gpu
+G = golden()
+
+# scheduler_test.go:28-62
+TEST_POLICY1 = {("default", "test-policy"): {
+    "scheduleonmetric": [("dummyMetric1", "GreaterThan", 0)],
+    "dontschedule": [("dummyMetric1", "GreaterThan", 40)]}}
+TEST_POLICY2 = {("default", "other-policy"): TEST_POLICY1[("default", "test-policy")]}
+
+
+def node(name):
+    return {"metadata": {"name": name}, "spec": {}, "status": {}}
+
+
+def args(pod_labels, names, key_case=str):
+    a = {"Pod": {"metadata": {"name": "big pod", "labels": pod_labels, "namespace": "default"}},
+         "Nodes": {"metadata": {}, "items": [node(n) for n in names]},
+         "NodeNames": list(names)}
+    return json.dumps({key_case(k): v for k, v in a.items()}).encode()
+
+
+TWO_NODES = dict(pod_labels={"telemetry-policy": "test-policy"}, names=["node A", "node B"])
+
+
+def tas(ctx, metric_values, policies, gen):
+    names = ["node A", "node B"]
+    v, pres, inexact = sn.tas_snapshot_from_metrics(
+        {"dummyMetric1": {k: str(x) for k, x in metric_values.items()}}, names)
+    assert not inexact
+    ctx.tas_snapshot_set(gen, v, pres)
+    return ext.MetricsExtender(ctx, gen, names, ["dummyMetric1"], policies)
+
+
+def test_prioritize_golden_g5(ctx):
+    g = G["G5_prioritize"]
+    m = tas(ctx, g["metrics"]["dummyMetric1"], TEST_POLICY1, 8100)
+    for case in (str, str.lower):  # the kube-scheduler sends lower-case keys
+        status, body = m.prioritize(args(**TWO_NODES, key_case=case))
+        assert status == 200
+        assert [[h["Host"], h["Score"]] for h in json.loads(body)] == g["want"]
+        assert body.endswith(b"\n")
+
+
+def test_prioritize_errors_g6(ctx):
+    # policy not found -> [] (scheduler_test.go:175-183)
+    m = tas(ctx, {"node A": 90, "node B": 100}, TEST_POLICY2, 8101)
+    assert m.prioritize(args(**TWO_NODES)) == (200, b"[]\n")
+    # unlabelled pod -> 400 and [] (scheduler_test.go:104-112; telemetryscheduler.go:50-53)
+    m = tas(ctx, {"node A": 100, "node B": 90}, TEST_POLICY1, 8102)
+    status, body = m.prioritize(args({"useless-label": "test-policy"}, ["node A"]))
+    assert status == 400 and body == b"[]\n"
+    # malformed arguments: extender.Args{} has Nodes == nil -> decode error, nothing written
+    assert m.prioritize(b"{}") == (200, b"")
+    assert m.prioritize(b"") == (200, b"")
+
+
+def test_filter_golden_g7(ctx):
+    g = G["G7_filter"]
+    for gen, c in enumerate(g["cases"], start=8110):
+        m = tas(ctx, c["metrics"]["dummyMetric1"], TEST_POLICY1, gen)
+        status, body = m.filter(args(**TWO_NODES))
+        assert status == 200
+        res = json.loads(body)
+        # the reference test's assertion (scheduler_test.go:321-337)
+        assert sorted(res["FailedNodes"]) == sorted(c["want_failed"])
+        assert res["NodeNames"] == c["want_node_names"]
+        assert [it["metadata"]["name"] for it in res["Nodes"]["items"] or []] == c["want_passed"]
+
+
+def test_filter_nil_results(ctx):
+    m = tas(ctx, {"node A": 10, "node B": 30}, TEST_POLICY1, 8120)
+    # no policy label, policy not cached, no nodes: nil FilterResult -> 404 + null
+    assert m.filter(args({"useless-label": "x"}, ["node A"])) == (404, b"null\n")
+    m2 = tas(ctx, {"node A": 10, "node B": 30}, TEST_POLICY2, 8121)
+    assert m2.filter(args(**TWO_NODES)) == (404, b"null\n")
+    assert m.filter(args({"telemetry-policy": "test-policy"}, [])) == (404, b"null\n")
+    # no dontschedule strategy
+    m3 = tas(ctx, {"node A": 10}, {("default", "test-policy"): {
+        "scheduleonmetric": [("dummyMetric1", "GreaterThan", 0)]}}, 8122)
+    assert m3.filter(args(**TWO_NODES)) == (404, b"null\n")
+    assert m.bind(b"{}") == (404, b"")
+
+
+def gas_cluster():
+    nodes = [{"labels": {"gpu.intel.com/cards": "card0.card1"},
+              "allocatable": {"gpu.intel.com/i915": "2", "gpu.intel.com/memory.max": "16G"}},
+             {"labels": {}, "allocatable": {}}]
+    return ["node-1", "node-2"], nodes
+
+
+def gas_pod(name, mem="5G", i915="1"):
+    return {"metadata": {"name": name, "namespace": "default"},
+            "spec": {"containers": [{"resources": {"requests": {
+                "gpu.intel.com/i915": i915, "gpu.intel.com/memory.max": mem}}}]}}
+
+
+def test_gas_filter_and_bind_readme(ctx):
+    # README.md:15-21 worked example through the GAS verbs: three 5 GB pods bound in turn
+    names, nodes = gas_cluster()
+    kinds = ["gpu.intel.com/i915", "gpu.intel.com/memory.max"]
+    n_cards, cap, used, card_names = sn.gas_snapshot_from_nodes(nodes, kinds)
+    ctx.gas_snapshot_set(8200, n_cards, cap, used)
+    pods = {("default", f"p{i}"): gas_pod(f"p{i}") for i in range(3)}
+    g = ext.GASExtender(ctx, 8200, names, card_names, kinds, pods)
+    body = json.dumps({"Pod": pods[("default", "p0")], "NodeNames": names}).encode()
+    status, out = g.filter(body)
+    res = json.loads(out)
+    assert status == 200 and res["NodeNames"] == ["node-1"]
+    assert res["FailedNodes"] == {"node-2": "Not enough GPU-resources for deployment"}
+    want = G["G11_gas_readme"]["memory_example"]["want"]
+    for i, w in enumerate(want):
+        status, out = g.bind(json.dumps({"PodName": f"p{i}", "PodNamespace": "default",
+                                         "PodUID": "", "Node": "node-1"}).encode())
+        if w["fits"]:
+            assert (status, out) == (200, b'{"Error":""}\n')
+            ann = pods[("default", f"p{i}")]["metadata"]["annotations"]["gas-container-cards"]
+            assert ann == w["annotation"]
+        else:
+            assert (status, out) == (404, b'{"Error":"will not fit"}\n')
+    # after the binds the node is full for a fourth pod: filter sees the committed usage
+    status, out = g.filter(body)
+    assert json.loads(out)["NodeNames"] is None
+    # errors
+    assert g.filter(json.dumps({"Pod": pods[("default", "p0")], "NodeNames": []}).encode())[0] == 404
+    assert g.bind(json.dumps({"PodName": "nope", "PodNamespace": "default"}).encode()) == \
+        (404, b'{"Error":"pod \\"nope\\" not found"}\n')
+    assert g.prioritize(b"{}") == (404, b"")
