@@ -259,3 +259,47 @@ class GASExtender:
     def _error(msg: str) -> bytes:
         """BindingResult{Error: msg} through json.NewEncoder (:508-513)."""
         return wire.binding_result(msg)
+
+
+class DescheduleEnforcer:
+    """deschedule.Strategy.Enforce over the registered deschedule strategies
+    (telemetry-aware-scheduling/pkg/strategies/deschedule/enforce.go:57-164):
+    nodeStatusForStrategy (pas_tas_violations), updateNodeLabels (pas_tas_label_plan) and
+    the PATCH bodies (pas_label_patch_json).
+
+    strategies: [(policy name, [(metric, op, target), ...])] in registration order."""
+
+    def __init__(self, ctx: Context, gen: int, node_names: Sequence[str],
+                 metric_names: Sequence[str], strategies: Sequence[Tuple[str, list]]):
+        self.ctx, self.gen = ctx, gen
+        self.node_names = list(node_names)
+        self.metric_index = {m: i for i, m in enumerate(metric_names)}
+        self.names = [s[0] for s in strategies]
+        metric, op, target, off = [], [], [], [0]
+        for _, rules in strategies:
+            for m, o, t in rules:
+                metric.append(self.metric_index.get(m, -1))
+                code = parse_operator(o)
+                if code < 0:
+                    raise ValueError(f"unknown operator {o!r}")  # the reference panics
+                op.append(code)
+                target.append(int(t))
+            off.append(len(metric))
+        self.rules = make_rules(metric, op, target)
+        self.rule_off = np.array(off, np.int32)
+
+    def enforce(self, node_labels: Sequence[Mapping[str, str]]):
+        """(totalViolations, {node name: PATCH body}) for the listed nodes' current labels;
+        every node gets a body, "[]" when nothing changes (enforce.go:104-135)."""
+        n, s = len(self.node_names), len(self.names)
+        viol = self.ctx.tas_violations(self.gen, self.rules, self.rule_off)
+        labels = np.zeros((s, w64(n)), np.uint64)
+        for i, lab in enumerate(node_labels):
+            for j, name in enumerate(self.names):
+                if name in lab:
+                    labels[j, i >> 6] |= np.uint64(1 << (i & 63))
+        add, rem, total = self.ctx.tas_label_plan(n, viol, labels)
+        from .context import label_patch_json
+        bodies = {self.node_names[i]: label_patch_json(self.names, int(add[i]), int(rem[i]))
+                  for i in range(n)}
+        return total, bodies

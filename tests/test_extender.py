@@ -138,3 +138,21 @@ def test_gas_filter_and_bind_readme(ctx):
     assert g.bind(json.dumps({"PodName": "nope", "PodNamespace": "default"}).encode()) == \
         (404, b'{"Error":"pod \\"nope\\" not found"}\n')
     assert g.prioritize(b"{}") == (404, b"")
+
+
+def test_deschedule_enforce_g4(ctx):
+    # deschedule/enforce_test.go:38-52 through the Enforce mirror
+    from test_oracle_golden import apply_label_patch
+    g = G["G4_deschedule_enforce"]
+    for gen, c in enumerate(g["cases"], start=8300):
+        v, pres, _ = sn.tas_snapshot_from_metrics(
+            {m: {k: str(x) for k, x in vals.items()} for m, vals in g["metrics"].items()},
+            g["nodes"], ["memory", "cpu"])
+        ctx.tas_snapshot_set(gen, v, pres)
+        e = ext.DescheduleEnforcer(ctx, gen, g["nodes"], ["memory", "cpu"],
+                                   [(g["policy"], [tuple(r) for r in c["rules"]])])
+        total, bodies = e.enforce([c["labels"]])
+        assert total == c["derived"]["total"]
+        assert bodies["node-1"].decode() == c["derived"]["patch"]
+        after = apply_label_patch(c["labels"], bodies["node-1"])
+        assert [n for n in g["nodes"] if after.get(g["policy"]) == "violating"] == c["want"]
