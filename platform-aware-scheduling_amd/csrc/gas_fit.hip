@@ -265,8 +265,6 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     const int64_t* __restrict__ used, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts,
     uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
-  __shared__ GasSel stage[kMultiBatch][PAS_GAS_MAX_SELECTIONS];
-  __shared__ int32_t stage_pod[kMultiBatch];
   const int32_t n = blockIdx.x * kTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
@@ -275,24 +273,20 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
   int32_t i0, i1;
   list_share(&counts[1], &i0, &i1);
-  for (int32_t b0 = i0; b0 < i1; b0 += kMultiBatch) {
-    const int32_t nb = min(kMultiBatch, i1 - b0);
-    constexpr int kWords = (int)(sizeof(GasSel) / 16) * PAS_GAS_MAX_SELECTIONS;
-    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * PAS_GAS_MAX_SELECTIONS);
-    int4* dst = reinterpret_cast<int4*>(&stage[0][0]);
-    for (int32_t i = threadIdx.x; i < nb * kWords; i += kTpb) dst[i] = src[i];
-    if (threadIdx.x < nb) stage_pod[threadIdx.x] = multi[b0 + threadIdx.x];
-    __syncthreads();
-    for (int32_t j = 0; j < nb; ++j) {
-      const int32_t pw = __builtin_amdgcn_readfirstlane(stage_pod[j]);
+  // pod words and selection records are wave-uniform: scalar loads straight into SGPRs (a
+  // selection used to cost a dozen readfirstlanes from an LDS stage)
+  {
+    for (int32_t i = i0; i < i1; ++i) {
+      const GasSel* stage_j = sels + (int64_t)i * PAS_GAS_MAX_SELECTIONS;
+      const int32_t pw = multi[i];
       const int64_t p = pw & 0xFFFFFF;
       const int32_t steps = pw >> 24;
       uint32_t out = 0u;
       if (steps == 2) {
         // two selections without touching free: the second one sees card c0 with the
         // first take added to its need, every other card as it was
-        const GasSel& e0 = stage[j][0];
-        const GasSel& e1 = stage[j][1];
+        const GasSel& e0 = stage_j[0];
+        const GasSel& e1 = stage_j[1];
         int64_t cmp0[Q], cmp1[Q], cmp1t[Q];
         bool ovf = false;  // need1 + take0 beyond int64: card c0 cannot take the second
 #pragma unroll
@@ -338,7 +332,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
         bool fits = true;
         uint32_t word = 0;
         for (int32_t t = 0; t < steps; ++t) {
-          const GasSel& e = stage[j][t];  // broadcast LDS reads, then SGPRs
+          const GasSel& e = stage_j[t];
           int64_t cmp[Q], take[Q];
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
@@ -363,7 +357,6 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
       }
       put_result<kBits>(res, fit, p, N, n, valid, out);
     }
-    __syncthreads();  // the next batch rewrites the stage
   }
 }
 
