@@ -16,12 +16,22 @@
 // means need > INT64_MAX - used >= free.  Taking a card (addRM) is free -= need.  A
 // negative need on a requested kind fails every card (:343-347).
 //
-// The pod loop is wave-uniform: pod records are staged in LDS per batch and read into
-// SGPRs, so each card check is one 64-bit compare against an SGPR.  The prep kernel splits
-// the batch: pods with at most one card selection (the common case: one container, one
-// i915) go to a kernel that only reads free; pods with several selections go to a kernel
-// that takes cards in place (per-card lane-masked updates) and undoes them afterwards, so
-// the first kernel keeps a small register footprint.
+// The pod loop is wave-uniform: pod records sit in SGPRs, so each card check is one 64-bit
+// compare against an SGPR.  The prep kernel splits the batch: pods with at most one card
+// selection (the common case: one container, one i915) go to a kernel that only reads free;
+// pods with several selections go to a kernel that takes cards in a working copy
+// (per-card lane-masked updates), so the first kernel keeps a small register footprint.
+//
+// Kind skipping (exact, decided per pod before the fit kernels): gmin[q] = the minimum of
+// free[k][q] over every card of every labelled node of the snapshot (gas_minfree_kernel).
+// When a single-selection pod's need of kind q is <= gmin[q], no check of kind q can fail
+// anywhere, so its compares are dropped: the prep kernel files the pod under list 1 + q (the
+// lowest such kind) or list 0, and the single kernel instantiates one body per list, so the
+// skip costs nothing per (pod, node).  The last kind the selection requests stays compared,
+// so cards a node does not have (free -1 everywhere) still fail.  In the C3 mix the i915
+// kind (1 per selection against >= 30 free) goes: single kernel 502 -> 381 us.  The same
+// for multi-selection pods (bound = need plus the takes before it) measured 1587 -> 1609 us,
+// so that kernel keeps every kind: it is not bound by its compares.
 #include <hip/hip_runtime.h>
 
 #include "pas_internal.h"
@@ -41,7 +51,8 @@ struct alignas(16) GasStep {
   int64_t take[PAS_GAS_MAX_RES];
   int32_t num_i915;  // getNumI915 (:192-198); 0 = no selection (skipped, :206-208, :215)
   int32_t bad;       // a requested kind has a negative per-GPU need (:343-347)
-  int32_t pad[2];
+  int32_t kinds;     // bit q: kind q requested
+  int32_t pad;
 };
 
 // One card selection of a pod with several: compare and take vectors (kinds as GasStep).
@@ -51,7 +62,6 @@ struct alignas(16) GasSel {
   int32_t bad;
   int32_t pad[3];
 };
-constexpr int kMultiBatch = 8;  // multi-selection pods staged in LDS per round
 
 // Pod with at most one card selection: its selecting step, or steps == 0.
 struct alignas(16) GasSingle {
@@ -75,6 +85,7 @@ __device__ GasStep container_step(int64_t i, int32_t n_res, int32_t i915,
   }
   GasStep g = {};
   g.num_i915 = m != 0u ? (int32_t)min(ni, (int64_t)PAS_GAS_MAX_SELECTIONS + 1) : 0;
+  g.kinds = (int32_t)(m & ((1u << n_res) - 1u));
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
     const bool has = q < n_res && ((m >> q) & 1u);
@@ -87,14 +98,51 @@ __device__ GasStep container_step(int64_t i, int32_t n_res, int32_t i915,
   return g;
 }
 
-// One thread per pod files it under `single` (<= 1 selection: its selecting step) or
-// `multi` (several: its steps, containers in order then gpuNum, expanded into its slot of
-// the selection list; more than PAS_GAS_MAX_SELECTIONS are beyond the packed result and
-// keep only the count).
+// The list a single-selection pod is filed under: 1 + q for the lowest kind q whose need is
+// within gmin[q] (every real card of every node has that much free, so the compare always
+// holds), else 0.  The last kind the selection requests is kept: cards a node does not have
+// read free = -1 and must keep failing.  A bad selection fails in any list.
+__device__ __forceinline__ int32_t skip_list(int32_t n_res, const int64_t (&cmp)[PAS_GAS_MAX_RES],
+                                             uint32_t kinds,
+                                             const unsigned long long* __restrict__ gflip) {
+  for (int q = 0; q < n_res; ++q) {
+    if (!((kinds >> q) & 1u) || kinds == (1u << q)) continue;
+    const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
+    if (cmp[q] <= gmin) return 1 + q;
+  }
+  return 0;
+}
+
+// A slot in list `list` for each active lane: one atomic per distinct list in the wave (lanes
+// of different lists hit different counters, which the compiler would leave one per lane).
+__device__ __forceinline__ int32_t wave_slot(int32_t* __restrict__ counts, int32_t list) {
+  unsigned long long todo = __ballot(1);
+  int32_t slot = 0;
+  while (todo) {
+    const int leader = __builtin_ctzll(todo);
+    const int32_t l = __shfl(list, leader, 64);
+    const unsigned long long m = __ballot(list == l);
+    int32_t base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(&counts[l], __popcll(m));
+    base = __shfl(base, leader, 64);
+    if (list == l)
+      slot = base + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    todo &= ~m;
+  }
+  return slot;
+}
+
+// One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
+// list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: its steps,
+// containers in order then gpuNum, into its row of `sels`; more than PAS_GAS_MAX_SELECTIONS
+// are beyond the packed result and keep only the count).  counts: [n_res + 1] single lists,
+// then the multi list.
 __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
                                 int32_t i915, const int64_t* __restrict__ req,
                                 const uint32_t* __restrict__ mask,
                                 const int32_t* __restrict__ n_containers,
+                                const unsigned long long* __restrict__ gflip,
                                 GasSingle* __restrict__ single, int32_t* __restrict__ multi,
                                 GasSel* __restrict__ sels, int32_t* __restrict__ counts) {
   const int32_t p = blockIdx.x * kTpb + threadIdx.x;
@@ -102,6 +150,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   const int32_t nc = min(max(n_containers[p], 0), max_containers);
   const int64_t row = (int64_t)p * max_containers;
   int32_t steps = 0;
+  uint32_t kinds = 0;
   GasSingle one = {};
   one.pod = p;
   for (int32_t c = 0; c < nc; ++c) {
@@ -111,16 +160,19 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
 #pragma unroll
         for (int q = 0; q < PAS_GAS_MAX_RES; ++q) one.cmp[q] = g.cmp[q];
         one.bad = g.bad;
+        kinds = g.kinds;
       }
       steps = min(steps + g.num_i915, PAS_GAS_MAX_SELECTIONS + 1);
     }
   }
-  if (steps <= 1) {
+  const bool one_sel = steps <= 1;
+  const int32_t l = steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0;
+  const int32_t slot = wave_slot(counts, one_sel ? l : n_res + 1);
+  if (one_sel) {
     one.steps = steps;
-    single[atomicAdd(&counts[0], 1)] = one;
+    single[(int64_t)l * n_pods + slot] = one;
     return;
   }
-  const int32_t slot = atomicAdd(&counts[1], 1);
   multi[slot] = p | (steps << 24);
   if (steps > PAS_GAS_MAX_SELECTIONS) return;
   GasSel* out = sels + (int64_t)slot * PAS_GAS_MAX_SELECTIONS;
@@ -137,6 +189,40 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
       e.bad = g.bad;
       out[k] = e;
     }
+  }
+}
+
+// gflip[q] = INT64_MAX - gmin[q] (kept flipped so that a zeroed buffer is the identity of the
+// unsigned atomicMax): per node the minimum free over its cards, per workgroup the minimum
+// over its nodes, one atomic per workgroup and kind.  Nodes without the cards label or not in
+// the lister never fit, so they do not count.
+__global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K, int32_t n_res,
+                                                           const int32_t* __restrict__ n_cards,
+                                                           const int64_t* __restrict__ cap,
+                                                           const int64_t* __restrict__ used,
+                                                           unsigned long long* __restrict__ gflip) {
+  __shared__ int64_t red[kTpb / 64][PAS_GAS_MAX_RES];
+  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+  const int32_t nc = n < N ? min(n_cards[n], K) : 0;
+  for (int q = 0; q < n_res; ++q) {
+    int64_t m = INT64_MAX;
+    const int64_t c = nc > 0 ? cap[(int64_t)n * n_res + q] : 0;
+    for (int k = 0; k < nc; ++k) {
+      const int64_t u = used[((int64_t)n * K + k) * n_res + q];
+      const int64_t f = (c > 0 && u >= 0) ? c - u : -1;
+      m = f < m ? f : m;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const int64_t o = __shfl_xor(m, off, 64);
+      m = o < m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][q] = m;
+  }
+  __syncthreads();
+  if (threadIdx.x < n_res) {
+    int64_t m = INT64_MAX;
+    for (int w = 0; w < kTpb / 64; ++w) m = red[w][threadIdx.x] < m ? red[w][threadIdx.x] : m;
+    atomicMax(&gflip[threadIdx.x], (unsigned long long)INT64_MAX - (unsigned long long)m);
   }
 }
 
@@ -163,7 +249,7 @@ typedef unsigned long long lane_mask;  // one bit per lane of the wave (ballot)
 
 // First card (lexicographic rank) passing checkResourceCapacity, or -1: cmp[q] <= free[k][q]
 // for every kind (cmp is INT64_MIN for kinds the container does not request).
-template <int Q>
+template <int Q, int SKIP>
 __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
                                          const int64_t (&cmp)[Q]) {
   int chosen = -1;
@@ -171,7 +257,8 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
   for (int k = kMaxCards - 1; k >= 0; --k) {  // first fit = lowest k
     bool ok = true;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) ok = ok && cmp[q] <= free[k][q];
+    for (int q = 0; q < Q; ++q)
+      if (q != SKIP) ok = ok && cmp[q] <= free[k][q];
     chosen = ok ? k : chosen;
   }
   return chosen;
@@ -215,22 +302,17 @@ __device__ __forceinline__ void list_share(const int32_t* count, int32_t* b, int
   *e = min(cnt, *b + per);
 }
 
-// Pods with at most one selection: a read-only first fit per (pod, node lane).
-template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
-    int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
-    const int64_t* __restrict__ used, const GasSingle* __restrict__ single,
-    const int32_t* __restrict__ counts, uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
-  __shared__ GasSingle stage[kPodBatch];
-  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
-  int64_t free[kMaxCards][Q];
-  load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
-  // FetchNode error / missing cards label -> errWontFit before any container (:282-298)
-  const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
+// Pods with at most one selection, list `l` (kind SKIP = l - 1 dropped): a read-only first
+// fit per (pod, node lane), pod records staged in LDS per batch and read into SGPRs.
+template <int Q, int SKIP, bool kBits>
+__device__ __forceinline__ void single_list(const int64_t (&free)[kMaxCards][Q],
+                                            uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                            const GasSingle* __restrict__ single,
+                                            const int32_t* __restrict__ count, GasSingle* stage,
+                                            uint32_t* __restrict__ res,
+                                            uint64_t* __restrict__ fit) {
   int32_t i0, i1;
-  list_share(&counts[0], &i0, &i1);
+  list_share(count, &i0, &i1);
   for (int32_t b0 = i0; b0 < i1; b0 += kPodBatch) {
     const int32_t nb = min(kPodBatch, i1 - b0);
     constexpr int kWords = (int)(sizeof(GasSingle) / 16);
@@ -245,8 +327,9 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
       if (__builtin_amdgcn_readfirstlane(r.steps) == 1) {
         int64_t cmp[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) cmp[q] = uniform64(r.cmp[q]);
-        const int k = __builtin_amdgcn_readfirstlane(r.bad) ? -1 : first_fit<Q>(free, cmp);
+        for (int q = 0; q < Q; ++q) cmp[q] = q == SKIP ? 0 : uniform64(r.cmp[q]);
+        const int k =
+            __builtin_amdgcn_readfirstlane(r.bad) ? -1 : first_fit<Q, SKIP>(free, cmp);
         out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
       }
       put_result<kBits>(res, fit, pod, N, n, valid, out);
@@ -255,10 +338,43 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
   }
 }
 
+template <int Q, bool kBits, int L = 0>
+__device__ __forceinline__ void single_lists(const int64_t (&free)[kMaxCards][Q],
+                                             uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                             int32_t P, const GasSingle* __restrict__ single,
+                                             const int32_t* __restrict__ counts,
+                                             GasSingle* stage, uint32_t* __restrict__ res,
+                                             uint64_t* __restrict__ fit) {
+  single_list<Q, L - 1, kBits>(free, node_ok, N, n, valid, single + (int64_t)L * P, counts + L,
+                               stage, res, fit);
+  if constexpr (L < Q)
+    single_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, single, counts, stage, res,
+                                  fit);
+}
+
+template <int Q, bool kBits>
+__global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
+    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
+    const GasSingle* __restrict__ single, const int32_t* __restrict__ counts,
+    uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
+  __shared__ GasSingle stage[kPodBatch];
+  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  int64_t free[kMaxCards][Q];
+  load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
+  // FetchNode error / missing cards label -> errWontFit before any container (:282-298)
+  const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
+  single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage, res, fit);
+}
+
 // Pods with several selections: the steps in order (containers, then gpuNum), each taking
 // the first fitting card (free drops by the need for the following steps).  Two
 // selections need no state (the second sees the first take added to card c0's need);
-// more work on a copy of free.  Pod step lists are staged in LDS per batch.
+// more work on a copy of free.  One list: dropping a kind from the compares does not pay
+// here (measured: 1711 us with or without it for C3; the multi-selection pods are not bound
+// by their compares).
 template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
@@ -272,7 +388,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
   const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
   int32_t i0, i1;
-  list_share(&counts[1], &i0, &i1);
+  list_share(counts, &i0, &i1);
   // pod words and selection records are wave-uniform: scalar loads straight into SGPRs (a
   // selection used to cost a dozen readfirstlanes from an LDS stage)
   {
@@ -296,7 +412,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
           // INT64_MIN + 0 stays unrequested
           ovf |= __builtin_add_overflow(cmp1[q], uniform64(e0.take[q]), &cmp1t[q]);
         }
-        const int c0 = __builtin_amdgcn_readfirstlane(e0.bad) ? -1 : first_fit<Q>(free, cmp0);
+        const int c0 = __builtin_amdgcn_readfirstlane(e0.bad) ? -1 : first_fit<Q, -1>(free, cmp0);
         int c1 = -1;
         if (!__builtin_amdgcn_readfirstlane(e1.bad)) {
           // card k fits the second selection: cmp1 <= free (k != c0) or cmp1t <= free
@@ -339,7 +455,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
             cmp[q] = uniform64(e.cmp[q]);
             take[q] = uniform64(e.take[q]);
           }
-          const int k = __builtin_amdgcn_readfirstlane(e.bad) ? -1 : first_fit<Q>(w, cmp);
+          const int k = __builtin_amdgcn_readfirstlane(e.bad) ? -1 : first_fit<Q, -1>(w, cmp);
           fits = fits && k >= 0;
           // per card taken by some lane of the wave (uniform branch), a per-lane select: a
           // divergent branch around the update would make the compiler copy the array
@@ -369,14 +485,17 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
   if (N == 0 || n_pods == 0) return PAS_OK;
-  // scratch: single-selection records | multi-selection pod words | their selection lists
-  // | 2 counts
+  // scratch: single-selection records [Q+1][P] | multi-selection pod words [P] | their
+  // selection rows [P][8] | the flipped kind minima [4] and counts [Q+2] (zeroed together)
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
-  const size_t b_single = (sizeof(GasSingle) * (size_t)n_pods + 255) & ~size_t(255);
+  const int32_t NL = Q + 1;
+  const size_t b_single = (sizeof(GasSingle) * (size_t)NL * n_pods + 255) & ~size_t(255);
   const size_t b_multi = (sizeof(int32_t) * (size_t)n_pods + 255) & ~size_t(255);
   const size_t b_sels =
       (sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS * (size_t)n_pods + 255) & ~size_t(255);
-  const size_t need = b_single + b_multi + b_sels + 256;
+  constexpr size_t b_tail = (PAS_GAS_MAX_RES + 2) * sizeof(int32_t) +
+                            PAS_GAS_MAX_RES * sizeof(unsigned long long);
+  const size_t need = b_single + b_multi + b_sels + b_tail;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -391,29 +510,33 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   GasSingle* single = reinterpret_cast<GasSingle*>(base);
   int32_t* multi = reinterpret_cast<int32_t*>(base + b_single);
   GasSel* sels = reinterpret_cast<GasSel*>(base + b_single + b_multi);
-  int32_t* counts = reinterpret_cast<int32_t*>(base + b_single + b_multi + b_sels);
+  unsigned long long* gflip =
+      reinterpret_cast<unsigned long long*>(base + b_single + b_multi + b_sels);
+  int32_t* counts = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
-  PAS_HIP(ctx, hipMemsetAsync(counts, 0, 2 * sizeof(int32_t), s));
+  PAS_HIP(ctx, hipMemsetAsync(gflip, 0, b_tail, s));
+  gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
+                                                           gflip);
   gas_prep_kernel<<<(n_pods + kTpb - 1) / kTpb, kTpb, 0, s>>>(
-      n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, single, multi,
-      sels, counts);
+      n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
+      multi, sels, counts);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   // grids: node blocks x pod chunks, ~4096 blocks for the whole batch; each kernel splits
-  // its device-counted list evenly over its chunks
+  // each of its device-counted lists evenly over its chunks
   const int32_t node_blocks = (N + kTpb - 1) / kTpb;
   const int32_t chunks = std::max(1, std::min(n_pods, (4096 + node_blocks - 1) / node_blocks));
   const dim3 grid((unsigned)node_blocks, (unsigned)chunks);
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
   switch (Q * 2 + (bits ? 1 : 0)) {
-#define PAS_GAS_CASE(QQ, B)                                                                     \
-  case QQ * 2 + B:                                                                              \
-    gas_fit_single_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, single, \
-                                                       counts, d_res, d_fit);                   \
+#define PAS_GAS_CASE(QQ, B)                                                                    \
+  case QQ * 2 + B:                                                                             \
+    gas_fit_single_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, n_pods, g.n_cards, g.cap, g.used, \
+                                                       single, counts, d_res, d_fit);          \
     gas_fit_multi_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, multi,   \
-                                                      sels, counts, d_res, d_fit);              \
+                                                      sels, counts + NL, d_res, d_fit);        \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)

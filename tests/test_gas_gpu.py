@@ -157,3 +157,34 @@ def test_extreme_multi_selection_fuzz(ctx, oracle, seed):
     want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
     got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("q", [2, 3, 4])
+def test_kind_skip_lists(ctx, oracle, q):
+    # a roomy cluster: every real card has >= 500 free of kinds 1.., so pods whose needs (plus
+    # their earlier takes) stay within that minimum are filed under a kind-skipping list; the
+    # boundary (== and == + 1 of the minimum), pods requesting a single kind (which must keep
+    # failing on missing cards), nodes with fewer cards than K and nodes without the label
+    rng = np.random.default_rng(40 + q)
+    n, k, p, c = 500, 4, 96, 3
+    n_cards = rng.integers(-1, k + 1, size=n).astype(np.int32)
+    cap = np.full((n, q), 2000, np.int64)
+    cap[:, 0] = 4
+    used = rng.integers(0, 1500, size=(n, k, q)).astype(np.int64)
+    used[:, :, 0] = rng.integers(0, 5, size=(n, k))
+    used[n_cards <= 0] = 1999  # unlabelled nodes do not lower the minimum
+    real = np.arange(k)[None, :] < np.maximum(n_cards, 0)[:, None]
+    gmin = [(cap[:, None, j] - used[:, :, j])[real].min() for j in range(q)]
+    req = rng.integers(0, 40, size=(p, c, q)).astype(np.int64)
+    req[:, :, 0] = rng.integers(0, 3, size=(p, c))
+    for pi in range(0, p, 4):  # exactly at / one beyond the minimum of kind 1 (one selection)
+        req[pi, 0, 1] = gmin[1] + (pi // 4) % 2
+    mask = rng.integers(0, 1 << q, size=(p, c)).astype(np.uint32) | 1
+    mask[::5] = 1  # only i915: nothing to skip but the last common kind
+    mask[1::7] = 3
+    ncont = rng.integers(1, c + 1, size=p).astype(np.int32)
+    ncont[::4] = 1
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
+    np.testing.assert_array_equal(got, want)
+    assert 0.1 < (want >> 31).mean() < 0.95
