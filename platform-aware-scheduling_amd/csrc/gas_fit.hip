@@ -369,6 +369,24 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
   single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage, res, fit);
 }
 
+// The compare / take fields of one selection record, kinds [0, Q) (scalar loads).
+struct SelHead {
+  int64_t cmp[PAS_GAS_MAX_RES];
+  int64_t take[PAS_GAS_MAX_RES];
+  int32_t bad;
+};
+template <int Q>
+__device__ __forceinline__ SelHead sel_head(const GasSel* e) {
+  SelHead h = {};
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    h.cmp[q] = e->cmp[q];
+    h.take[q] = e->take[q];
+  }
+  h.bad = e->bad;
+  return h;
+}
+
 // Pods with several selections: the steps in order (containers, then gpuNum), each taking
 // the first fitting card (free drops by the need for the following steps).  Two
 // selections need no state (the second sees the first take added to card c0's need);
@@ -391,18 +409,31 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   list_share(counts, &i0, &i1);
   // pod words and selection records are wave-uniform: scalar loads straight into SGPRs (a
   // selection used to cost a dozen readfirstlanes from an LDS stage)
+  // The next pod's word and first two selections are loaded one iteration ahead: otherwise
+  // every pod waits on two scalar-load round trips before its first compare.
   {
+    SelHead nh = {}, nh1 = {};
+    int32_t npw = 0;
+    if (i0 < i1) {
+      npw = multi[i0];
+      nh = sel_head<Q>(sels + (int64_t)i0 * PAS_GAS_MAX_SELECTIONS);
+      nh1 = sel_head<Q>(sels + (int64_t)i0 * PAS_GAS_MAX_SELECTIONS + 1);
+    }
     for (int32_t i = i0; i < i1; ++i) {
       const GasSel* stage_j = sels + (int64_t)i * PAS_GAS_MAX_SELECTIONS;
-      const int32_t pw = multi[i];
+      const int32_t pw = npw;
+      const SelHead e0 = nh, e1 = nh1;
+      if (i + 1 < i1) {
+        npw = multi[i + 1];
+        nh = sel_head<Q>(stage_j + PAS_GAS_MAX_SELECTIONS);
+        nh1 = sel_head<Q>(stage_j + PAS_GAS_MAX_SELECTIONS + 1);
+      }
       const int64_t p = pw & 0xFFFFFF;
       const int32_t steps = pw >> 24;
       uint32_t out = 0u;
       if (steps == 2) {
         // two selections without touching free: the second one sees card c0 with the
         // first take added to its need, every other card as it was
-        const GasSel& e0 = stage_j[0];
-        const GasSel& e1 = stage_j[1];
         int64_t cmp0[Q], cmp1[Q], cmp1t[Q];
         bool ovf = false;  // need1 + take0 beyond int64: card c0 cannot take the second
 #pragma unroll
@@ -447,8 +478,11 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
           for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
         bool fits = true;
         uint32_t word = 0;
+        // the next step's record is loaded before the current step's compares (slot
+        // min(t + 1, 7) of the row is always in bounds)
+        SelHead e = e0;
         for (int32_t t = 0; t < steps; ++t) {
-          const GasSel& e = stage_j[t];
+          const SelHead en = sel_head<Q>(stage_j + min(t + 1, PAS_GAS_MAX_SELECTIONS - 1));
           int64_t cmp[Q], take[Q];
 #pragma unroll
           for (int q = 0; q < Q; ++q) {
@@ -468,6 +502,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
 #pragma unroll
               for (int q = 0; q < Q; ++q) w[kk][q] -= k == kk ? tv[q] : 0;
           word |= (uint32_t)(k & 7) << (3 * t);
+          e = en;
         }
         out = fits ? (node_ok | ((uint32_t)steps << 24) | word) : 0u;
       }
