@@ -20,7 +20,8 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles")
 TAS_PATH = ("tas_prep_kernel", "tas_eval_kernel")
-GAS_PATH = ("gas_prep_kernel", "gas_fit_single_kernel", "gas_fit_multi_kernel")
+GAS_PATH = ("gas_minfree_kernel", "gas_prep_kernel", "gas_fit_single_kernel",
+            "gas_fit_multi_kernel")
 
 
 def short(name):
