@@ -258,8 +258,8 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
     bool ok = true;
 #pragma unroll
     for (int q = 0; q < Q; ++q)
-      if (q != SKIP) ok = ok && cmp[q] <= free[k][q];
-    chosen = ok ? k : chosen;
+      if (q != SKIP) ok &= cmp[q] <= free[k][q];  // lane masks and-ed in SALU
+    chosen = ok ? k : chosen;                    // one select per card
   }
   return chosen;
 }

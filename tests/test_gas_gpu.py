@@ -188,3 +188,26 @@ def test_kind_skip_lists(ctx, oracle, q):
     got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
     np.testing.assert_array_equal(got, want)
     assert 0.1 < (want >> 31).mean() < 0.95
+
+
+@pytest.mark.parametrize("cap_max", [2**31 - 2, 2**31 - 1])
+def test_narrow_kind_boundary(ctx, oracle, cap_max):
+    # kinds whose cap stays <= INT32_MAX - 1 on every node compare in 32 bits (needs clamped):
+    # needs around INT32_MAX and beyond, over-committed cards (used > cap: free < -1), negative
+    # usage, and the first value that keeps the kind 64-bit; one and several selections
+    rng = np.random.default_rng(cap_max & 0xFF)
+    n, k, q, p, c = 300, 4, 3, 64, 3
+    n_cards = rng.integers(0, k + 1, size=n).astype(np.int32)
+    cap = rng.choice(np.array([1, 1000, cap_max - 5, cap_max], np.int64), size=(n, q))
+    cap[:, 2] = 2**40  # one kind always 64-bit
+    used = rng.choice(np.array([0, 1, 999, cap_max - 6, cap_max, 2**31 + 7, 2**40, -3], np.int64),
+                      size=(n, k, q))
+    req = rng.choice(np.array([0, 1, 5, cap_max - 6, cap_max - 1, 2**31 - 1, 2**31, 2**33],
+                              np.int64), size=(p, c, q))
+    req[:, :, 0] = rng.integers(1, 3, size=(p, c))  # i915 selections per container
+    mask = rng.integers(0, 1 << q, size=(p, c)).astype(np.uint32) | 1
+    ncont = rng.integers(1, c + 1, size=p).astype(np.int32)
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
+    np.testing.assert_array_equal(got, want)
+    assert 0.02 < (want >> 31).mean() < 0.98
