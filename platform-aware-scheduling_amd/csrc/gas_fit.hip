@@ -454,7 +454,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
               bool ok = true;
 #pragma unroll
               for (int q = 0; q < Q; ++q)
-                ok = ok && (c0 == k ? cmp1t[q] : cmp1[q]) <= free[k][q];
+                ok &= (c0 == k ? cmp1t[q] : cmp1[q]) <= free[k][q];
               c1 = ok ? k : c1;
             }
           } else {
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
             for (int k = kMaxCards - 1; k >= 0; --k) {
               bool ok = c0 != k;
 #pragma unroll
-              for (int q = 0; q < Q; ++q) ok = ok && cmp1[q] <= free[k][q];
+              for (int q = 0; q < Q; ++q) ok &= cmp1[q] <= free[k][q];
               c1 = ok ? k : c1;
             }
           }
