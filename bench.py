@@ -26,12 +26,31 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
 
-import pas_amd  # noqa: E402
-from pas_amd import _lib  # noqa: E402
-from pas_amd import distrib  # noqa: E402
-from pas_amd import shard  # noqa: E402
-from pas_amd.distrib import timed_steps, whole_job_rate  # noqa: E402
-from pas_amd import workload as wl  # noqa: E402
+
+def _load_distrib():
+    """pas_amd/distrib.py by path: importing the package would load libpas.so, and the parent
+    that launches one child per GPU must not touch HIP at all."""
+    import importlib.util
+    path = os.path.join(ROOT, "platform-aware-scheduling_amd", "pas_amd", "distrib.py")
+    spec = importlib.util.spec_from_file_location("pas_amd_distrib_bench", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+distrib = _load_distrib()
+timed_steps, whole_job_rate = distrib.timed_steps, distrib.whole_job_rate
+
+# libpas.so and the modules that load it are imported in main(), after the decision to
+# launch one child process per GPU: the launching parent must not initialise HIP.
+pas_amd = _lib = shard = wl = None
+
+
+def _load_package():
+    global pas_amd, _lib, shard, wl
+    import pas_amd as _p
+    from pas_amd import _lib as _l, shard as _s, workload as _w
+    pas_amd, _lib, shard, wl = _p, _l, _s, _w
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "pod-node evals/sec (filter+prioritize), 4k pods×100k nodes; % of HBM peak"
@@ -330,7 +349,7 @@ def bench_deschedule(args, world, rank):
     def step():
         ctx.tas_violations_device(1, S, len(rules), rules_t, off_t, viol_t, stream)
         ctx.tas_label_plan_device(n_local, S, viol_t, labels_t, add_t, rem_t, total_t, stream)
-        gathered["v"] = shard.gather_violations(viol_t, world)
+        gathered["v"] = shard.gather_violations(viol_t, world, N)
 
     for _ in range(args.warmup):
         step()
@@ -426,12 +445,28 @@ def bench_c5(args, world, rank):
     return out
 
 
+def bench_launch_check(args, world, rank):
+    """Self-launch check (tests/test_bench_launch.py): the ranks bench.py started join a
+    gloo group and time empty steps with the same barrier / max-over-ranks protocol."""
+    elapsed = timed_steps(lambda: None, args.steps, args.warmup, world,
+                          sync=lambda: None)
+    import torch.distributed as dist
+    return {"metric": "launch check", "value": float(world), "unit": "ranks", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / max(args.steps, 1) * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "none",
+            "data": "none", "config": {"workload": "launch_check", "world_size":
+                                       dist.get_world_size() if world > 1 else 1,
+                                       "backend": dist.get_backend() if world > 1 else None,
+                                       "rank0_pid": os.getpid()}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["tas", "gas", "deschedule", "c5"], default="tas")
+    ap.add_argument("--workload", choices=["tas", "gas", "deschedule", "c5", "launch_check"],
+                    default="tas")
     ap.add_argument("--pods", type=int, default=None)
     ap.add_argument("--nodes", type=int, default=None)
     ap.add_argument("--metrics", type=int, default=64)
@@ -440,15 +475,33 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        # no launcher: start one child per GPU (fresh processes, nothing initialised here)
+        sys.exit(distrib.launch_local_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)]
+                                            + sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        ap.error(f"--gpus {args.gpus} disagrees with WORLD_SIZE={env_world} from the launcher")
     defaults = {"tas": (4096, 100_000), "gas": (10_000, 50_000), "deschedule": (0, 1_000_000),
-                "c5": (65_536, 1_000_000)}
+                "c5": (65_536, 1_000_000), "launch_check": (0, 0)}
     dp, dn = defaults[args.workload]
     args.pods = args.pods or dp
     args.nodes = args.nodes or dn
-    world, rank, _ = distrib.setup()
-    fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule,
-          "c5": bench_c5}[args.workload]
-    out = fn(args, world, rank)
+    if args.workload == "launch_check":
+        world, rank, _ = distrib.setup("gloo")
+        out = bench_launch_check(args, world, rank)
+    else:
+        _load_package()
+        world, rank, _ = distrib.setup()
+        fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule,
+              "c5": bench_c5}[args.workload]
+        out = fn(args, world, rank)
+        if world > 1:
+            import torch.distributed as dist
+            out["config"]["world_size"] = dist.get_world_size()
+            out["config"]["backend"] = dist.get_backend()
     if rank == 0:
         print(json.dumps(out), flush=True)
     distrib.teardown(world)

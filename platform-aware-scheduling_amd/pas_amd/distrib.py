@@ -95,3 +95,38 @@ def whole_job_rate(units_per_rank_per_step, world, steps, elapsed_s):
 def batch_seed(base, rank):
     """Seed of rank `rank`'s independent pod batch (weak scaling: same size per rank)."""
     return base + 7919 * rank
+
+
+def launch_local_ranks(n, argv, master_port=None):
+    """Start `argv` as n local ranks (RANK = LOCAL_RANK = r, WORLD_SIZE = n, rendezvous on
+    127.0.0.1) the way torchrun would, wait for all of them and return the first non-zero
+    exit status (0 if every rank succeeded).  The caller must not have initialised HIP:
+    the children are fresh processes (no fork of a GPU context, no exec of this one)."""
+    import signal
+    import socket
+    import subprocess
+    if master_port is None:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            master_port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ)
+        env.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master_port))
+        procs.append(subprocess.Popen(argv, env=env))
+    rc = 0
+    pending = list(procs)
+    while pending:
+        for p in list(pending):
+            code = p.poll()
+            if code is None:
+                continue
+            pending.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in pending:  # one rank failed: the others would block in a collective
+                    q.send_signal(signal.SIGTERM)
+        if pending:
+            time.sleep(0.05)
+    return rc if rc >= 0 else 128 - rc

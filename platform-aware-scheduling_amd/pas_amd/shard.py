@@ -71,14 +71,25 @@ class ShardedTopK:
 
     def run(self, gen: int, n_pods: int, n_rules: int, rules_t, rule_off_t, prio_t, cand_t=None,
             stream=None):
+        """`stream`: the torch.cuda.Stream the kernels run on (None = torch's current stream).
+        The collectives run on torch's current stream, so the two are ordered with
+        wait_stream in both directions when they differ."""
         k = self.k
+        on_gpu = torch.cuda.is_available() and str(self.device).startswith("cuda")
+        cur = torch.cuda.current_stream() if on_gpu else None
+        if stream is None:
+            stream = cur
         key = self._buf("key", (n_pods, k), torch.int64)
         node = self._buf("node", (n_pods, k), torch.int32)
         ln = self._buf("len", (n_pods,), torch.int32)
         self.ctx.tas_topk_device(gen, n_pods, n_rules, rules_t, rule_off_t, prio_t, cand_t, k,
                                  self.node_base, key, node, ln, stream)
+        if on_gpu and stream != cur:
+            cur.wait_stream(stream)  # records written before the all-gather reads them
         keys_all = _all_gather(key, self.world)
         nodes_all = _all_gather(node, self.world)
+        if on_gpu and stream != cur:
+            stream.wait_stream(cur)  # gathered records complete before the merge reads them
         out_node = self._buf("out_node", (n_pods, k), torch.int32)
         out_len = self._buf("out_len", (n_pods,), torch.int32)
         self.ctx.topk_merge_device(n_pods, k, self.world, keys_all, nodes_all, out_node, out_len,
@@ -86,21 +97,22 @@ class ShardedTopK:
         return out_node, out_len
 
 
-def gather_violations(viol_local: torch.Tensor, world: int) -> torch.Tensor:
-    """Cluster violation bitmaps [S][W64_total] from every rank's [S][W64_shard] sweep
-    (shards from node_range: equal word counts except a shorter last shard, which is
-    padded here for the collective and trimmed by the caller's W64_total)."""
+def gather_violations(viol_local: torch.Tensor, world: int, n_total: int) -> torch.Tensor:
+    """Cluster violation bitmaps [S][W64(n_total)] from every rank's [S][W64_shard] sweep.
+
+    Shard widths are static (node_range over n_total): every shard but the last has the
+    same word count wmax, the last is padded to wmax for the collective, and the
+    concatenation is trimmed to W64(n_total).  No size exchange runs per step."""
     s, w = viol_local.shape
     if world == 1:
         return viol_local
-    import torch.distributed as dist
-    wmax = torch.tensor([w], dtype=torch.int64,
-                        device=viol_local.device if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(wmax, op=dist.ReduceOp.MAX)
-    wmax = int(wmax.item())
+    n0, n1 = node_range(n_total, world, 0)
+    wmax = (n1 - n0 + 63) // 64
+    if w > wmax:
+        raise ValueError(f"shard has {w} words, node_range gives at most {wmax}")
     padded = viol_local
     if w < wmax:
         padded = torch.zeros((s, wmax), dtype=viol_local.dtype, device=viol_local.device)
         padded[:, :w] = viol_local
     parts = _all_gather(padded, world).reshape(world, s, wmax)
-    return parts.permute(1, 0, 2).reshape(s, world * wmax)
+    return parts.permute(1, 0, 2).reshape(s, world * wmax)[:, :(n_total + 63) // 64]

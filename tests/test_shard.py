@@ -148,7 +148,7 @@ def _gloo_worker(rank, world, port, out_dir):
     drules, doff = wl.make_deschedule_rules(snap, 4, 3, seed=0xC4)
     sv, sp = shard_snapshot(v, pres, n0, n1)
     viol = oracle.tas_violations(sv, sp, drules, doff)
-    full = gather_violations(torch.from_numpy(viol.view(np.int64)), world).numpy()
+    full = gather_violations(torch.from_numpy(viol.view(np.int64)), world, n).numpy()
     padded = np.full((P, k), -1, np.int64)
     for p, lst in enumerate(merged):
         padded[p, :len(lst)] = lst
@@ -289,9 +289,12 @@ def _gpu_worker(rank, world, port, out_dir):
         rules_t, off_t, prio_t, cand_t = _rule_tensors(batch, shard_cand(batch.cand, v.shape[1],
                                                                          n0, n1))
         st = ShardedTopK(c, 12, world, rank, n0)
+        # rank 0: the kernels on a stream of their own (ordered against the collectives with
+        # wait_stream); rank 1: torch's current stream (stream=None)
+        s = torch.cuda.Stream() if rank == 0 else None
         out_node, out_len = st.run(3, len(batch.prio), len(batch.rules), rules_t, off_t, prio_t,
-                                   cand_t)
-        c.synchronize()
+                                   cand_t, stream=s)
+        torch.cuda.synchronize()
         np.save(os.path.join(out_dir, f"nodes{rank}.npy"), out_node.cpu().numpy())
         np.save(os.path.join(out_dir, f"lens{rank}.npy"), out_len.cpu().numpy())
     distrib.teardown(world)
