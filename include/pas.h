@@ -86,15 +86,23 @@ int pas_synchronize(pas_ctx* ctx);
  * Replaces the map lookup in core.EvaluateRule (operator.go:14-25). */
 int pas_parse_operator(const char* op);
 
-/* resource.Quantity string (k8s.io/apimachinery v0.22.2 grammar: sign, digits,
- * optional fraction, optional suffix n u m k M G T P E Ki Mi Gi Ti Pi Ei or
- * e/E exponent) -> exact int64 value*1000.  PAS_ENOTEXACT if the value has
- * sub-milli precision or is outside int64 milli range; PAS_EINVAL if unparsable. */
+/* resource.Quantity string -> the parsed quantity's value * 1000, exactly.  Parsing is
+ * resource.ParseQuantity of k8s.io/apimachinery v0.22.2 (sign, digits, optional fraction,
+ * suffix n u m k M G T P E Ki Mi Gi Ti Pi Ei or e/E exponent), including its inf.Dec
+ * path: values it cannot hold as int64Amount are rounded away from zero to 1e-9 and
+ * capped at +-(2^63 - 1) — the value core.EvaluateRule compares (operator.go:16-22).
+ * PAS_ENOTEXACT if that value has sub-milli precision or is outside int64 milli range;
+ * PAS_EINVAL if ParseQuantity would fail. */
 int pas_quantity_to_milli(const char* quantity, int64_t* milli_out);
 
-/* resource.Quantity.AsInt64 as the reference uses it, ignoring `ok`
- * (gpuscheduler/utils.go:23, scheduler.go:155): the integer value, or 0 when the
- * quantity is non-integral or out of int64 range.  PAS_EINVAL if unparsable. */
+/* resource.ParseQuantity(quantity).AsInt64() with `ok` ignored, as the reference uses it
+ * (gpuscheduler/utils.go:23, scheduler.go:155).  That is 0 — even for integral values —
+ * for an inf.Dec-backed quantity (19 or more significant digits, a fraction with a
+ * binary suffix, a binary suffix past the int64Amount precision estimate such as "1Pi",
+ * scale below nano) and for an int64Amount with negative scale ("1000m", "10.0");
+ * value * 10^scale (0 on overflow) otherwise.  Pass the string the informer decoded: the
+ * apiserver stores quantities in canonical form ("1000m" arrives as "1").
+ * PAS_EINVAL if ParseQuantity would fail. */
 int pas_quantity_as_int64(const char* quantity, int64_t* out);
 
 /* ------------------------------------------------------------------------- */

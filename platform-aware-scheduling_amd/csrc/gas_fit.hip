@@ -133,11 +133,24 @@ __device__ __forceinline__ int32_t wave_slot(int32_t* __restrict__ counts, int32
   return slot;
 }
 
+// The list a multi-selection pod is filed under: 1 + q for the lowest kind q that some
+// selection requests and whose compare can be dropped from every selection's scan of the
+// cards the pod has not taken from yet (untouched cards hold their snapshot free, >= gmin[q]):
+// each selection either does not request q or needs at most gmin[q] of it and requests
+// another kind too (cards a node does not have must keep failing).  Cards the pod has taken
+// from are always compared on every kind.  Else 0.
+__device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_mask,
+                                                   uint32_t req_mask) {
+  const uint32_t m = ok_mask & req_mask & ((1u << n_res) - 1u);
+  return m ? 1 + __builtin_ctz(m) : 0;
+}
+
 // One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
-// list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: its steps,
-// containers in order then gpuNum, into its row of `sels`; more than PAS_GAS_MAX_SELECTIONS
-// are beyond the packed result and keep only the count).  counts: [n_res + 1] single lists,
-// then the multi list.
+// list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
+// [n_res + 1][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list); a multi
+// pod's selections (containers in order, then gpuNum) go to its own row sels[pod][8].  More
+// than PAS_GAS_MAX_SELECTIONS selections are beyond the packed result and keep only the
+// count.  counts: [n_res + 1] single lists, then [n_res + 1] multi lists.
 __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
                                 int32_t i915, const int64_t* __restrict__ req,
                                 const uint32_t* __restrict__ mask,
@@ -151,6 +164,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   const int64_t row = (int64_t)p * max_containers;
   int32_t steps = 0;
   uint32_t kinds = 0;
+  uint32_t skip_ok = (1u << n_res) - 1u, skip_req = 0;  // multi_skip_list
   GasSingle one = {};
   one.pod = p;
   for (int32_t c = 0; c < nc; ++c) {
@@ -163,19 +177,28 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
         kinds = g.kinds;
       }
       steps = min(steps + g.num_i915, PAS_GAS_MAX_SELECTIONS + 1);
+      const uint32_t gk = (uint32_t)g.kinds;
+      skip_req |= gk;
+      for (int q = 0; q < n_res; ++q) {
+        if (!((gk >> q) & 1u)) continue;
+        const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
+        if (g.cmp[q] > gmin || gk == (1u << q)) skip_ok &= ~(1u << q);
+      }
     }
   }
   const bool one_sel = steps <= 1;
-  const int32_t l = steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0;
-  const int32_t slot = wave_slot(counts, one_sel ? l : n_res + 1);
+  const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0)
+                            : multi_skip_list(n_res, skip_ok, skip_req);
+  const int32_t nl = n_res + 1;
+  const int32_t slot = wave_slot(counts, one_sel ? l : nl + l);
   if (one_sel) {
     one.steps = steps;
     single[(int64_t)l * n_pods + slot] = one;
     return;
   }
-  multi[slot] = p | (steps << 24);
+  multi[(int64_t)l * n_pods + slot] = p | (steps << 24);
   if (steps > PAS_GAS_MAX_SELECTIONS) return;
-  GasSel* out = sels + (int64_t)slot * PAS_GAS_MAX_SELECTIONS;
+  GasSel* out = sels + (int64_t)p * PAS_GAS_MAX_SELECTIONS;
   int32_t k = 0;
   for (int32_t c = 0; c < nc; ++c) {
     const GasStep g = container_step(row + c, n_res, i915, req, mask);
@@ -264,15 +287,6 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
   return chosen;
 }
 
-// A wave-uniform value copied into a VGPR pair, so that selects against the condition mask
-// (VCC, one scalar operand) do not re-materialise it per use.
-__device__ __forceinline__ int64_t to_vgpr64(int64_t x) {
-  uint32_t lo = (uint32_t)x, hi = (uint32_t)((uint64_t)x >> 32);
-  asm volatile("v_mov_b32 %0, %0" : "+v"(lo));
-  asm volatile("v_mov_b32 %0, %0" : "+v"(hi));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-
 __device__ __forceinline__ int64_t uniform64(int64_t x) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
@@ -294,11 +308,26 @@ __device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t*
   }
 }
 
-// This block's share [*b, *e) of a device-counted list, split evenly over gridDim.y.
-__device__ __forceinline__ void list_share(const int32_t* count, int32_t* b, int32_t* e) {
+// Blocks of the fit kernels cover (node block, pod chunk) pairs.  A 1-D grid is mapped so
+// that every chunk of a node block runs on the same XCD (block b runs on XCD b % 8,
+// MI355X_MICROARCH.md): pairs are ordered node-major and each XCD takes a contiguous run of
+// them, so a node block's snapshot rows are fetched into one L2 only.
+struct BlockTile {
+  int32_t node_block, chunk, chunks;
+};
+__device__ __forceinline__ BlockTile block_tile(int32_t chunks) {
+  const int32_t nb = gridDim.x, b = blockIdx.x;
+  const int32_t xcd = b & 7, per = nb >> 3, rem = nb & 7;
+  const int32_t pos = xcd * per + min(xcd, rem) + (b >> 3);
+  return BlockTile{pos / chunks, pos % chunks, chunks};
+}
+
+// This block's share [*b, *e) of a device-counted list, split evenly over the chunks.
+__device__ __forceinline__ void list_share(const int32_t* count, const BlockTile& bt, int32_t* b,
+                                           int32_t* e) {
   const int32_t cnt = __builtin_amdgcn_readfirstlane(*count);
-  const int32_t per = (cnt + (int32_t)gridDim.y - 1) / (int32_t)gridDim.y;
-  *b = min(cnt, (int32_t)blockIdx.y * per);
+  const int32_t per = (cnt + bt.chunks - 1) / bt.chunks;
+  *b = min(cnt, bt.chunk * per);
   *e = min(cnt, *b + per);
 }
 
@@ -309,10 +338,10 @@ __device__ __forceinline__ void single_list(const int64_t (&free)[kMaxCards][Q],
                                             uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                             const GasSingle* __restrict__ single,
                                             const int32_t* __restrict__ count, GasSingle* stage,
-                                            uint32_t* __restrict__ res,
+                                            const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
   int32_t i0, i1;
-  list_share(count, &i0, &i1);
+  list_share(count, bt, &i0, &i1);
   for (int32_t b0 = i0; b0 < i1; b0 += kPodBatch) {
     const int32_t nb = min(kPodBatch, i1 - b0);
     constexpr int kWords = (int)(sizeof(GasSingle) / 16);
@@ -343,12 +372,13 @@ __device__ __forceinline__ void single_lists(const int64_t (&free)[kMaxCards][Q]
                                              uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                              int32_t P, const GasSingle* __restrict__ single,
                                              const int32_t* __restrict__ counts,
-                                             GasSingle* stage, uint32_t* __restrict__ res,
+                                             GasSingle* stage, const BlockTile& bt,
+                                             uint32_t* __restrict__ res,
                                              uint64_t* __restrict__ fit) {
   single_list<Q, L - 1, kBits>(free, node_ok, N, n, valid, single + (int64_t)L * P, counts + L,
-                               stage, res, fit);
+                               stage, bt, res, fit);
   if constexpr (L < Q)
-    single_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, single, counts, stage, res,
+    single_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, single, counts, stage, bt, res,
                                   fit);
 }
 
@@ -356,17 +386,18 @@ template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
-    const GasSingle* __restrict__ single, const int32_t* __restrict__ counts,
+    const GasSingle* __restrict__ single, const int32_t* __restrict__ counts, int32_t chunks,
     uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
   __shared__ GasSingle stage[kPodBatch];
-  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+  const BlockTile bt = block_tile(chunks);
+  const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   int64_t free[kMaxCards][Q];
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
   // FetchNode error / missing cards label -> errWontFit before any container (:282-298)
   const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
-  single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage, res, fit);
+  single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage, bt, res, fit);
 }
 
 // The compare / take fields of one selection record, kinds [0, Q) (scalar loads).
@@ -387,128 +418,190 @@ __device__ __forceinline__ SelHead sel_head(const GasSel* e) {
   return h;
 }
 
-// Pods with several selections: the steps in order (containers, then gpuNum), each taking
-// the first fitting card (free drops by the need for the following steps).  Two
-// selections need no state (the second sees the first take added to card c0's need);
-// more work on a copy of free.  One list: dropping a kind from the compares does not pay
-// here (measured: 1711 us with or without it for C3; the multi-selection pods are not bound
-// by their compares).
+// Lane mask of a <= v (a wave-uniform, in SGPRs): the compare writes the mask directly.
+__device__ __forceinline__ uint64_t le_mask(int64_t a, int64_t v) {
+  uint64_t m;
+  asm("v_cmp_le_i64_e64 %0, %1, %2" : "=s"(m) : "s"(a), "v"(v));
+  return m;
+}
+
+// bm * 2 + (this lane's bit of `mask`): one v_addc with the lane mask as carry-in.  Cards are
+// pushed from the last to the first, so bit k of the result is card k.  `mask` must come from
+// a scalar instruction (an s_and of compare masks): a VALU-written SGPR read as a lane mask by
+// the next VALU instruction needs wait states that inline assembly does not get.
+__device__ __forceinline__ uint32_t push_bit(uint32_t bm, uint64_t mask) {
+  uint32_t r;
+  uint64_t carry_out;
+  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(carry_out) : "v"(bm), "s"(mask));
+  return r;
+}
+
+constexpr int kMT = 128;  // threads per multi-selection block
+// LDS working copy of the lanes' free capacity: cur[k][q][tid] for cards k < 8, plus row 8
+// where lanes without a fitting card put their takes (never read as a real card).
+template <int Q>
+constexpr size_t multi_lds_bytes() { return sizeof(int64_t) * 9 * Q * kMT; }
+
+// Pods with several selections (list `list`, kind SKIP = list - 1 dropped from the scans of
+// untouched cards): the selections in order (containers, then gpuNum), each taking the first
+// card that passes checkResourceCapacity (:341-383) with the pod's earlier takes (addRM,
+// resource_map.go:38-53) included.
+//   * Cards the pod has not taken from yet still hold the snapshot's free values, which stay
+//     in registers: one compare per (card, kind), the per-card verdicts packed into a lane
+//     bit mask bm (bit k = card k), masked by the cards not taken from (tm_not).
+//   * Cards it has taken from are the cards of the earlier selections (slots s < t); their
+//     current free lives in the lane's LDS column and is compared on every kind.
+//   * The selection is the lowest card of either set; taking it subtracts the need from the
+//     LDS column (ds_add_u64 of -need, no return).  After the pod the touched cards' columns
+//     are rewritten from the registers.
+// The per-lane state of one pod's selections: slot s = the card taken at selection s and the
+// LDS index of its column.
+struct MultiState {
+  uint32_t tm_not;  // bit k set: card k not taken from yet
+  uint32_t word;    // packed card ranks
+  bool fits;
+  int32_t slot_c[PAS_GAS_MAX_SELECTIONS];
+  int32_t slot_a[PAS_GAS_MAX_SELECTIONS];
+};
+
+// Selection T of the pod (recursion = full unroll, so slots are registers); returns when the
+// pod has no more selections or no node of the wave can still fit it.
+template <int Q, int SKIP, int T>
+__device__ __forceinline__ void multi_step(const int64_t (&free)[kMaxCards][Q], int64_t* cur,
+                                           int32_t tid, uint64_t live_mask, int32_t S,
+                                           const GasSel* rec, SelHead e, MultiState& st) {
+  if constexpr (T < PAS_GAS_MAX_SELECTIONS) {
+    if (T >= S) return;
+    if (e.bad) {  // a negative need fails every card (:343-347)
+      st.fits = false;
+      return;
+    }
+    // next record's scalar loads in flight during this selection
+    const SelHead en = sel_head<Q>(rec + min(T + 1, PAS_GAS_MAX_SELECTIONS - 1));
+    // untouched cards: snapshot free in registers; per card the kinds' compare masks and-ed
+    // in SALU (with the live lanes, so the mask is always a scalar result)
+    constexpr int kCompared = Q - (SKIP >= 0 ? 1 : 0);
+    uint32_t bm = 0u;
+#pragma unroll
+    for (int k = kMaxCards - 1; k >= 0; --k) {
+      uint64_t m = ~0ull;
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (q != SKIP) m &= le_mask(e.cmp[q], free[k][q]);
+      if (kCompared == 1) m &= live_mask;  // one compare: an s_and makes the mask scalar
+      bm = push_bit(bm, m);
+    }
+    const uint32_t u = bm & st.tm_not;
+    uint32_t c = u ? (uint32_t)__builtin_ctz(u) : 8u;
+    // touched cards: current free in LDS, every kind
+#pragma unroll
+    for (int sl = 0; sl < T; ++sl) {
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) ok &= e.cmp[q] <= cur[st.slot_a[sl] + q * kMT];
+      c = ok ? min(c, (uint32_t)st.slot_c[sl]) : c;
+    }
+    st.fits = st.fits && c < 8u;
+    if (!__ballot(st.fits)) return;  // no node of the wave fits the pod any more
+    st.slot_c[T] = (int32_t)c;
+    st.slot_a[T] = (int32_t)c * (Q * kMT) + tid;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (e.take[q] != 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&cur[st.slot_a[T] + q * kMT]),
+                  (unsigned long long)(-e.take[q]));
+    st.tm_not &= ~(1u << c);
+    st.word |= (c & 7u) << (3 * T);
+    multi_step<Q, SKIP, T + 1>(free, cur, tid, live_mask, S, rec, en, st);
+  }
+}
+
+// Pods with several selections (list `list`, kind SKIP = list - 1 dropped from the scans of
+// untouched cards): the selections in order (containers, then gpuNum), each taking the first
+// card that passes checkResourceCapacity (:341-383) with the pod's earlier takes (addRM,
+// resource_map.go:38-53) included.
+//   * Cards the pod has not taken from yet still hold the snapshot's free values, which stay
+//     in registers: one compare per (card, kind), the per-card verdicts packed into a lane
+//     bit mask bm (bit k = card k), masked by the cards not taken from (tm_not).
+//   * Cards it has taken from are the cards of the earlier selections (slots s < t); their
+//     current free lives in the lane's LDS column and is compared on every kind.
+//   * The selection is the lowest card of either set; taking it subtracts the need from the
+//     LDS column (ds_add_u64 of -need, no return).  After the pod the touched cards' columns
+//     are rewritten from the registers.
+template <int Q, int SKIP, bool kBits>
+__device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], int64_t* cur,
+                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                           const int32_t* __restrict__ list,
+                                           const GasSel* __restrict__ sels,
+                                           const int32_t* __restrict__ count, const BlockTile& bt,
+                                           uint32_t* __restrict__ res,
+                                           uint64_t* __restrict__ fit) {
+  const int32_t tid = threadIdx.x;
+  const bool live = valid && node_ok != 0u;
+  const uint64_t live_mask = __ballot(live);
+  int32_t i0, i1;
+  list_share(count, bt, &i0, &i1);
+  for (int32_t i = i0; i < i1; ++i) {
+    const int32_t pw = list[i];
+    const int64_t pod = pw & 0xFFFFFF;
+    const int32_t S = pw >> 24;
+    uint32_t out = 0u;
+    if (S <= PAS_GAS_MAX_SELECTIONS) {
+      const GasSel* rec = sels + pod * PAS_GAS_MAX_SELECTIONS;
+      MultiState st;
+      st.tm_not = 0xFFu;
+      st.word = 0u;
+      st.fits = live;
+      multi_step<Q, SKIP, 0>(free, cur, tid, live_mask, S, rec, sel_head<Q>(rec), st);
+      out = st.fits ? (node_ok | ((uint32_t)S << 24) | st.word) : 0u;
+      // restore the touched cards' columns
+#pragma unroll
+      for (int k = 0; k < kMaxCards; ++k) {
+        const bool touched = !((st.tm_not >> k) & 1u);
+        if (__ballot(touched) && touched)
+#pragma unroll
+          for (int q = 0; q < Q; ++q) cur[(k * Q + q) * kMT + tid] = free[k][q];
+      }
+    }
+    put_result<kBits>(res, fit, pod, N, n, valid, out);
+  }
+}
+
+template <int Q, bool kBits, int L = 0>
+__device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], int64_t* cur,
+                                            uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                            int32_t P, const int32_t* __restrict__ multi,
+                                            const GasSel* __restrict__ sels,
+                                            const int32_t* __restrict__ counts,
+                                            const BlockTile& bt, uint32_t* __restrict__ res,
+                                            uint64_t* __restrict__ fit) {
+  multi_list<Q, L - 1, kBits>(free, cur, node_ok, N, n, valid, multi + (int64_t)L * P, sels,
+                              counts + L, bt, res, fit);
+  if constexpr (L < Q)
+    multi_lists<Q, kBits, L + 1>(free, cur, node_ok, N, n, valid, P, multi, sels, counts, bt,
+                                 res, fit);
+}
+
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
-    int32_t N, int32_t K, const int32_t* __restrict__ n_cards, const int64_t* __restrict__ cap,
-    const int64_t* __restrict__ used, const int32_t* __restrict__ multi,
-    const GasSel* __restrict__ sels, const int32_t* __restrict__ counts,
-    uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
-  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+__global__ __launch_bounds__(kMT) void gas_fit_multi_kernel(
+    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
+    const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
+    const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
+    uint64_t* __restrict__ fit) {
+  extern __shared__ __attribute__((aligned(16))) int64_t cur[];
+  const BlockTile bt = block_tile(chunks);
+  const int32_t n = bt.node_block * kMT + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   int64_t free[kMaxCards][Q];
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cur[(k * Q + q) * kMT + threadIdx.x] = free[k][q];
   const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
-  int32_t i0, i1;
-  list_share(counts, &i0, &i1);
-  // pod words and selection records are wave-uniform: scalar loads straight into SGPRs (a
-  // selection used to cost a dozen readfirstlanes from an LDS stage)
-  // The next pod's word and first two selections are loaded one iteration ahead: otherwise
-  // every pod waits on two scalar-load round trips before its first compare.
-  {
-    SelHead nh = {}, nh1 = {};
-    int32_t npw = 0;
-    if (i0 < i1) {
-      npw = multi[i0];
-      nh = sel_head<Q>(sels + (int64_t)i0 * PAS_GAS_MAX_SELECTIONS);
-      nh1 = sel_head<Q>(sels + (int64_t)i0 * PAS_GAS_MAX_SELECTIONS + 1);
-    }
-    for (int32_t i = i0; i < i1; ++i) {
-      const GasSel* stage_j = sels + (int64_t)i * PAS_GAS_MAX_SELECTIONS;
-      const int32_t pw = npw;
-      const SelHead e0 = nh, e1 = nh1;
-      if (i + 1 < i1) {
-        npw = multi[i + 1];
-        nh = sel_head<Q>(stage_j + PAS_GAS_MAX_SELECTIONS);
-        nh1 = sel_head<Q>(stage_j + PAS_GAS_MAX_SELECTIONS + 1);
-      }
-      const int64_t p = pw & 0xFFFFFF;
-      const int32_t steps = pw >> 24;
-      uint32_t out = 0u;
-      if (steps == 2) {
-        // two selections without touching free: the second one sees card c0 with the
-        // first take added to its need, every other card as it was
-        int64_t cmp0[Q], cmp1[Q], cmp1t[Q];
-        bool ovf = false;  // need1 + take0 beyond int64: card c0 cannot take the second
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          cmp0[q] = uniform64(e0.cmp[q]);
-          cmp1[q] = uniform64(e1.cmp[q]);
-          // INT64_MIN + 0 stays unrequested
-          ovf |= __builtin_add_overflow(cmp1[q], uniform64(e0.take[q]), &cmp1t[q]);
-        }
-        const int c0 = __builtin_amdgcn_readfirstlane(e0.bad) ? -1 : first_fit<Q, -1>(free, cmp0);
-        int c1 = -1;
-        if (!__builtin_amdgcn_readfirstlane(e1.bad)) {
-          // card k fits the second selection: cmp1 <= free (k != c0) or cmp1t <= free
-          // (k == c0; never when need1 + take0 overflows, a uniform and rare case)
-          if (!ovf) {
-#pragma unroll
-            for (int k = kMaxCards - 1; k >= 0; --k) {
-              bool ok = true;
-#pragma unroll
-              for (int q = 0; q < Q; ++q)
-                ok &= (c0 == k ? cmp1t[q] : cmp1[q]) <= free[k][q];
-              c1 = ok ? k : c1;
-            }
-          } else {
-#pragma unroll
-            for (int k = kMaxCards - 1; k >= 0; --k) {
-              bool ok = c0 != k;
-#pragma unroll
-              for (int q = 0; q < Q; ++q) ok &= cmp1[q] <= free[k][q];
-              c1 = ok ? k : c1;
-            }
-          }
-        }
-        out = (c0 >= 0 && c1 >= 0) ? (node_ok | (2u << 24) | (uint32_t)c0 | ((uint32_t)c1 << 3))
-                                   : 0u;
-      } else if (steps <= PAS_GAS_MAX_SELECTIONS) {
-        // three or more selections: take cards in a working copy of free
-        int64_t w[kMaxCards][Q];
-#pragma unroll
-        for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-          for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
-        bool fits = true;
-        uint32_t word = 0;
-        // the next step's record is loaded before the current step's compares (slot
-        // min(t + 1, 7) of the row is always in bounds)
-        SelHead e = e0;
-        for (int32_t t = 0; t < steps; ++t) {
-          const SelHead en = sel_head<Q>(stage_j + min(t + 1, PAS_GAS_MAX_SELECTIONS - 1));
-          int64_t cmp[Q], take[Q];
-#pragma unroll
-          for (int q = 0; q < Q; ++q) {
-            cmp[q] = uniform64(e.cmp[q]);
-            take[q] = uniform64(e.take[q]);
-          }
-          const int k = __builtin_amdgcn_readfirstlane(e.bad) ? -1 : first_fit<Q, -1>(w, cmp);
-          fits = fits && k >= 0;
-          // per card taken by some lane of the wave (uniform branch), a per-lane select: a
-          // divergent branch around the update would make the compiler copy the array
-          int64_t tv[Q];  // the takes in VGPRs once per step (a select may read one SGPR)
-#pragma unroll
-          for (int q = 0; q < Q; ++q) tv[q] = to_vgpr64(take[q]);
-#pragma unroll
-          for (int kk = 0; kk < kMaxCards; ++kk)
-            if (__ballot(k == kk))
-#pragma unroll
-              for (int q = 0; q < Q; ++q) w[kk][q] -= k == kk ? tv[q] : 0;
-          word |= (uint32_t)(k & 7) << (3 * t);
-          e = en;
-        }
-        out = fits ? (node_ok | ((uint32_t)steps << 24) | word) : 0u;
-      }
-      put_result<kBits>(res, fit, p, N, n, valid, out);
-    }
-  }
+  multi_lists<Q, kBits>(free, cur, node_ok, N, n, valid, P, multi, sels, counts, bt, res, fit);
 }
 
 }  // namespace
@@ -520,15 +613,15 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
   if (N == 0 || n_pods == 0) return PAS_OK;
-  // scratch: single-selection records [Q+1][P] | multi-selection pod words [P] | their
-  // selection rows [P][8] | the flipped kind minima [4] and counts [Q+2] (zeroed together)
+  // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][P] | their
+  // selection rows [P][8] | the flipped kind minima [4] and counts [2(Q+1)] (zeroed together)
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   const int32_t NL = Q + 1;
   const size_t b_single = (sizeof(GasSingle) * (size_t)NL * n_pods + 255) & ~size_t(255);
-  const size_t b_multi = (sizeof(int32_t) * (size_t)n_pods + 255) & ~size_t(255);
+  const size_t b_multi = (sizeof(int32_t) * (size_t)NL * n_pods + 255) & ~size_t(255);
   const size_t b_sels =
       (sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS * (size_t)n_pods + 255) & ~size_t(255);
-  constexpr size_t b_tail = (PAS_GAS_MAX_RES + 2) * sizeof(int32_t) +
+  constexpr size_t b_tail = 2 * (PAS_GAS_MAX_RES + 1) * sizeof(int32_t) +
                             PAS_GAS_MAX_RES * sizeof(unsigned long long);
   const size_t need = b_single + b_multi + b_sels + b_tail;
   if (need > ctx->aux_bytes) {
@@ -558,20 +651,21 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
       multi, sels, counts);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
-  // grids: node blocks x pod chunks, ~4096 blocks for the whole batch; each kernel splits
-  // each of its device-counted lists evenly over its chunks
-  const int32_t node_blocks = (N + kTpb - 1) / kTpb;
-  const int32_t chunks = std::max(1, std::min(n_pods, (4096 + node_blocks - 1) / node_blocks));
-  const dim3 grid((unsigned)node_blocks, (unsigned)chunks);
+  // grids: (node block, pod chunk) pairs, ~4096 blocks for the single kernel and ~8192 for
+  // the multi kernel (half the nodes per block); each kernel splits each of its
+  // device-counted lists evenly over the chunks
+  const int32_t nb_s = (N + kTpb - 1) / kTpb, nb_m = (N + kMT - 1) / kMT;
+  const int32_t ch_s = std::max(1, std::min(n_pods, (4096 + nb_s - 1) / nb_s));
+  const int32_t ch_m = std::max(1, std::min(n_pods, (8192 + nb_m - 1) / nb_m));
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
-    gas_fit_single_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, n_pods, g.n_cards, g.cap, g.used, \
-                                                       single, counts, d_res, d_fit);          \
-    gas_fit_multi_kernel<QQ, B><<<grid, kTpb, 0, s>>>(N, K, g.n_cards, g.cap, g.used, multi,   \
-                                                      sels, counts + NL, d_res, d_fit);        \
+    gas_fit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                 \
+        N, K, n_pods, g.n_cards, g.cap, g.used, single, counts, ch_s, d_res, d_fit);           \
+    gas_fit_multi_kernel<QQ, B><<<nb_m * ch_m, kMT, multi_lds_bytes<QQ>(), s>>>(               \
+        N, K, n_pods, g.n_cards, g.cap, g.used, multi, sels, counts + NL, ch_m, d_res, d_fit); \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)

@@ -125,95 +125,6 @@ void free_gas(pas_ctx* ctx) {
   g = GasSnapshot{};
 }
 
-// ---------------------------------------------------------------------------
-// resource.Quantity -> exact scaled integer
-// ---------------------------------------------------------------------------
-
-// Parses the k8s.io/apimachinery v0.22.2 quantity grammar
-// (<signedNumber><suffix>, suffix in {"" n u m k M G T P E Ki..Ei, e<int>, E<int>})
-// into mantissa * 10^exp10 * 2^exp2 and scales it by 10^extra10 exactly.
-// Returns PAS_OK with *out set, PAS_ENOTEXACT if non-integral after scaling or out of
-// int64 range, PAS_EINVAL if unparsable.
-static int quantity_scaled(const char* s, int extra10, int64_t* out) {
-  if (!s) return PAS_EINVAL;
-  const char* p = s;
-  bool neg = false;
-  if (*p == '+' || *p == '-') { neg = (*p == '-'); ++p; }
-  __int128 mant = 0;
-  int ndigits = 0, nfrac = 0, sig = 0;
-  bool seen_dot = false, overflow = false;
-  for (;; ++p) {
-    if (*p >= '0' && *p <= '9') {
-      ++ndigits;
-      if (seen_dot) ++nfrac;
-      if (mant != 0 || *p != '0') {
-        if (++sig > 36) { overflow = true; }
-        else mant = mant * 10 + (*p - '0');
-      }
-    } else if (*p == '.' && !seen_dot) {
-      seen_dot = true;
-    } else {
-      break;
-    }
-  }
-  if (ndigits == 0) return PAS_EINVAL;
-  int exp10 = 0, exp2 = 0;
-  const std::string suf(p);
-  if (suf.empty()) {
-  } else if (suf == "n") { exp10 = -9;
-  } else if (suf == "u") { exp10 = -6;
-  } else if (suf == "m") { exp10 = -3;
-  } else if (suf == "k") { exp10 = 3;
-  } else if (suf == "M") { exp10 = 6;
-  } else if (suf == "G") { exp10 = 9;
-  } else if (suf == "T") { exp10 = 12;
-  } else if (suf == "P") { exp10 = 15;
-  } else if (suf == "E") { exp10 = 18;
-  } else if (suf == "Ki") { exp2 = 10;
-  } else if (suf == "Mi") { exp2 = 20;
-  } else if (suf == "Gi") { exp2 = 30;
-  } else if (suf == "Ti") { exp2 = 40;
-  } else if (suf == "Pi") { exp2 = 50;
-  } else if (suf == "Ei") { exp2 = 60;
-  } else if ((suf[0] == 'e' || suf[0] == 'E') && suf.size() > 1) {
-    const char* q = suf.c_str() + 1;
-    bool eneg = false;
-    if (*q == '+' || *q == '-') { eneg = (*q == '-'); ++q; }
-    if (!*q) return PAS_EINVAL;
-    long e = 0;
-    for (; *q; ++q) {
-      if (*q < '0' || *q > '9') return PAS_EINVAL;
-      e = e * 10 + (*q - '0');
-      if (e > 100000) return PAS_ENOTEXACT;
-    }
-    exp10 = (int)(eneg ? -e : e);
-  } else {
-    return PAS_EINVAL;
-  }
-  if (overflow) return PAS_ENOTEXACT;
-  const __int128 lim = ((__int128)1) << 120;
-  for (int i = 0; i < exp2; ++i) {
-    mant *= 2;
-    if (mant > lim) return PAS_ENOTEXACT;
-  }
-  int e = exp10 + extra10 - nfrac;
-  if (mant == 0) { *out = 0; return PAS_OK; }
-  while (e > 0) {
-    mant *= 10;
-    --e;
-    if (mant > lim) return PAS_ENOTEXACT;
-  }
-  while (e < 0) {
-    if (mant % 10 != 0) return PAS_ENOTEXACT;
-    mant /= 10;
-    ++e;
-  }
-  const __int128 v = neg ? -mant : mant;
-  if (v > (__int128)INT64_MAX || v < (__int128)INT64_MIN) return PAS_ENOTEXACT;
-  *out = (int64_t)v;
-  return PAS_OK;
-}
-
 struct Carve {
   char* base;
   size_t off = 0;
@@ -304,19 +215,7 @@ int pas_parse_operator(const char* op) {
   return PAS_EINVAL;
 }
 
-int pas_quantity_to_milli(const char* quantity, int64_t* milli_out) {
-  if (!milli_out) return PAS_EINVAL;
-  return quantity_scaled(quantity, 3, milli_out);
-}
-
-int pas_quantity_as_int64(const char* quantity, int64_t* out) {
-  if (!out) return PAS_EINVAL;
-  int64_t v = 0;
-  const int rc = quantity_scaled(quantity, 0, &v);
-  if (rc == PAS_EINVAL) return rc;
-  *out = (rc == PAS_OK) ? v : 0;  // AsInt64 `ok` ignored by the reference -> 0
-  return PAS_OK;
-}
+// pas_quantity_to_milli / pas_quantity_as_int64: quantity.cpp (host only)
 
 // --------------------------------------------------------------------------- TAS
 
