@@ -41,7 +41,6 @@ namespace {
 
 constexpr int kTpb = 256;
 constexpr int kMaxCards = PAS_GAS_MAX_CARDS;
-constexpr int kPodBatch = 64;  // pod records staged in LDS per round
 
 // A (pod, container) step, in compare form: cmp[q] = per-GPU need of a requested kind
 // (getPerGPUResourceRequest :180-190), INT64_MIN for the others, so every card passes them
@@ -55,21 +54,31 @@ struct alignas(16) GasStep {
   int32_t pad;
 };
 
-// One card selection of a pod with several: compare and take vectors (kinds as GasStep).
+// One card selection of a pod with several, per kind q: {cmp, -take} (kinds as GasStep: the
+// need of a requested kind, INT64_MIN / 0 for the others), one 16-byte load per kind.
 struct alignas(16) GasSel {
-  int64_t cmp[PAS_GAS_MAX_RES];
-  int64_t take[PAS_GAS_MAX_RES];
-  int32_t bad;
-  int32_t pad[3];
+  int64_t ct[PAS_GAS_MAX_RES][2];
 };
+// A pod with 2 or 3 selections is resolved in closed form from threshold compares on the
+// snapshot free values (see multi_closed): threshold j per kind, in compare form (INT64_MIN
+// for kinds the selection does not request).  The 7 thresholds of a 3-selection pod:
+//   0: n0   1: n1   2: n1 + t0   3: n2   4: n2 + t0   5: n2 + t1   6: n2 + t0 + t1
+// (n = the selection's need, t = an earlier selection's take); a 2-selection pod uses 0-2.
+// over bit j: threshold j overflows int64, so no card can pass it (:367-371).
+struct alignas(16) GasThresholds {
+  int64_t th[7][PAS_GAS_MAX_RES];
+  int32_t over;
+  int32_t pad[7];
+};
+static_assert(sizeof(GasThresholds) <= sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS, "row");
+constexpr int32_t kBadPod = 1 << 30;  // multi-list word flag: a selection has a negative need
 
-// Pod with at most one card selection: its selecting step, or steps == 0.
+// Pod with at most one card selection: its selecting step (compare form), and
+// word = pod | steps << 24 | bad << 30 (steps 0: no selection, fits every labelled node).
 struct alignas(16) GasSingle {
   int64_t cmp[PAS_GAS_MAX_RES];
-  int32_t pod;
-  int32_t steps;
-  int32_t bad;
-  int32_t pad;
+  int32_t word;
+  int32_t pad[3];
 };
 
 // getPerGPUResourceRequest: copy the container's map and, when numI915 > 1, divide
@@ -134,11 +143,10 @@ __device__ __forceinline__ int32_t wave_slot(int32_t* __restrict__ counts, int32
 }
 
 // The list a multi-selection pod is filed under: 1 + q for the lowest kind q that some
-// selection requests and whose compare can be dropped from every selection's scan of the
-// cards the pod has not taken from yet (untouched cards hold their snapshot free, >= gmin[q]):
-// each selection either does not request q or needs at most gmin[q] of it and requests
-// another kind too (cards a node does not have must keep failing).  Cards the pod has taken
-// from are always compared on every kind.  Else 0.
+// selection requests and whose compares can be dropped: the pod's total take of q is at most
+// gmin[q], so any selection's need plus any earlier takes on a card stays within every real
+// card's snapshot free; and every selection requesting q requests another kind too (cards a
+// node does not have must keep failing).  Else 0.
 __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_mask,
                                                    uint32_t req_mask) {
   const uint32_t m = ok_mask & req_mask & ((1u << n_res) - 1u);
@@ -148,7 +156,8 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
 // One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
 // list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
 // [n_res + 1][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list); a multi
-// pod's selections (containers in order, then gpuNum) go to its own row sels[pod][8].  More
+// pod's selections (containers in order, then gpuNum) go to the row sels[list][slot][8] of
+// its list position.  More
 // than PAS_GAS_MAX_SELECTIONS selections are beyond the packed result and keep only the
 // count.  counts: [n_res + 1] single lists, then [n_res + 1] multi lists.
 __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
@@ -165,15 +174,16 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   int32_t steps = 0;
   uint32_t kinds = 0;
   uint32_t skip_ok = (1u << n_res) - 1u, skip_req = 0;  // multi_skip_list
+  int64_t cum[PAS_GAS_MAX_RES] = {};                     // the pod's total take per kind
   GasSingle one = {};
-  one.pod = p;
+  int32_t one_bad = 0;
   for (int32_t c = 0; c < nc; ++c) {
     const GasStep g = container_step(row + c, n_res, i915, req, mask);
     if (g.num_i915 > 0) {
       if (steps == 0) {
 #pragma unroll
         for (int q = 0; q < PAS_GAS_MAX_RES; ++q) one.cmp[q] = g.cmp[q];
-        one.bad = g.bad;
+        one_bad = g.bad;
         kinds = g.kinds;
       }
       steps = min(steps + g.num_i915, PAS_GAS_MAX_SELECTIONS + 1);
@@ -181,10 +191,17 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
       skip_req |= gk;
       for (int q = 0; q < n_res; ++q) {
         if (!((gk >> q) & 1u)) continue;
-        const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
-        if (g.cmp[q] > gmin || gk == (1u << q)) skip_ok &= ~(1u << q);
+        // saturating: a total past INT64_MAX only has to exceed every gmin
+        const int64_t add = g.take[q] > 0 ? g.take[q] : 0;
+        for (int32_t r = 0; r < g.num_i915; ++r)
+          cum[q] = cum[q] > INT64_MAX - add ? INT64_MAX : cum[q] + add;
+        if (gk == (1u << q)) skip_ok &= ~(1u << q);
       }
     }
+  }
+  for (int q = 0; q < n_res; ++q) {
+    const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
+    if (cum[q] > gmin) skip_ok &= ~(1u << q);
   }
   const bool one_sel = steps <= 1;
   const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0)
@@ -192,27 +209,58 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   const int32_t nl = n_res + 1;
   const int32_t slot = wave_slot(counts, one_sel ? l : nl + l);
   if (one_sel) {
-    one.steps = steps;
+    one.word = p | (steps << 24) | (one_bad ? kBadPod : 0);
     single[(int64_t)l * n_pods + slot] = one;
     return;
   }
-  multi[(int64_t)l * n_pods + slot] = p | (steps << 24);
-  if (steps > PAS_GAS_MAX_SELECTIONS) return;
-  GasSel* out = sels + (int64_t)p * PAS_GAS_MAX_SELECTIONS;
-  int32_t k = 0;
+  if (steps > PAS_GAS_MAX_SELECTIONS) {
+    multi[(int64_t)l * n_pods + slot] = p | (steps << 24);
+    return;
+  }
+  // the pod's row sits at its list position, so a batch of a list is one contiguous copy
+  GasSel* out = sels + ((int64_t)l * n_pods + slot) * PAS_GAS_MAX_SELECTIONS;
+  int32_t k = 0, bad = 0;
+  int64_t cmp3[3][PAS_GAS_MAX_RES], take3[3][PAS_GAS_MAX_RES];  // first 3 selections
   for (int32_t c = 0; c < nc; ++c) {
     const GasStep g = container_step(row + c, n_res, i915, req, mask);
+    bad |= g.num_i915 > 0 ? g.bad : 0;
     for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
+      if (k < 3) {
+        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+          cmp3[k][q] = g.cmp[q];
+          take3[k][q] = g.take[q];
+        }
+      }
+      if (steps <= 3) continue;
       GasSel e = {};
 #pragma unroll
       for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
-        e.cmp[q] = g.cmp[q];
-        e.take[q] = g.take[q];
+        e.ct[q][0] = g.cmp[q];
+        e.ct[q][1] = (int64_t)(0ull - (unsigned long long)g.take[q]);
       }
-      e.bad = g.bad;
       out[k] = e;
     }
   }
+  if (steps <= 3) {
+    // thresholds: need plus the takes of a subset of the earlier selections (cards taken
+    // from by exactly those selections); unrequested kinds stay INT64_MIN
+    GasThresholds t = {};
+    const int32_t subs[7][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {2, 0, 0},
+                                {2, 1, 0}, {2, 0, 1}, {2, 1, 1}};  // {selection, +t0, +t1}
+    for (int j = 0; j < (steps == 2 ? 3 : 7); ++j) {
+      const int32_t sel = subs[j][0];
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+        int64_t v = cmp3[sel][q];
+        if (v != INT64_MIN) {
+          for (int e = 0; e < 2; ++e)
+            if (subs[j][1 + e] && __builtin_add_overflow(v, take3[e][q], &v)) t.over |= 1 << j;
+        }
+        t.th[j][q] = v;
+      }
+    }
+    *reinterpret_cast<GasThresholds*>(out) = t;
+  }
+  multi[(int64_t)l * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
 }
 
 // gflip[q] = INT64_MAX - gmin[q] (kept flipped so that a zeroed buffer is the identity of the
@@ -296,10 +344,17 @@ __device__ __forceinline__ int64_t uniform64(int64_t x) {
 // One (pod, node) result: the packed word, or (kBits) the fit bit in the pod's row of a
 // node bitmap, written per 64-node word by lane 0 of the wave (waves cover aligned
 // 64-node ranges).
+#ifndef PAS_GAS_ABLATE
+#define PAS_GAS_ABLATE 0  // diagnostic timing builds only: 1 = no result stores (outputs wrong)
+#endif
 template <bool kBits>
 __device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t* __restrict__ fit,
                                            int64_t p, int32_t N, int32_t n, bool valid,
                                            uint32_t out) {
+  if (PAS_GAS_ABLATE & 1) {
+    if (out == 0x7fffffffu) res[n] = out;  // keeps the work alive; never true
+    return;
+  }
   if (kBits) {
     const uint64_t b = __ballot(valid && (out >> 31));
     if ((threadIdx.x & 63) == 0 && n < N) fit[p * ((N + 63) / 64) + (n >> 6)] = b;
@@ -331,8 +386,14 @@ __device__ __forceinline__ void list_share(const int32_t* count, const BlockTile
   *e = min(cnt, *b + per);
 }
 
+constexpr int kPodBatch = 64;  // single-selection pod records staged in LDS per round and wave
+
 // Pods with at most one selection, list `l` (kind SKIP = l - 1 dropped): a read-only first
-// fit per (pod, node lane), pod records staged in LDS per batch and read into SGPRs.
+// fit per (pod, node lane).  Each wave stages the records of kPodBatch pods in its own LDS
+// slice (no block barrier) and reads them back with broadcast LDS reads: the compare values
+// stay in VGPRs, only the pod word goes to an SGPR.  (Vector loads of each record straight
+// from memory wait for the previous pod's result store: vmcnt counts stores and completes
+// in order.)
 template <int Q, int SKIP, bool kBits>
 __device__ __forceinline__ void single_list(const int64_t (&free)[kMaxCards][Q],
                                             uint32_t node_ok, int32_t N, int32_t n, bool valid,
@@ -340,30 +401,51 @@ __device__ __forceinline__ void single_list(const int64_t (&free)[kMaxCards][Q],
                                             const int32_t* __restrict__ count, GasSingle* stage,
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
+  const int32_t lane = threadIdx.x & 63;
   int32_t i0, i1;
   list_share(count, bt, &i0, &i1);
   for (int32_t b0 = i0; b0 < i1; b0 += kPodBatch) {
     const int32_t nb = min(kPodBatch, i1 - b0);
     constexpr int kWords = (int)(sizeof(GasSingle) / 16);
+    constexpr int kIters = kPodBatch * kWords / 64;
+    static_assert(kPodBatch * kWords % 64 == 0, "stage copy");
     const int4* src = reinterpret_cast<const int4*>(single + b0);
-    int4* dst = reinterpret_cast<int4*>(stage);
-    for (int32_t i = threadIdx.x; i < nb * kWords; i += kTpb) dst[i] = src[i];
-    __syncthreads();
-    for (int32_t j = 0; j < nb; ++j) {
-      const GasSingle& r = stage[j];  // broadcast LDS reads, then SGPRs
-      const int64_t pod = __builtin_amdgcn_readfirstlane(r.pod);
-      uint32_t out = node_ok;
-      if (__builtin_amdgcn_readfirstlane(r.steps) == 1) {
-        int64_t cmp[Q];
+    int4 v[kIters];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) cmp[q] = q == SKIP ? 0 : uniform64(r.cmp[q]);
-        const int k =
-            __builtin_amdgcn_readfirstlane(r.bad) ? -1 : first_fit<Q, SKIP>(free, cmp);
+    for (int it = 0; it < kIters; ++it) {
+      const int32_t c = lane + it * 64;
+      v[it] = c < nb * kWords ? src[c] : int4{0, 0, 0, 0};
+    }
+    __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    // broadcast LDS reads, the next pod's issued before this pod's compares
+    int64_t cmp[Q];
+    int32_t word;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cmp[q] = q == SKIP ? 0 : stage[0].cmp[q];
+    word = stage[0].word;
+    for (int32_t j = 0; j < nb; ++j) {
+      const int32_t jn = min(j + 1, kPodBatch - 1);
+      int64_t ncmp[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) ncmp[q] = q == SKIP ? 0 : stage[jn].cmp[q];
+      const int32_t nword = stage[jn].word;
+      const int32_t w = __builtin_amdgcn_readfirstlane(word);
+      const int64_t pod = w & 0xFFFFFF;
+      uint32_t out = node_ok;
+      if (((w >> 24) & 0xF) == 1) {
+        const int k = (w & kBadPod) ? -1 : first_fit<Q, SKIP>(free, cmp);
         out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
       }
       put_result<kBits>(res, fit, pod, N, n, valid, out);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) cmp[q] = ncmp[q];
+      word = nword;
     }
-    __syncthreads();  // the next batch rewrites the stage
   }
 }
 
@@ -388,7 +470,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
     const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
     const GasSingle* __restrict__ single, const int32_t* __restrict__ counts, int32_t chunks,
     uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
-  __shared__ GasSingle stage[kPodBatch];
+  __shared__ GasSingle stage[kTpb / 64][kPodBatch];  // a slice per wave
   const BlockTile bt = block_tile(chunks);
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
@@ -397,211 +479,401 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
   // FetchNode error / missing cards label -> errWontFit before any container (:282-298)
   const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
-  single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage, bt, res, fit);
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage[wave], bt, res,
+                         fit);
 }
 
-// The compare / take fields of one selection record, kinds [0, Q) (scalar loads).
-struct SelHead {
-  int64_t cmp[PAS_GAS_MAX_RES];
-  int64_t take[PAS_GAS_MAX_RES];
-  int32_t bad;
-};
-template <int Q>
-__device__ __forceinline__ SelHead sel_head(const GasSel* e) {
-  SelHead h = {};
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    h.cmp[q] = e->cmp[q];
-    h.take[q] = e->take[q];
-  }
-  h.bad = e->bad;
-  return h;
-}
-
-// Lane mask of a <= v (a wave-uniform, in SGPRs): the compare writes the mask directly.
-__device__ __forceinline__ uint64_t le_mask(int64_t a, int64_t v) {
-  uint64_t m;
-  asm("v_cmp_le_i64_e64 %0, %1, %2" : "=s"(m) : "s"(a), "v"(v));
-  return m;
-}
-
-// bm * 2 + (this lane's bit of `mask`): one v_addc with the lane mask as carry-in.  Cards are
-// pushed from the last to the first, so bit k of the result is card k.  `mask` must come from
-// a scalar instruction (an s_and of compare masks): a VALU-written SGPR read as a lane mask by
-// the next VALU instruction needs wait states that inline assembly does not get.
-__device__ __forceinline__ uint32_t push_bit(uint32_t bm, uint64_t mask) {
+// A group of cards of the untouched-card scan: bm * 2 + (1 if need[q] <= free[q] for the C
+// compared kinds), card by card from the highest, so bit k of the final mask is card k.
+// The blocks declare the SCC clobber of their s_and's.  One assembly block per group issues
+// every compare of the group first (they write lane
+// masks), then the s_and's combining each card's kinds (with `live` when there is only one
+// kind, so the carry-in always comes from a scalar write: a VALU-written SGPR read as a lane
+// mask by the next VALU needs wait states inline assembly does not get), then one v_addc per
+// card with its mask as carry-in.  The compares' latency is covered by the group's other
+// compares; a block per group also keeps the scheduler from hoisting every card's compares
+// and running out of SGPRs for their masks.
+#define PAS_CMP(m, n, f) "v_cmp_le_i64_e64 %[" #m "], %[" #n "], %[" #f "]\n\t"
+#define PAS_AND(d, a, b) "s_and_b64 %[" #d "], %[" #a "], %[" #b "]\n\t"
+#define PAS_ADDC(r, x, m) "v_addc_co_u32_e64 %[" #r "], %[co], %[" #x "], %[" #x "], %[" #m "]\n\t"
+// C = 1: 4 cards per block
+__device__ __forceinline__ uint32_t push4_c1(uint32_t bm, int64_t n0, int64_t f0, int64_t f1,
+                                             int64_t f2, int64_t f3, uint64_t live) {
   uint32_t r;
-  uint64_t carry_out;
-  asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(carry_out) : "v"(bm), "s"(mask));
+  uint64_t m0, m1, m2, m3, co;
+  asm(PAS_CMP(m0, n0, f0) PAS_CMP(m1, n0, f1) PAS_CMP(m2, n0, f2) PAS_CMP(m3, n0, f3)
+      PAS_AND(m0, m0, lv) PAS_AND(m1, m1, lv) PAS_AND(m2, m2, lv) PAS_AND(m3, m3, lv)
+      PAS_ADDC(r, bm, m0) PAS_ADDC(r, r, m1) PAS_ADDC(r, r, m2) PAS_ADDC(r, r, m3)
+      : [r] "=&v"(r), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+        [co] "=&s"(co)
+      : [n0] "v"(n0), [f0] "v"(f0), [f1] "v"(f1), [f2] "v"(f2), [f3] "v"(f3), [lv] "s"(live),
+        [bm] "v"(bm)
+      : "scc");
   return r;
 }
+// C = 2: 4 cards per block
+__device__ __forceinline__ uint32_t push4_c2(uint32_t bm, int64_t n0, int64_t n1, int64_t a0,
+                                             int64_t a1, int64_t b0, int64_t b1, int64_t c0,
+                                             int64_t c1, int64_t d0, int64_t d1) {
+  uint32_t r;
+  uint64_t m0, m1, m2, m3, m4, m5, m6, m7, co;
+  asm(PAS_CMP(m0, n0, a0) PAS_CMP(m1, n1, a1) PAS_CMP(m2, n0, b0) PAS_CMP(m3, n1, b1)
+      PAS_CMP(m4, n0, c0) PAS_CMP(m5, n1, c1) PAS_CMP(m6, n0, d0) PAS_CMP(m7, n1, d1)
+      PAS_AND(m0, m0, m1) PAS_AND(m2, m2, m3) PAS_AND(m4, m4, m5) PAS_AND(m6, m6, m7)
+      PAS_ADDC(r, bm, m0) PAS_ADDC(r, r, m2) PAS_ADDC(r, r, m4) PAS_ADDC(r, r, m6)
+      : [r] "=&v"(r), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+        [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [co] "=&s"(co)
+      : [n0] "v"(n0), [n1] "v"(n1), [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1),
+        [c0] "v"(c0), [c1] "v"(c1), [d0] "v"(d0), [d1] "v"(d1), [bm] "v"(bm)
+      : "scc");
+  return r;
+}
+// C = 3: 2 cards per block
+__device__ __forceinline__ uint32_t push2_c3(uint32_t bm, int64_t n0, int64_t n1, int64_t n2,
+                                             int64_t a0, int64_t a1, int64_t a2, int64_t b0,
+                                             int64_t b1, int64_t b2) {
+  uint32_t r;
+  uint64_t m0, m1, m2, m3, m4, m5, co;
+  asm(PAS_CMP(m0, n0, a0) PAS_CMP(m1, n1, a1) PAS_CMP(m2, n2, a2) PAS_CMP(m3, n0, b0)
+      PAS_CMP(m4, n1, b1) PAS_CMP(m5, n2, b2)
+      PAS_AND(m0, m0, m1) PAS_AND(m3, m3, m4) PAS_AND(m0, m0, m2) PAS_AND(m3, m3, m5)
+      PAS_ADDC(r, bm, m0) PAS_ADDC(r, r, m3)
+      : [r] "=&v"(r), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+        [m4] "=&s"(m4), [m5] "=&s"(m5), [co] "=&s"(co)
+      : [n0] "v"(n0), [n1] "v"(n1), [n2] "v"(n2), [a0] "v"(a0), [a1] "v"(a1), [a2] "v"(a2),
+        [b0] "v"(b0), [b1] "v"(b1), [b2] "v"(b2), [bm] "v"(bm)
+      : "scc");
+  return r;
+}
+// C = 4: 2 cards per block
+__device__ __forceinline__ uint32_t push2_c4(uint32_t bm, const int64_t (&n)[4],
+                                             const int64_t (&a)[4], const int64_t (&b)[4]) {
+  uint32_t r;
+  uint64_t m0, m1, m2, m3, m4, m5, m6, m7, co;
+  asm(PAS_CMP(m0, n0, a0) PAS_CMP(m1, n1, a1) PAS_CMP(m2, n2, a2) PAS_CMP(m3, n3, a3)
+      PAS_CMP(m4, n0, b0) PAS_CMP(m5, n1, b1) PAS_CMP(m6, n2, b2) PAS_CMP(m7, n3, b3)
+      PAS_AND(m0, m0, m1) PAS_AND(m4, m4, m5) PAS_AND(m2, m2, m3) PAS_AND(m6, m6, m7)
+      PAS_AND(m0, m0, m2) PAS_AND(m4, m4, m6)
+      PAS_ADDC(r, bm, m0) PAS_ADDC(r, r, m4)
+      : [r] "=&v"(r), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3),
+        [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7), [co] "=&s"(co)
+      : [n0] "v"(n[0]), [n1] "v"(n[1]), [n2] "v"(n[2]), [n3] "v"(n[3]), [a0] "v"(a[0]),
+        [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [b0] "v"(b[0]), [b1] "v"(b[1]),
+        [b2] "v"(b[2]), [b3] "v"(b[3]), [bm] "v"(bm)
+      : "scc");
+  return r;
+}
+// C = 2, two threshold rows A and B over the same 2 cards, their carry chains interleaved
+// (two independent dependence chains in one block)
+__device__ __forceinline__ void push2x2_c2(uint32_t& ba, uint32_t& bb, int64_t a0, int64_t a1,
+                                           int64_t b0, int64_t b1, int64_t x0, int64_t x1,
+                                           int64_t y0, int64_t y1) {
+  uint32_t ra, rb;
+  uint64_t m0, m1, m2, m3, m4, m5, m6, m7, co;
+  asm(PAS_CMP(m0, a0, x0) PAS_CMP(m1, a1, x1) PAS_CMP(m2, b0, x0) PAS_CMP(m3, b1, x1)
+      PAS_CMP(m4, a0, y0) PAS_CMP(m5, a1, y1) PAS_CMP(m6, b0, y0) PAS_CMP(m7, b1, y1)
+      PAS_AND(m0, m0, m1) PAS_AND(m2, m2, m3) PAS_AND(m4, m4, m5) PAS_AND(m6, m6, m7)
+      PAS_ADDC(ra, ia, m0) PAS_ADDC(rb, ib, m2) PAS_ADDC(ra, ra, m4) PAS_ADDC(rb, rb, m6)
+      : [ra] "=&v"(ra), [rb] "=&v"(rb), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
+        [m3] "=&s"(m3), [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7),
+        [co] "=&s"(co)
+      : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1), [x0] "v"(x0), [x1] "v"(x1),
+        [y0] "v"(y0), [y1] "v"(y1), [ia] "v"(ba), [ib] "v"(bb)
+      : "scc");
+  ba = ra;
+  bb = rb;
+}
+#undef PAS_CMP
+#undef PAS_AND
+#undef PAS_ADDC
 
-constexpr int kMT = 128;  // threads per multi-selection block
-// LDS working copy of the lanes' free capacity: cur[k][q][tid] for cards k < 8, plus row 8
-// where lanes without a fitting card put their takes (never read as a real card).
-template <int Q>
-constexpr size_t multi_lds_bytes() { return sizeof(int64_t) * 9 * Q * kMT; }
+// Two fit masks at once (rows a and b), interleaved where a two-row block exists (C = 2).
+template <int C>
+__device__ __forceinline__ void fit_mask2(const int64_t (&a)[C], const int64_t (&b)[C],
+                                          const int64_t (&fr)[kMaxCards][C], uint64_t live,
+                                          uint32_t* ma, uint32_t* mb);
 
-// Pods with several selections (list `list`, kind SKIP = list - 1 dropped from the scans of
-// untouched cards): the selections in order (containers, then gpuNum), each taking the first
-// card that passes checkResourceCapacity (:341-383) with the pod's earlier takes (addRM,
-// resource_map.go:38-53) included.
-//   * Cards the pod has not taken from yet still hold the snapshot's free values, which stay
-//     in registers: one compare per (card, kind), the per-card verdicts packed into a lane
-//     bit mask bm (bit k = card k), masked by the cards not taken from (tm_not).
-//   * Cards it has taken from are the cards of the earlier selections (slots s < t); their
-//     current free lives in the lane's LDS column and is compared on every kind.
-//   * The selection is the lowest card of either set; taking it subtracts the need from the
-//     LDS column (ds_add_u64 of -need, no return).  After the pod the touched cards' columns
-//     are rewritten from the registers.
-// The per-lane state of one pod's selections: slot s = the card taken at selection s and the
-// LDS index of its column.
-struct MultiState {
-  uint32_t tm_not;  // bit k set: card k not taken from yet
-  uint32_t word;    // packed card ranks
-  bool fits;
-  int32_t slot_c[PAS_GAS_MAX_SELECTIONS];
-  int32_t slot_a[PAS_GAS_MAX_SELECTIONS];
-};
-
-// Selection T of the pod (recursion = full unroll, so slots are registers); returns when the
-// pod has no more selections or no node of the wave can still fit it.
-template <int Q, int SKIP, int T>
-__device__ __forceinline__ void multi_step(const int64_t (&free)[kMaxCards][Q], int64_t* cur,
-                                           int32_t tid, uint64_t live_mask, int32_t S,
-                                           const GasSel* rec, SelHead e, MultiState& st) {
-  if constexpr (T < PAS_GAS_MAX_SELECTIONS) {
-    if (T >= S) return;
-    if (e.bad) {  // a negative need fails every card (:343-347)
-      st.fits = false;
-      return;
-    }
-    // next record's scalar loads in flight during this selection
-    const SelHead en = sel_head<Q>(rec + min(T + 1, PAS_GAS_MAX_SELECTIONS - 1));
-    // untouched cards: snapshot free in registers; per card the kinds' compare masks and-ed
-    // in SALU (with the live lanes, so the mask is always a scalar result)
-    constexpr int kCompared = Q - (SKIP >= 0 ? 1 : 0);
-    uint32_t bm = 0u;
+// Bit mask of the cards k (bit k) with need[j] <= fr[k][j] for all C compared kinds.
+template <int C>
+__device__ __forceinline__ uint32_t fit_mask(const int64_t (&need)[C],
+                                             const int64_t (&fr)[kMaxCards][C], uint64_t live) {
+  uint32_t bm = 0u;
+  if constexpr (C == 1) {
+#ifdef PAS_C1_PERCARD
 #pragma unroll
     for (int k = kMaxCards - 1; k >= 0; --k) {
-      uint64_t m = ~0ull;
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (q != SKIP) m &= le_mask(e.cmp[q], free[k][q]);
-      if (kCompared == 1) m &= live_mask;  // one compare: an s_and makes the mask scalar
-      bm = push_bit(bm, m);
+      uint32_t r;
+      uint64_t m0, co;
+      asm("v_cmp_le_i64_e64 %1, %3, %4\n\t"
+          "s_and_b64 %1, %1, %5\n\t"
+          "v_addc_co_u32_e64 %0, %2, %6, %6, %1"
+          : "=&v"(r), "=&s"(m0), "=&s"(co)
+          : "v"(need[0]), "v"(fr[k][0]), "s"(live), "v"(bm)
+          : "scc");
+      bm = r;
     }
-    const uint32_t u = bm & st.tm_not;
-    uint32_t c = u ? (uint32_t)__builtin_ctz(u) : 8u;
-    // touched cards: current free in LDS, every kind
+#else
+    bm = push4_c1(bm, need[0], fr[7][0], fr[6][0], fr[5][0], fr[4][0], live);
+    bm = push4_c1(bm, need[0], fr[3][0], fr[2][0], fr[1][0], fr[0][0], live);
+#endif
+  } else if constexpr (C == 2) {
+    bm = push4_c2(bm, need[0], need[1], fr[7][0], fr[7][1], fr[6][0], fr[6][1], fr[5][0],
+                  fr[5][1], fr[4][0], fr[4][1]);
+    bm = push4_c2(bm, need[0], need[1], fr[3][0], fr[3][1], fr[2][0], fr[2][1], fr[1][0],
+                  fr[1][1], fr[0][0], fr[0][1]);
+  } else if constexpr (C == 3) {
 #pragma unroll
-    for (int sl = 0; sl < T; ++sl) {
-      bool ok = true;
+    for (int k = kMaxCards - 1; k > 0; k -= 2)
+      bm = push2_c3(bm, need[0], need[1], need[2], fr[k][0], fr[k][1], fr[k][2], fr[k - 1][0],
+                    fr[k - 1][1], fr[k - 1][2]);
+  } else {
 #pragma unroll
-      for (int q = 0; q < Q; ++q) ok &= e.cmp[q] <= cur[st.slot_a[sl] + q * kMT];
-      c = ok ? min(c, (uint32_t)st.slot_c[sl]) : c;
-    }
-    st.fits = st.fits && c < 8u;
-    if (!__ballot(st.fits)) return;  // no node of the wave fits the pod any more
-    st.slot_c[T] = (int32_t)c;
-    st.slot_a[T] = (int32_t)c * (Q * kMT) + tid;
+    for (int k = kMaxCards - 1; k > 0; k -= 2) bm = push2_c4(bm, need, fr[k], fr[k - 1]);
+  }
+  return bm;
+}
+
+constexpr int kMB = 8;  // multi-selection pods staged in LDS per round and wave
+constexpr int kRowChunks = PAS_GAS_MAX_SELECTIONS * (int)sizeof(GasSel) / 16;  // 16-B per row
+
+// Fit mask of the compared kinds (all but SKIP) of a threshold row: bit k = card k's snapshot
+// free passes every compared threshold.
+template <int C>
+__device__ __forceinline__ void fit_mask2(const int64_t (&a)[C], const int64_t (&b)[C],
+                                          const int64_t (&fr)[kMaxCards][C], uint64_t live,
+                                          uint32_t* ma, uint32_t* mb) {
+  if constexpr (C == 2) {
+    uint32_t x = 0u, y = 0u;
 #pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (e.take[q] != 0)
-        atomicAdd(reinterpret_cast<unsigned long long*>(&cur[st.slot_a[T] + q * kMT]),
-                  (unsigned long long)(-e.take[q]));
-    st.tm_not &= ~(1u << c);
-    st.word |= (c & 7u) << (3 * T);
-    multi_step<Q, SKIP, T + 1>(free, cur, tid, live_mask, S, rec, en, st);
+    for (int k = kMaxCards - 1; k > 0; k -= 2)
+      push2x2_c2(x, y, a[0], a[1], b[0], b[1], fr[k][0], fr[k][1], fr[k - 1][0], fr[k - 1][1]);
+    *ma = x;
+    *mb = y;
+  } else {
+    *ma = fit_mask<C>(a, fr, live);
+    *mb = fit_mask<C>(b, fr, live);
   }
 }
 
-// Pods with several selections (list `list`, kind SKIP = list - 1 dropped from the scans of
-// untouched cards): the selections in order (containers, then gpuNum), each taking the first
-// card that passes checkResourceCapacity (:341-383) with the pod's earlier takes (addRM,
-// resource_map.go:38-53) included.
-//   * Cards the pod has not taken from yet still hold the snapshot's free values, which stay
-//     in registers: one compare per (card, kind), the per-card verdicts packed into a lane
-//     bit mask bm (bit k = card k), masked by the cards not taken from (tm_not).
-//   * Cards it has taken from are the cards of the earlier selections (slots s < t); their
-//     current free lives in the lane's LDS column and is compared on every kind.
-//   * The selection is the lowest card of either set; taking it subtracts the need from the
-//     LDS column (ds_add_u64 of -need, no return).  After the pod the touched cards' columns
-//     are rewritten from the registers.
+template <int Q, int SKIP>
+__device__ __forceinline__ uint32_t th_mask(const int64_t (&free)[kMaxCards][Q], const int64_t* th,
+                                            uint64_t live) {
+  constexpr int kSkip = Q == 1 ? -1 : SKIP;  // a selection's only kind is never skipped
+  constexpr int kC = Q - (kSkip >= 0 ? 1 : 0);
+  int64_t need[kC];
+  int64_t fr[kMaxCards][kC];
+#pragma unroll
+  for (int q = 0, j = 0; q < Q; ++q)
+    if (q != kSkip) need[j++] = th[q];
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != kSkip) fr[k][j++] = free[k][q];
+  return fit_mask<kC>(need, fr, live);
+}
+
+template <int Q, int SKIP>
+__device__ __forceinline__ void th_mask2(const int64_t (&free)[kMaxCards][Q], const int64_t* ta,
+                                         const int64_t* tb, uint64_t live, uint32_t* ma,
+                                         uint32_t* mb) {
+  constexpr int kSkip = Q == 1 ? -1 : SKIP;
+  constexpr int kC = Q - (kSkip >= 0 ? 1 : 0);
+  int64_t a[kC], b[kC];
+  int64_t fr[kMaxCards][kC];
+#pragma unroll
+  for (int q = 0, j = 0; q < Q; ++q)
+    if (q != kSkip) {
+      a[j] = ta[q];
+      b[j++] = tb[q];
+    }
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != kSkip) fr[k][j++] = free[k][q];
+  fit_mask2<kC>(a, b, fr, live, ma, mb);
+}
+
+__device__ __forceinline__ uint32_t lowest(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : 8u; }
+__device__ __forceinline__ uint32_t bit(uint32_t m, uint32_t k) { return (m >> k) & 1u; }
+
+// A pod with 2 or 3 selections, in closed form.  Selection t takes the first card whose free
+// covers its need plus the takes already on that card (addRM, resource_map.go:38-53); which
+// earlier takes those are depends only on the earlier choices, so every combination is one
+// threshold row of the snapshot free values (GasThresholds) and each row is one fit mask:
+//   c0 = lowest(m0)
+//   c1 = min(lowest(m1 without c0), c0 if m2 has c0)
+//   c2 = min(lowest(m3 without c0, c1),
+//            c0 == c1 ? (c0 if m6 has c0) : min(c0 if m4 has c0, c1 if m5 has c1))
+// The masks are independent of each other (no per-lane state, no dependent chain).
+template <int Q, int SKIP>
+__device__ __forceinline__ uint32_t multi_closed(const int64_t (&free)[kMaxCards][Q],
+                                                 const GasThresholds& t, int32_t S,
+                                                 uint64_t live, uint32_t node_ok) {
+  // every row read before the masks (one LDS round trip), masks without branches: an
+  // overflowing threshold's mask is computed and cleared
+  const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
+  const int rows = S == 3 ? 7 : 3;
+  int64_t th[7][Q];
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) th[j][q] = j < 3 || S == 3 ? t.th[j][q] : 0;
+  uint32_t m[7];
+  th_mask2<Q, SKIP>(free, th[0], th[1], live, &m[0], &m[1]);
+  m[2] = th_mask<Q, SKIP>(free, th[2], live);
+  if (rows == 7) {
+    th_mask2<Q, SKIP>(free, th[3], th[4], live, &m[3], &m[4]);
+    th_mask2<Q, SKIP>(free, th[5], th[6], live, &m[5], &m[6]);
+  } else {
+    m[3] = m[4] = m[5] = m[6] = 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+    if ((over >> j) & 1) m[j] = 0u;  // an overflowing threshold passes no card
+  const uint32_t c0 = lowest(m[0]);
+  const uint32_t c1 = min(lowest(m[1] & ~(1u << c0)), bit(m[2], c0) ? c0 : 8u);
+  uint32_t word = c0 | (c1 << 3);
+  bool fits = c0 < 8u && c1 < 8u;
+  if (S == 3) {
+    const uint32_t untouched = lowest(m[3] & ~(1u << c0) & ~(1u << c1));
+    const uint32_t touched =
+        c0 == c1 ? (bit(m[6], c0) ? c0 : 8u)
+                 : min(bit(m[4], c0) ? c0 : 8u, bit(m[5], c1) ? c1 : 8u);
+    const uint32_t c2 = min(untouched, touched);
+    fits = fits && c2 < 8u;
+    word |= c2 << 6;
+  }
+  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
+// A pod with 4 to 8 selections: the selections in order on a working copy of the free values
+// (registers), each a fit mask on the copy; the chosen card's copy drops by the take, updated
+// under the lanes that chose it (one branch per card some lane chose).
+template <int Q, int SKIP>
+__device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards][Q],
+                                                const GasSel* rec, int32_t S, uint64_t live,
+                                                uint32_t node_ok) {
+  typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+  int64_t w[kMaxCards][Q];
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
+  bool fits = true;
+  uint32_t word = 0u;
+  for (int32_t t = 0; t < S; ++t) {
+    int64_t cmp[Q], neg[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const v2i64 ct = *reinterpret_cast<const v2i64*>(rec[t].ct[q]);
+      cmp[q] = ct.x;
+      neg[q] = ct.y;
+    }
+    const uint32_t c = lowest(th_mask<Q, SKIP>(w, cmp, live));
+    fits = fits && c < 8u;
+    if (!__ballot(fits)) break;
+#pragma unroll
+    for (int kk = 0; kk < kMaxCards; ++kk)
+      if (__ballot(c == (uint32_t)kk) && c == (uint32_t)kk)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) w[kk][q] += neg[q];
+    word |= (c & 7u) << (3 * t);
+  }
+  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
+// Pods with several selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
+// the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
+// reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
+// waiting for its copy does not hold up the other waves of the block.
 template <int Q, int SKIP, bool kBits>
-__device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], int64_t* cur,
-                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
-                                           const int32_t* __restrict__ list,
+__device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
+                                           int32_t* stage_w, uint32_t node_ok, int32_t N,
+                                           int32_t n, bool valid, const int32_t* __restrict__ list,
                                            const GasSel* __restrict__ sels,
                                            const int32_t* __restrict__ count, const BlockTile& bt,
                                            uint32_t* __restrict__ res,
                                            uint64_t* __restrict__ fit) {
-  const int32_t tid = threadIdx.x;
-  const bool live = valid && node_ok != 0u;
-  const uint64_t live_mask = __ballot(live);
+  const int32_t lane = threadIdx.x & 63;
+  const uint64_t live = __ballot(valid && node_ok != 0u);
   int32_t i0, i1;
   list_share(count, bt, &i0, &i1);
-  for (int32_t i = i0; i < i1; ++i) {
-    const int32_t pw = list[i];
-    const int64_t pod = pw & 0xFFFFFF;
-    const int32_t S = pw >> 24;
-    uint32_t out = 0u;
-    if (S <= PAS_GAS_MAX_SELECTIONS) {
-      const GasSel* rec = sels + pod * PAS_GAS_MAX_SELECTIONS;
-      MultiState st;
-      st.tm_not = 0xFFu;
-      st.word = 0u;
-      st.fits = live;
-      multi_step<Q, SKIP, 0>(free, cur, tid, live_mask, S, rec, sel_head<Q>(rec), st);
-      out = st.fits ? (node_ok | ((uint32_t)S << 24) | st.word) : 0u;
-      // restore the touched cards' columns
+  for (int32_t b0 = i0; b0 < i1; b0 += kMB) {
+    const int32_t nb = min(kMB, i1 - b0);
+    // every load of the batch in flight before the LDS writes (rows past nb: not read)
+    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * PAS_GAS_MAX_SELECTIONS);
+    constexpr int kIters = kMB * kRowChunks / 64;
+    int4 v[kIters];
 #pragma unroll
-      for (int k = 0; k < kMaxCards; ++k) {
-        const bool touched = !((st.tm_not >> k) & 1u);
-        if (__ballot(touched) && touched)
-#pragma unroll
-          for (int q = 0; q < Q; ++q) cur[(k * Q + q) * kMT + tid] = free[k][q];
-      }
+    for (int it = 0; it < kIters; ++it) {
+      const int32_t c = lane + it * 64;
+      v[it] = c < nb * kRowChunks ? src[c] : int4{0, 0, 0, 0};
     }
-    put_result<kBits>(res, fit, pod, N, n, valid, out);
+    const int32_t wd = lane < nb ? list[b0 + lane] : 0;
+    __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
+    if (lane < nb) stage_w[lane] = wd;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    for (int32_t j = 0; j < nb; ++j) {
+      const int32_t pw = __builtin_amdgcn_readfirstlane(stage_w[j]);
+      const int32_t pod = pw & 0xFFFFFF;
+      const int32_t S = (pw >> 24) & 0xF;
+      const GasSel* rec = stage + j * PAS_GAS_MAX_SELECTIONS;
+      uint32_t out = 0u;
+      if (!(pw & kBadPod)) {
+        if (S <= 3)
+          out = multi_closed<Q, SKIP>(free, *reinterpret_cast<const GasThresholds*>(rec), S, live,
+                                      node_ok);
+        else if (S <= PAS_GAS_MAX_SELECTIONS)
+          out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
+      }
+      put_result<kBits>(res, fit, pod, N, n, valid, out);
+    }
   }
 }
 
 template <int Q, bool kBits, int L = 0>
-__device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], int64_t* cur,
-                                            uint32_t node_ok, int32_t N, int32_t n, bool valid,
-                                            int32_t P, const int32_t* __restrict__ multi,
+__device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
+                                            int32_t* stage_w, uint32_t node_ok, int32_t N,
+                                            int32_t n, bool valid, int32_t P,
+                                            const int32_t* __restrict__ multi,
                                             const GasSel* __restrict__ sels,
                                             const int32_t* __restrict__ counts,
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
-  multi_list<Q, L - 1, kBits>(free, cur, node_ok, N, n, valid, multi + (int64_t)L * P, sels,
-                              counts + L, bt, res, fit);
+  multi_list<Q, L - 1, kBits>(free, stage, stage_w, node_ok, N, n, valid, multi + (int64_t)L * P,
+                              sels + (int64_t)L * P * PAS_GAS_MAX_SELECTIONS, counts + L, bt,
+                              res, fit);
   if constexpr (L < Q)
-    multi_lists<Q, kBits, L + 1>(free, cur, node_ok, N, n, valid, P, multi, sels, counts, bt,
-                                 res, fit);
+    multi_lists<Q, kBits, L + 1>(free, stage, stage_w, node_ok, N, n, valid, P, multi, sels,
+                                 counts, bt, res, fit);
 }
 
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kMT) void gas_fit_multi_kernel(
+__global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
     const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
     const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
     uint64_t* __restrict__ fit) {
-  extern __shared__ __attribute__((aligned(16))) int64_t cur[];
+  __shared__ GasSel stage[kTpb / 64][PAS_GAS_MAX_SELECTIONS * kMB];  // a slice per wave
+  __shared__ int32_t stage_w[kTpb / 64][kMB];
   const BlockTile bt = block_tile(chunks);
-  const int32_t n = bt.node_block * kMT + threadIdx.x;
+  const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   int64_t free[kMaxCards][Q];
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) cur[(k * Q + q) * kMT + threadIdx.x] = free[k][q];
   const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
-  multi_lists<Q, kBits>(free, cur, node_ok, N, n, valid, P, multi, sels, counts, bt, res, fit);
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  multi_lists<Q, kBits>(free, stage[wave], stage_w[wave], node_ok, N, n, valid, P, multi, sels,
+                        counts, bt, res, fit);
 }
 
 }  // namespace
@@ -614,13 +886,14 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
   if (N == 0 || n_pods == 0) return PAS_OK;
   // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][P] | their
-  // selection rows [P][8] | the flipped kind minima [4] and counts [2(Q+1)] (zeroed together)
+  // selection rows [Q+1][P][8] | the flipped kind minima [4] and counts [2(Q+1)] (zeroed
+  // together)
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   const int32_t NL = Q + 1;
   const size_t b_single = (sizeof(GasSingle) * (size_t)NL * n_pods + 255) & ~size_t(255);
   const size_t b_multi = (sizeof(int32_t) * (size_t)NL * n_pods + 255) & ~size_t(255);
   const size_t b_sels =
-      (sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS * (size_t)n_pods + 255) & ~size_t(255);
+      (sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS * (size_t)NL * n_pods + 255) & ~size_t(255);
   constexpr size_t b_tail = 2 * (PAS_GAS_MAX_RES + 1) * sizeof(int32_t) +
                             PAS_GAS_MAX_RES * sizeof(unsigned long long);
   const size_t need = b_single + b_multi + b_sels + b_tail;
@@ -651,12 +924,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
       multi, sels, counts);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
-  // grids: (node block, pod chunk) pairs, ~4096 blocks for the single kernel and ~8192 for
-  // the multi kernel (half the nodes per block); each kernel splits each of its
+  // grids: (node block, pod chunk) pairs, ~4096 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
-  const int32_t nb_s = (N + kTpb - 1) / kTpb, nb_m = (N + kMT - 1) / kMT;
+  const int32_t nb_s = (N + kTpb - 1) / kTpb;
   const int32_t ch_s = std::max(1, std::min(n_pods, (4096 + nb_s - 1) / nb_s));
-  const int32_t ch_m = std::max(1, std::min(n_pods, (8192 + nb_m - 1) / nb_m));
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
   switch (Q * 2 + (bits ? 1 : 0)) {
@@ -664,8 +935,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   case QQ * 2 + B:                                                                             \
     gas_fit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                 \
         N, K, n_pods, g.n_cards, g.cap, g.used, single, counts, ch_s, d_res, d_fit);           \
-    gas_fit_multi_kernel<QQ, B><<<nb_m * ch_m, kMT, multi_lds_bytes<QQ>(), s>>>(               \
-        N, K, n_pods, g.n_cards, g.cap, g.used, multi, sels, counts + NL, ch_m, d_res, d_fit); \
+    gas_fit_multi_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                  \
+        N, K, n_pods, g.n_cards, g.cap, g.used, multi, sels, counts + NL, ch_s, d_res, d_fit); \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
