@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PAS_ABI_VERSION 1
+#define PAS_ABI_VERSION 2
 
 typedef enum pas_status {
   PAS_OK = 0,
@@ -214,9 +214,27 @@ int pas_label_patch_json(int32_t n_strategies, const char* const* names, uint64_
 /* GPU Aware Scheduling                                                      */
 /* ------------------------------------------------------------------------- */
 
-#define PAS_GAS_MAX_CARDS 8      /* cards per node held in registers */
-#define PAS_GAS_MAX_RES 4        /* gpu.intel.com/ resource kinds per batch */
-#define PAS_GAS_MAX_SELECTIONS 8 /* sum over containers of i915 count per pod */
+#define PAS_GAS_MAX_CARDS 64      /* cards per node (label gpu.intel.com/cards entries) */
+#define PAS_GAS_MAX_RES 4         /* gpu.intel.com/ resource kinds per batch */
+#define PAS_GAS_MAX_SELECTIONS 64 /* card selections per pod: sum over containers of i915 */
+#define PAS_GAS_PACKED 8          /* selections / card ranks the packed result word holds */
+/* bits 24-27 of a result word besides a count S <= PAS_GAS_PACKED: */
+#define PAS_GAS_SEL_EXTENDED 15   /* the pod fits (bit 31 set) but its card selection does not
+                                     pack: more than 8 selections or a card rank >= 8; the
+                                     selection is in the side buffer of pas_gas_fit_ex */
+#define PAS_GAS_SEL_LIMIT 14      /* more than PAS_GAS_MAX_SELECTIONS selections: not evaluated
+                                     (bit 31 clear), counted by pas_gas_limit_count */
+
+/* Card selection of one (pod, node) that does not fit the packed word (PAS_GAS_SEL_EXTENDED):
+ * card[0 .. n_sel) are the ranks of the node's cards, selection by selection (containers in
+ * order), i.e. the "gas-container-cards" annotation (:317-335). */
+typedef struct pas_gas_selection {
+  int32_t pod;
+  int32_t node;
+  int32_t n_sel;
+  int32_t reserved;
+  uint8_t card[PAS_GAS_MAX_SELECTIONS];
+} pas_gas_selection;
 
 /* Frozen allocation snapshot (Cache.getNodeResourceStatus,
  * gpuscheduler/node_resource_cache.go:474-491) in node-major SoA:
@@ -231,7 +249,7 @@ int pas_label_patch_json(int32_t n_strategies, const char* const* names, uint64_
  *                                       (sort.Strings, :216-224) order of card name;
  *                                       cards in the usage map but not in the label are
  *                                       left out (skipped at :230-234)
- * max_cards <= PAS_GAS_MAX_CARDS, n_res <= PAS_GAS_MAX_RES. */
+ * max_cards <= PAS_GAS_MAX_CARDS (64), n_res <= PAS_GAS_MAX_RES. */
 int pas_gas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
                          int32_t n_res, const int32_t* n_cards, const int64_t* cap_per_gpu,
                          const int64_t* used);
@@ -251,17 +269,41 @@ int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
  *   n_containers [n_pods]
  * Output res_out[n_pods][n_nodes], one word per (pod, node):
  *   bit 31     the pod fits (node passes GASExtender.filterNodes, :467-473)
- *   bits 24-27 number of card selections S (= sum of per-container i915 counts)
+ *   bits 24-27 number of card selections S (= sum of per-container i915 counts) when
+ *              S <= 8 and every selected card rank is < 8; else PAS_GAS_SEL_EXTENDED
+ *              (fits, selection in pas_gas_fit_ex's side buffer) or PAS_GAS_SEL_LIMIT
  *   bits 0-23  S 3-bit card ranks (lexicographic index into the node's cards),
  *              selection j at bits 3j..3j+2, containers in order, i.e. the
- *              "gas-container-cards" annotation (:317-335) in packed form.
- * PAS_ECAPACITY if a pod needs more than PAS_GAS_MAX_SELECTIONS selections. */
+ *              "gas-container-cards" annotation (:317-335) in packed form; 0 otherwise.
+ * The reference has no limit on selections per pod or cards per node (scheduler.go:200-257;
+ * the GPU plugin's -shared-dev-num lets one card take many selections); here nodes may have
+ * up to PAS_GAS_MAX_CARDS cards and pods up to PAS_GAS_MAX_SELECTIONS selections.  The host
+ * call returns PAS_ECAPACITY for a pod beyond that; the _device calls mark its words
+ * PAS_GAS_SEL_LIMIT (bitmap bits 0) and count the pods (pas_gas_limit_count). */
 int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out);
 int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
                        int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
                        const int32_t* d_n_containers, uint32_t* d_res_out, void* hip_stream);
+
+/* pas_gas_fit plus the side buffer of the selections that do not pack: side[0 .. cap) gets
+ * one record per PAS_GAS_SEL_EXTENDED word (in no particular order); *side_count = the number
+ * of such words (records beyond cap are dropped: call again with a larger buffer). */
+int pas_gas_fit_ex(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                   int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                   const int32_t* n_containers, uint32_t* res_out, pas_gas_selection* side,
+                   int64_t side_cap, int64_t* side_count);
+/* d_side_count: device int64, zeroed by the call, then the count (read it after the stream). */
+int pas_gas_fit_ex_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                          int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
+                          const int32_t* d_n_containers, uint32_t* d_res_out,
+                          pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
+                          void* hip_stream);
+
+/* Pods of the last GAS fit call on this context beyond PAS_GAS_MAX_SELECTIONS (their words
+ * are PAS_GAS_SEL_LIMIT, their bitmap bits 0).  Waits for the call's stream. */
+int pas_gas_limit_count(pas_ctx* ctx, int64_t* n_pods_out);
 
 /* GAS filter verdicts only, as node bitmaps fit_out[n_pods][W64(n_nodes)] (bit = bit 31 of
  * the pas_gas_fit word).  Used to intersect GAS with TAS candidates (cand of the TAS calls)
@@ -288,11 +330,20 @@ int pas_gas_bind(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_bin
                  int32_t max_containers, int32_t i915_index, const int64_t* req,
                  const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
                  int32_t* status_out);
+/* pas_gas_bind plus every bind's full card selection: cards_out[b][0 .. n_sel_out[b]) (ranks,
+ * selection by selection; n_sel_out 0 when it does not fit), for selections that do not
+ * pack into the result word. */
+int pas_gas_bind_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
+                    const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
+                    int32_t max_containers, int32_t i915_index, const int64_t* req,
+                    const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
+                    int32_t* status_out, uint8_t* cards_out /*[n_binds][64]*/,
+                    int32_t* n_sel_out);
 
 /* Pods leaving nodes: Cache.adjustPodResources(remove) (node_resource_cache.go:240-287) with
  * each pod's annotation, in call order.  Container c of release r has cards_per_container
  * [r][c] cards (its "gas-container-cards" segment), listed in container order in
- * cards[r][8] as ranks into the node's cards; request / count is subtracted from each card
+ * cards[r][8] (at most 8 in all; pas_gas_release_ex: 64) as ranks into the node's cards; request / count is subtracted from each card
  * (subtractRM, resource_map.go:55-73,103-127: clamp at 0; a negative amount, or a card the
  * node's label does not list, is an input error and nothing changes).  The snapshot keeps
  * no "key absent" state: a label card has every kind, so subtracting from a kind that was
@@ -302,6 +353,12 @@ int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_
                     int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
                     const int32_t* n_containers, const int32_t* cards_per_container,
                     const int32_t* cards, int32_t* status_out);
+/* pas_gas_release with cards[r][PAS_GAS_MAX_SELECTIONS] (annotations of up to 64 cards). */
+int pas_gas_release_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
+                       const int32_t* rel_pod, const int32_t* rel_node, int32_t n_pods,
+                       int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
+                       const int32_t* n_containers, const int32_t* cards_per_container,
+                       const int32_t* cards, int32_t* status_out);
 
 /* Read back the resident usage used[N][K][Q] and its generation. */
 int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out);

@@ -52,12 +52,14 @@ def load():
         "or_rm_subtract_rm": (c_int, [POINTER(OrRm), POINTER(OrRm)]),
         "or_rm_divide": (c_int, [POINTER(OrRm), c_int32]),
         "or_check_resource_capacity": (c_int, [POINTER(OrRm), POINTER(OrRm), POINTER(OrRm)]),
+        "or_gas_fit_ex": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
+                                  P, P, P, P, P, P]),
         "or_gas_fit": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
                                P, P, P, P]),
         "or_gas_bind": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, P, P, c_int32,
-                                c_int32, P, P, P, P, P]),
+                                c_int32, P, P, P, P, P, P, P]),
         "or_gas_release": (c_int, [c_int32, c_int32, c_int32, P, P, c_int32, P, P, c_int32,
-                                   P, P, P, P, P, P]),
+                                   P, P, P, P, P, c_int32, P]),
         "or_label_plan": (c_int, [c_int32, c_int32, P, P, P, P, P]),
         "or_label_patch_json": (c_int64, [c_int32, P, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_char_p, c_int64]),
@@ -121,7 +123,13 @@ def tas_violations(v_milli, present, rules, rule_off):
     return out
 
 
-def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index):
+MAX_SEL = 64  # OR_GAS_MAX_SEL
+SEL_EXTENDED = 15
+SEL_LIMIT = 14
+
+
+def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index, selections=False):
+    """Result words [P][N]; with selections=True also (sel [P][N][64] uint8, nsel [P][N])."""
     n_cards = np.ascontiguousarray(n_cards, np.int32)
     cap = np.ascontiguousarray(cap, np.int64)
     used = np.ascontiguousarray(used, np.int64)
@@ -131,16 +139,20 @@ def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index):
     n, k, q = used.shape
     p, c, _ = req.shape
     out = np.zeros((p, n), np.uint32)
-    rc = load().or_gas_fit(n, k, q, _p(n_cards), _p(cap), _p(used), p, c, i915_index, _p(req),
-                           _p(req_mask), _p(n_containers), _p(out))
+    sel = np.zeros((p, n, MAX_SEL), np.uint8) if selections else None
+    nsel = np.zeros((p, n), np.int32) if selections else None
+    rc = load().or_gas_fit_ex(n, k, q, _p(n_cards), _p(cap), _p(used), p, c, i915_index,
+                              _p(req), _p(req_mask), _p(n_containers), _p(out), _p(sel),
+                              _p(nsel))
     if rc != 0:
         raise ValueError(f"oracle gas_fit failed: {rc}")
-    return out
+    return (out, sel, nsel) if selections else out
 
 
-def gas_bind(n_cards, cap, used, req, req_mask, n_containers, i915_index, pods, nodes):
+def gas_bind(n_cards, cap, used, req, req_mask, n_containers, i915_index, pods, nodes,
+             selections=False):
     """Binds in order (bindNode: runSchedulingLogic + adjustPodResources(add)).
-    Returns (used after, result words, statuses)."""
+    Returns (used after, result words, statuses) [+ (cards [B][64], nsel [B])]."""
     n_cards = np.ascontiguousarray(n_cards, np.int32)
     cap = np.ascontiguousarray(cap, np.int64)
     used = np.array(used, np.int64, copy=True, order="C")
@@ -154,17 +166,20 @@ def gas_bind(n_cards, cap, used, req, req_mask, n_containers, i915_index, pods, 
     b = len(pods)
     res = np.zeros(b, np.uint32)
     st = np.zeros(b, np.int32)
+    cards = np.zeros((b, MAX_SEL), np.uint8)
+    nsel = np.zeros(b, np.int32)
     rc = load().or_gas_bind(n, k, q, _p(n_cards), _p(cap), _p(used), b, _p(pods), _p(nodes), c,
                             i915_index, _p(req), _p(req_mask), _p(n_containers), _p(res),
-                            _p(st))
+                            _p(st), _p(cards), _p(nsel))
     if rc != 0:
         raise ValueError(f"oracle gas_bind failed: {rc}")
-    return used, res, st
+    return (used, res, st, cards, nsel) if selections else (used, res, st)
 
 
 def gas_release(n_cards, used, req, req_mask, n_containers, pods, nodes, cards_per_container,
                 cards):
-    """Pods leaving nodes (adjustPodResources(remove)).  Returns (used after, statuses)."""
+    """Pods leaving nodes (adjustPodResources(remove)).  cards [R][8] or [R][64].
+    Returns (used after, statuses)."""
     n_cards = np.ascontiguousarray(n_cards, np.int32)
     used = np.array(used, np.int64, copy=True, order="C")
     req = np.ascontiguousarray(req, np.int64)
@@ -173,14 +188,14 @@ def gas_release(n_cards, used, req, req_mask, n_containers, pods, nodes, cards_p
     pods = np.ascontiguousarray(pods, np.int32)
     nodes = np.ascontiguousarray(nodes, np.int32)
     cpc = np.ascontiguousarray(cards_per_container, np.int32)
-    cards = np.ascontiguousarray(cards, np.int32)
+    r = len(pods)
+    cards = np.ascontiguousarray(cards, np.int32).reshape(r, -1)
     n, k, q = used.shape
     c = req.shape[1]
-    r = len(pods)
     st = np.zeros(r, np.int32)
     rc = load().or_gas_release(n, k, q, _p(n_cards), _p(used), r, _p(pods), _p(nodes), c,
                                _p(req), _p(req_mask), _p(n_containers), _p(cpc), _p(cards),
-                               _p(st))
+                               cards.shape[1] if r else 8, _p(st))
     if rc != 0:
         raise ValueError(f"oracle gas_release failed: {rc}")
     return used, st

@@ -357,23 +357,50 @@ int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const o
 
 /* ---- GAS runSchedulingLogic over the packed snapshot ---------------------- */
 
+/* The pod's card selections (getNumI915 summed over its containers, :192-198, 280-338),
+ * saturating past OR_GAS_MAX_SEL. */
+static int64_t pod_selections(int32_t n_res, int32_t i915_index, int32_t max_containers,
+                              const int64_t* req, const uint32_t* req_mask,
+                              int32_t n_containers, int32_t p) {
+  int64_t sel = 0;
+  for (int32_t c = 0; c < n_containers; ++c) {
+    const int64_t base = (int64_t)p * max_containers + c;
+    const uint32_t mask = req_mask[base];
+    if (mask == 0 || i915_index < 0 || !(mask >> i915_index & 1u)) continue;
+    const int64_t v = req[base * n_res + i915_index];
+    if (v > 0) sel += v > OR_GAS_MAX_SEL ? OR_GAS_MAX_SEL + 1 : v;
+    if (sel > OR_GAS_MAX_SEL) return OR_GAS_MAX_SEL + 1;
+  }
+  return sel;
+}
+
 /* Builds the reference's maps from the packed layout: capacity has every resource kind
  * with a positive per-GPU value... careful: a kind whose per-GPU capacity is 0 may
  * still be a key of the capacity map, but checkResourceCapacity treats "missing" and
  * "<= 0" identically (:349-354), so has = 1 with the stored value is equivalent. */
-int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
-               const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
-               int32_t max_containers, int32_t i915_index, const int64_t* req,
-               const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out) {
-  if (max_cards > 8 || n_res > OR_RM_MAX_KEYS) return -1;
-  or_rm node_used[8];
+int or_gas_fit_ex(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+                  const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
+                  int32_t max_containers, int32_t i915_index, const int64_t* req,
+                  const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
+                  uint8_t* sel_out, int32_t* nsel_out) {
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_RM_MAX_KEYS) return -1;
+  or_rm node_used[OR_GAS_MAX_CARDS];
+  uint8_t sel[OR_GAS_MAX_SEL];
   for (int32_t p = 0; p < n_pods; ++p) {
+    const int64_t total = pod_selections(n_res, i915_index, max_containers, req, req_mask,
+                                         n_containers[p], p);
     for (int32_t n = 0; n < n_nodes; ++n) {
-      uint32_t word = 0;
+      const int64_t pn = (int64_t)p * n_nodes + n;
+      if (nsel_out) nsel_out[pn] = 0;
+      if (total > OR_GAS_MAX_SEL) {                 /* beyond the build's documented limit */
+        res_out[pn] = (uint32_t)OR_GAS_SEL_LIMIT << 24;
+        continue;
+      }
       int fits = 1;
       int32_t nsel = 0;
       /* iCache.FetchNode error (:282-288) / no cards label -> errWontFit (:290-298) */
       if (n_cards[n] <= 0) fits = 0;
+      const int32_t ncard = n_cards[n] < max_cards ? n_cards[n] : max_cards;
       or_rm capacity;
       memset(&capacity, 0, sizeof capacity);
       if (fits) {
@@ -383,7 +410,7 @@ int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t*
         }
         /* readNodeResources deep copy (node_resource_cache.go:474-491) +
          * addEmptyResourceMaps (:269-275): a fresh copy per (pod, node) */
-        for (int32_t k = 0; k < n_cards[n]; ++k) {
+        for (int32_t k = 0; k < ncard; ++k) {
           memset(&node_used[k], 0, sizeof(or_rm));
           for (int32_t q = 0; q < n_res; ++q) {
             const int64_t u = used[((int64_t)n * max_cards + k) * n_res + q];
@@ -408,12 +435,11 @@ int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t*
           int fitted = 0;
           /* cards in sort.Strings order; stale cards are absent from the packed snapshot,
            * which equals skipping them (!gpuMap[gpuName] -> continue, :230-234) */
-          for (int32_t k = 0; k < n_cards[n]; ++k) {
+          for (int32_t k = 0; k < ncard; ++k) {
             if (or_check_resource_capacity(&per_gpu, &capacity, &node_used[k])) {
               if (or_rm_add_rm(&node_used[k], &per_gpu) == OR_RM_OK) {
                 fitted = 1;
-                if (nsel < 8) word |= (uint32_t)k << (3 * nsel);
-                ++nsel;                         /* cards = append(cards, gpuName) */
+                sel[nsel++] = (uint8_t)k;       /* cards = append(cards, gpuName) */
               }
               break;
             }
@@ -421,12 +447,32 @@ int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t*
           if (!fitted) { fits = 0; break; }    /* errWontFit :249-253 */
         }
       }
-      if (nsel > 8) return -2;                  /* beyond the packed encoding */
-      res_out[(int64_t)p * n_nodes + n] =
-          fits ? (0x80000000u | ((uint32_t)nsel << 24) | word) : 0u;
+      uint32_t word = 0;
+      if (fits) {
+        int packable = nsel <= 8;
+        for (int32_t j = 0; j < nsel; ++j) packable = packable && sel[j] < 8;
+        if (packable) {
+          word = 0x80000000u | ((uint32_t)nsel << 24);
+          for (int32_t j = 0; j < nsel; ++j) word |= (uint32_t)sel[j] << (3 * j);
+        } else {
+          word = 0x80000000u | ((uint32_t)OR_GAS_SEL_EXTENDED << 24);
+        }
+        if (sel_out) memcpy(sel_out + pn * OR_GAS_MAX_SEL, sel, (size_t)nsel);
+        if (nsel_out) nsel_out[pn] = nsel;
+      }
+      res_out[pn] = word;
     }
   }
   return 0;
+}
+
+int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+               const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
+               int32_t max_containers, int32_t i915_index, const int64_t* req,
+               const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out) {
+  return or_gas_fit_ex(n_nodes, max_cards, n_res, n_cards, cap_per_gpu, used, n_pods,
+                       max_containers, i915_index, req, req_mask, n_containers, res_out, NULL,
+                       NULL);
 }
 
 /* ---- GAS bind-time commit ------------------------------------------------- */
@@ -454,25 +500,31 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
                 const int64_t* cap_per_gpu, int64_t* used, int32_t n_binds,
                 const int32_t* bind_pod, const int32_t* bind_node, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
-                const int32_t* n_containers, uint32_t* res_out, int32_t* status) {
-  if (max_cards > 8 || n_res > OR_RM_MAX_KEYS) return -1;
+                const int32_t* n_containers, uint32_t* res_out, int32_t* status,
+                uint8_t* cards_out, int32_t* nsel_out) {
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_RM_MAX_KEYS) return -1;
   for (int32_t b = 0; b < n_binds; ++b) {
     const int32_t p = bind_pod[b], n = bind_node[b];
     if (n < 0 || n >= n_nodes) return -1;
     int64_t* u = used + (int64_t)n * max_cards * n_res;
     uint32_t word = 0;
+    uint8_t sel[OR_GAS_MAX_SEL];
+    int32_t nsel = 0;
+    if (cards_out) memset(cards_out + (int64_t)b * OR_GAS_MAX_SEL, 0, OR_GAS_MAX_SEL);
+    if (nsel_out) nsel_out[b] = 0;
     /* runSchedulingLogic(pod, node) on the current usage */
-    if (or_gas_fit(1, max_cards, n_res, n_cards + n, cap_per_gpu + (int64_t)n * n_res, u, 1,
-                   max_containers, i915_index, req + (int64_t)p * max_containers * n_res,
-                   req_mask + (int64_t)p * max_containers, n_containers + p, &word) != 0)
+    if (or_gas_fit_ex(1, max_cards, n_res, n_cards + n, cap_per_gpu + (int64_t)n * n_res, u, 1,
+                      max_containers, i915_index, req + (int64_t)p * max_containers * n_res,
+                      req_mask + (int64_t)p * max_containers, n_containers + p, &word, sel,
+                      &nsel) != 0)
       return -2;
     res_out[b] = word;
     if (!(word >> 31)) { status[b] = OR_GAS_WONT_FIT; continue; }
     /* adjustPodResources(add): the annotation lists, per container, the cards of its
      * selections (numCards = numI915); checked on a copy, then applied */
-    or_rm maps[8];
+    or_rm maps[OR_GAS_MAX_CARDS];
     node_maps(max_cards, n_res, n_cards[n], u, maps);
-    int32_t sel = 0, err = OR_RM_OK;
+    int32_t s_i = 0, err = OR_RM_OK;
     for (int32_t c = 0; c < n_containers[p] && !err; ++c) {
       const int64_t base = (int64_t)p * max_containers + c;
       or_rm r;
@@ -482,8 +534,8 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
         k_c = r.val[i915_index];
       if (k_c <= 0) continue;                       /* empty segment: skipped */
       or_rm_divide(&r, (int32_t)k_c);
-      for (int64_t g = 0; g < k_c && !err; ++g, ++sel)
-        err = or_rm_add_rm(&maps[(word >> (3 * sel)) & 7], &r);
+      for (int64_t g = 0; g < k_c && !err; ++g, ++s_i)
+        err = or_rm_add_rm(&maps[sel[s_i]], &r);
     }
     if (err) {                                       /* nothing changes */
       status[b] = err == OR_RM_ERR_OVERFLOW ? OR_GAS_ERR_OVERFLOW : OR_GAS_ERR_INPUT;
@@ -491,6 +543,8 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
     }
     for (int32_t k = 0; k < n_cards[n]; ++k)
       for (int32_t q = 0; q < n_res; ++q) u[(int64_t)k * n_res + q] = maps[k].val[q];
+    if (cards_out) memcpy(cards_out + (int64_t)b * OR_GAS_MAX_SEL, sel, (size_t)nsel);
+    if (nsel_out) nsel_out[b] = nsel;
     status[b] = OR_GAS_OK;
   }
   return 0;
@@ -500,14 +554,15 @@ int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int3
                    int64_t* used, int32_t n_rel, const int32_t* rel_pod,
                    const int32_t* rel_node, int32_t max_containers, const int64_t* req,
                    const uint32_t* req_mask, const int32_t* n_containers,
-                   const int32_t* cards_per_container, const int32_t* cards, int32_t* status) {
-  if (max_cards > 8 || n_res > OR_RM_MAX_KEYS) return -1;
+                   const int32_t* cards_per_container, const int32_t* cards, int32_t cards_stride,
+                   int32_t* status) {
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_RM_MAX_KEYS) return -1;
   for (int32_t r = 0; r < n_rel; ++r) {
     const int32_t p = rel_pod[r], n = rel_node[r];
     if (n < 0 || n >= n_nodes) return -1;
     int64_t* u = used + (int64_t)n * max_cards * n_res;
     const int32_t ncard = n_cards[n] > 0 ? n_cards[n] : 0;
-    or_rm maps[8], stale;
+    or_rm maps[OR_GAS_MAX_CARDS], stale;
     node_maps(max_cards, n_res, ncard, u, maps);
     int32_t off = 0, err = OR_RM_OK;
     for (int32_t c = 0; c < n_containers[p] && !err; ++c) {
@@ -518,7 +573,7 @@ int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int3
       container_map(n_res, req + base * n_res, req_mask[base], &q);
       or_rm_divide(&q, k_c);
       for (int32_t j = 0; j < k_c && !err; ++j) {
-        const int32_t k = cards[(int64_t)r * 8 + off + j];
+        const int32_t k = off + j < cards_stride ? cards[(int64_t)r * cards_stride + off + j] : -1;
         if (k >= 0 && k < ncard) {
           err = or_rm_subtract_rm(&maps[k], &q);
         } else {                                     /* new empty map for the card */

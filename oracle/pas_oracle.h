@@ -97,8 +97,21 @@ int or_rm_divide(or_rm* rm, int32_t divider);                 /* resource_map.go
 /* checkResourceCapacity (gpuscheduler/scheduler.go:341-383). */
 int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const or_rm* used);
 
+#define OR_GAS_MAX_CARDS 64
+#define OR_GAS_MAX_SEL 64
+#define OR_GAS_SEL_EXTENDED 15
+#define OR_GAS_SEL_LIMIT 14
+
 /* GAS filter over every (pod, node) of a packed snapshot, one runSchedulingLogic
- * (scheduler.go:280-338) each; same layouts and result encoding as pas_gas_fit. */
+ * (scheduler.go:280-338) each; same layouts and result encoding as pas_gas_fit (words of
+ * selections that do not pack: OR_GAS_SEL_EXTENDED; pods with more than 64 selections:
+ * OR_GAS_SEL_LIMIT, not evaluated).  or_gas_fit_ex also returns every fitting pair's full
+ * selection: sel_out[P][N][64] card ranks, nsel_out[P][N] counts (NULL: not wanted). */
+int or_gas_fit_ex(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
+                  const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
+                  int32_t max_containers, int32_t i915_index, const int64_t* req,
+                  const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
+                  uint8_t* sel_out, int32_t* nsel_out);
 int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
                const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
                int32_t max_containers, int32_t i915_index, const int64_t* req,
@@ -109,13 +122,15 @@ int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t*
  * (:280-338), then Cache.adjustPodResources(add) with the resulting annotation
  * (node_resource_cache.go:240-287: per container, request / numCards added to each of its
  * cards, all or nothing).  used is updated in place.  res_out[b] = the packed result word
- * (as or_gas_fit; 0 when it does not fit), status[b] = OR_GAS_* below. */
+ * (as or_gas_fit; 0 when it does not fit), status[b] = OR_GAS_* below; cards_out / nsel_out
+ * the full selection of each committed bind. */
 enum { OR_GAS_OK = 0, OR_GAS_WONT_FIT = 1, OR_GAS_ERR_INPUT = 2, OR_GAS_ERR_OVERFLOW = 3 };
 int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
                 const int64_t* cap_per_gpu, int64_t* used, int32_t n_binds,
                 const int32_t* bind_pod, const int32_t* bind_node, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
-                const int32_t* n_containers, uint32_t* res_out, int32_t* status);
+                const int32_t* n_containers, uint32_t* res_out, int32_t* status,
+                uint8_t* cards_out /*[n_binds][64] or NULL*/, int32_t* nsel_out);
 /* Cache.adjustPodResources(remove) (node_resource_cache.go:240-287) for pods leaving nodes,
  * in order: container c's cards are cards[r][off .. off + n_cc[r][c]) (off = sum of the
  * earlier containers' counts; ranks into the node's cards); its request / n_cc is
@@ -126,7 +141,8 @@ int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int3
                    int64_t* used, int32_t n_rel, const int32_t* rel_pod,
                    const int32_t* rel_node, int32_t max_containers, const int64_t* req,
                    const uint32_t* req_mask, const int32_t* n_containers,
-                   const int32_t* cards_per_container, const int32_t* cards, int32_t* status);
+                   const int32_t* cards_per_container, const int32_t* cards,
+                   int32_t cards_stride /*8 or 64*/, int32_t* status);
 
 #ifdef __cplusplus
 }

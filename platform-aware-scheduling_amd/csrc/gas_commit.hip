@@ -21,7 +21,6 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 64;
-constexpr int kMaxCards = PAS_GAS_MAX_CARDS;
 constexpr int kMaxRes = PAS_GAS_MAX_RES;
 
 // checkResourceCapacity (scheduler.go:341-383) for one requested kind.
@@ -44,11 +43,17 @@ struct BindArgs {
   const uint32_t* mask;    // [n_pods][C]
   const int32_t* ncont;    // [n_pods]
   const int32_t* cpc;      // release: [n_ops][C] cards per container
-  const int32_t* cards;    // release: [n_ops][8]
+  const int32_t* cards;    // release: [n_ops][cards_stride]
+  int32_t cards_stride;    // 8 (pas_gas_release) or PAS_GAS_MAX_SELECTIONS (_ex)
   uint32_t* res_out;       // bind: [n_ops]
   int32_t* status;         // [n_ops]
+  uint8_t* cards_out;      // bind_ex: [n_ops][PAS_GAS_MAX_SELECTIONS] or null
+  int32_t* nsel_out;       // bind_ex: [n_ops] or null
 };
 
+// KMAX: the snapshot's max_cards rounded up to 8 / 16 / 64 (the per-thread copies live in
+// registers for the common shapes, in scratch for 64-card snapshots).
+template <int KMAX>
 __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs a) {
   const int32_t sgi = blockIdx.x * kTpb + threadIdx.x;
   if (sgi >= n_seg) return;
@@ -56,7 +61,7 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
   const int32_t n = a.op_node[a.order[a.seg_off[sgi]]];
   const int32_t ncard = min(a.n_cards[n], K);
   int64_t* un = a.used + (int64_t)n * K * Q;
-  int64_t u[kMaxCards][kMaxRes], cap[kMaxRes];
+  int64_t u[KMAX][kMaxRes], cap[kMaxRes];
   for (int k = 0; k < K; ++k)
     for (int q = 0; q < Q; ++q) u[k][q] = un[k * Q + q];
   for (int q = 0; q < Q; ++q) cap[q] = a.cap[(int64_t)n * Q + q];
@@ -65,12 +70,13 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
     const int32_t p = a.op_pod[op];
     // runSchedulingLogic on the node's current usage: a working copy (readNodeResources,
     // node_resource_cache.go:474-491), first fit per selection, takes accumulate (addRM)
-    int64_t w[kMaxCards][kMaxRes];
+    int64_t w[KMAX][kMaxRes];
     for (int k = 0; k < K; ++k)
       for (int q = 0; q < Q; ++q) w[k][q] = u[k][q];
     bool fits = ncard > 0;  // FetchNode error / no cards label (:282-298)
     uint32_t word = 0;
     int32_t nsel = 0;
+    bool packable = true;
     for (int32_t c = 0; fits && c < a.ncont[p]; ++c) {
       const int64_t b = (int64_t)p * C + c;
       const uint32_t m = a.mask[b];
@@ -95,16 +101,24 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
         }
         for (int q = 0; q < Q; ++q)
           if ((m >> q) & 1u) w[chosen][q] += r[q];  // addRM after a passing check
-        if (nsel < 8) word |= (uint32_t)chosen << (3 * nsel);
+        if (nsel < PAS_GAS_PACKED) word |= (uint32_t)chosen << (3 * nsel);
+        packable = packable && chosen < PAS_GAS_PACKED;
+        if (a.cards_out && nsel < PAS_GAS_MAX_SELECTIONS)
+          a.cards_out[(int64_t)op * PAS_GAS_MAX_SELECTIONS + nsel] = (uint8_t)chosen;
         ++nsel;
       }
     }
     if (!fits) {
       a.res_out[op] = 0u;
       a.status[op] = PAS_GAS_WONT_FIT;
+      if (a.nsel_out) a.nsel_out[op] = 0;
       continue;
     }
-    a.res_out[op] = 0x80000000u | ((uint32_t)nsel << 24) | word;
+    // the pas_gas_fit word: selections that do not pack are PAS_GAS_SEL_EXTENDED
+    a.res_out[op] = nsel <= PAS_GAS_PACKED && packable
+                        ? 0x80000000u | ((uint32_t)nsel << 24) | word
+                        : 0x80000000u | ((uint32_t)PAS_GAS_SEL_EXTENDED << 24);
+    if (a.nsel_out) a.nsel_out[op] = nsel;
     // adjustPodResources(add) with that annotation adds request / numCards (= numI915) to
     // each selected card: exactly the working copy's takes, which cannot overflow after the
     // capacity checks
@@ -116,6 +130,7 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
     for (int q = 0; q < Q; ++q) un[k * Q + q] = u[k][q];
 }
 
+template <int KMAX>
 __global__ __launch_bounds__(kTpb) void gas_release_kernel(int32_t n_seg, BindArgs a) {
   const int32_t sgi = blockIdx.x * kTpb + threadIdx.x;
   if (sgi >= n_seg) return;
@@ -123,13 +138,13 @@ __global__ __launch_bounds__(kTpb) void gas_release_kernel(int32_t n_seg, BindAr
   const int32_t n = a.op_node[a.order[a.seg_off[sgi]]];
   const int32_t ncard = max(0, min(a.n_cards[n], K));
   int64_t* un = a.used + (int64_t)n * K * Q;
-  int64_t u[kMaxCards][kMaxRes];
+  int64_t u[KMAX][kMaxRes];
   for (int k = 0; k < K; ++k)
     for (int q = 0; q < Q; ++q) u[k][q] = un[k * Q + q];
   for (int32_t i = a.seg_off[sgi]; i < a.seg_off[sgi + 1]; ++i) {
     const int32_t op = a.order[i];
     const int32_t p = a.op_pod[op];
-    int64_t w[kMaxCards][kMaxRes];  // checkPodResourceAdjustment's copy
+    int64_t w[KMAX][kMaxRes];  // checkPodResourceAdjustment's copy
     for (int k = 0; k < K; ++k)
       for (int q = 0; q < Q; ++q) w[k][q] = u[k][q];
     bool ok = true;
@@ -142,7 +157,7 @@ __global__ __launch_bounds__(kTpb) void gas_release_kernel(int32_t n_seg, BindAr
       int64_t r[kMaxRes];
       for (int q = 0; q < Q; ++q) r[q] = a.req[b * Q + q] / kc;  // divide(numCards)
       for (int32_t j = 0; ok && j < kc; ++j) {
-        const int32_t k = a.cards[(int64_t)op * 8 + off + j];
+        const int32_t k = a.cards[(int64_t)op * a.cards_stride + off + j];
         const bool known = k >= 0 && k < ncard;
         for (int q = 0; q < Q; ++q) {
           if (!((m >> q) & 1u)) continue;
@@ -175,18 +190,29 @@ int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_con
                       int32_t i915_index, const int32_t* d_order, const int32_t* d_seg_off,
                       const int32_t* d_pod, const int32_t* d_node, const int64_t* d_req,
                       const uint32_t* d_mask, const int32_t* d_ncont, const int32_t* d_cpc,
-                      const int32_t* d_cards, uint32_t* d_res, int32_t* d_status,
+                      const int32_t* d_cards, int32_t cards_stride, uint32_t* d_res,
+                      int32_t* d_status, uint8_t* d_cards_out, int32_t* d_nsel_out,
                       hipStream_t s) {
   if (n_seg == 0) return PAS_OK;
   GasSnapshot& g = ctx->gas;
-  BindArgs a{g.max_cards, g.n_res, max_containers, i915_index, d_order, d_seg_off, d_pod,
-             d_node, g.n_cards, g.cap, g.used, d_req, d_mask, d_ncont, d_cpc, d_cards, d_res,
-             d_status};
+  BindArgs a{g.max_cards, g.n_res,  max_containers, i915_index, d_order, d_seg_off,
+             d_pod,       d_node,   g.n_cards,      g.cap,      g.used,  d_req,
+             d_mask,      d_ncont,  d_cpc,          d_cards,    cards_stride,
+             d_res,       d_status, d_cards_out,    d_nsel_out};
   const unsigned blocks = (unsigned)((n_seg + kTpb - 1) / kTpb);
-  if (release)
-    gas_release_kernel<<<blocks, kTpb, 0, s>>>(n_seg, a);
-  else
-    gas_bind_kernel<<<blocks, kTpb, 0, s>>>(n_seg, a);
+#define PAS_COMMIT(KM)                                       \
+  if (release)                                               \
+    gas_release_kernel<KM><<<blocks, kTpb, 0, s>>>(n_seg, a); \
+  else                                                       \
+    gas_bind_kernel<KM><<<blocks, kTpb, 0, s>>>(n_seg, a);
+  if (g.max_cards <= 8) {
+    PAS_COMMIT(8)
+  } else if (g.max_cards <= 16) {
+    PAS_COMMIT(16)
+  } else {
+    PAS_COMMIT(PAS_GAS_MAX_CARDS)
+  }
+#undef PAS_COMMIT
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
 }

@@ -40,7 +40,8 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
-constexpr int kMaxCards = PAS_GAS_MAX_CARDS;
+constexpr int kMaxCards = PAS_GAS_PACKED;  // cards of a fast-path node, in registers
+constexpr int kPacked = PAS_GAS_PACKED;    // selections of a fast-path pod
 
 // A (pod, container) step, in compare form: cmp[q] = per-GPU need of a requested kind
 // (getPerGPUResourceRequest :180-190), INT64_MIN for the others, so every card passes them
@@ -70,7 +71,7 @@ struct alignas(16) GasThresholds {
   int32_t over;
   int32_t pad[7];
 };
-static_assert(sizeof(GasThresholds) <= sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS, "row");
+static_assert(sizeof(GasThresholds) <= sizeof(GasSel) * kPacked, "row");
 constexpr int32_t kBadPod = 1 << 30;  // multi-list word flag: a selection has a negative need
 
 // Pod with at most one card selection: its selecting step (compare form), and
@@ -166,7 +167,9 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
                                 const int32_t* __restrict__ n_containers,
                                 const unsigned long long* __restrict__ gflip,
                                 GasSingle* __restrict__ single, int32_t* __restrict__ multi,
-                                GasSel* __restrict__ sels, int32_t* __restrict__ counts) {
+                                GasSel* __restrict__ sels, int32_t* __restrict__ counts,
+                                int32_t* __restrict__ big_pods, int32_t* __restrict__ n_big_pods,
+                                int32_t* __restrict__ pod_steps) {
   const int32_t p = blockIdx.x * kTpb + threadIdx.x;
   if (p >= n_pods) return;
   const int32_t nc = min(max(n_containers[p], 0), max_containers);
@@ -203,6 +206,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
     const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
     if (cum[q] > gmin) skip_ok &= ~(1u << q);
   }
+  pod_steps[p] = steps;
   const bool one_sel = steps <= 1;
   const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0)
                             : multi_skip_list(n_res, skip_ok, skip_req);
@@ -213,12 +217,13 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
     single[(int64_t)l * n_pods + slot] = one;
     return;
   }
-  if (steps > PAS_GAS_MAX_SELECTIONS) {
-    multi[(int64_t)l * n_pods + slot] = p | (steps << 24);
+  if (steps > kPacked) {  // gas_fit_generic_kernel; the fast kernel writes 0 first
+    multi[(int64_t)l * n_pods + slot] = p | ((kPacked + 1) << 24);
+    big_pods[atomicAdd(n_big_pods, 1)] = p;
     return;
   }
   // the pod's row sits at its list position, so a batch of a list is one contiguous copy
-  GasSel* out = sels + ((int64_t)l * n_pods + slot) * PAS_GAS_MAX_SELECTIONS;
+  GasSel* out = sels + ((int64_t)l * n_pods + slot) * kPacked;
   int32_t k = 0, bad = 0;
   int64_t cmp3[3][PAS_GAS_MAX_RES], take3[3][PAS_GAS_MAX_RES];  // first 3 selections
   for (int32_t c = 0; c < nc; ++c) {
@@ -271,10 +276,13 @@ __global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K,
                                                            const int32_t* __restrict__ n_cards,
                                                            const int64_t* __restrict__ cap,
                                                            const int64_t* __restrict__ used,
-                                                           unsigned long long* __restrict__ gflip) {
+                                                           unsigned long long* __restrict__ gflip,
+                                                           int32_t* __restrict__ big_nodes,
+                                                           int32_t* __restrict__ n_big_nodes) {
   __shared__ int64_t red[kTpb / 64][PAS_GAS_MAX_RES];
   const int32_t n = blockIdx.x * kTpb + threadIdx.x;
   const int32_t nc = n < N ? min(n_cards[n], K) : 0;
+  if (nc > kMaxCards) big_nodes[atomicAdd(n_big_nodes, 1)] = n;  // gas_fit_generic_kernel
   for (int q = 0; q < n_res; ++q) {
     int64_t m = INT64_MAX;
     const int64_t c = nc > 0 ? cap[(int64_t)n * n_res + q] : 0;
@@ -333,12 +341,6 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
     chosen = ok ? k : chosen;                    // one select per card
   }
   return chosen;
-}
-
-__device__ __forceinline__ int64_t uniform64(int64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)x >> 32));
-  return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
 // One (pod, node) result: the packed word, or (kBits) the fit bit in the pod's row of a
@@ -477,8 +479,9 @@ __global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
   const int32_t nc = valid ? n_cards[n] : 0;
   int64_t free[kMaxCards][Q];
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
-  // FetchNode error / missing cards label -> errWontFit before any container (:282-298)
-  const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
+  // FetchNode error / missing cards label -> errWontFit before any container (:282-298);
+  // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
+  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage[wave], bt, res,
                          fit);
@@ -635,7 +638,7 @@ __device__ __forceinline__ uint32_t fit_mask(const int64_t (&need)[C],
 }
 
 constexpr int kMB = 8;  // multi-selection pods staged in LDS per round and wave
-constexpr int kRowChunks = PAS_GAS_MAX_SELECTIONS * (int)sizeof(GasSel) / 16;  // 16-B per row
+constexpr int kRowChunks = kPacked * (int)sizeof(GasSel) / 16;  // 16-B chunks per row
 
 // Fit mask of the compared kinds (all but SKIP) of a threshold row: bit k = card k's snapshot
 // free passes every compared threshold.
@@ -804,7 +807,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
   for (int32_t b0 = i0; b0 < i1; b0 += kMB) {
     const int32_t nb = min(kMB, i1 - b0);
     // every load of the batch in flight before the LDS writes (rows past nb: not read)
-    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * PAS_GAS_MAX_SELECTIONS);
+    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
     constexpr int kIters = kMB * kRowChunks / 64;
     int4 v[kIters];
 #pragma unroll
@@ -824,13 +827,13 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
       const int32_t pw = __builtin_amdgcn_readfirstlane(stage_w[j]);
       const int32_t pod = pw & 0xFFFFFF;
       const int32_t S = (pw >> 24) & 0xF;
-      const GasSel* rec = stage + j * PAS_GAS_MAX_SELECTIONS;
+      const GasSel* rec = stage + j * kPacked;
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
         if (S <= 3)
           out = multi_closed<Q, SKIP>(free, *reinterpret_cast<const GasThresholds*>(rec), S, live,
                                       node_ok);
-        else if (S <= PAS_GAS_MAX_SELECTIONS)
+        else if (S <= kPacked)
           out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
       }
       put_result<kBits>(res, fit, pod, N, n, valid, out);
@@ -848,7 +851,7 @@ __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q],
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
   multi_list<Q, L - 1, kBits>(free, stage, stage_w, node_ok, N, n, valid, multi + (int64_t)L * P,
-                              sels + (int64_t)L * P * PAS_GAS_MAX_SELECTIONS, counts + L, bt,
+                              sels + (int64_t)L * P * kPacked, counts + L, bt,
                               res, fit);
   if constexpr (L < Q)
     multi_lists<Q, kBits, L + 1>(free, stage, stage_w, node_ok, N, n, valid, P, multi, sels,
@@ -862,7 +865,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
     const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
     uint64_t* __restrict__ fit) {
-  __shared__ GasSel stage[kTpb / 64][PAS_GAS_MAX_SELECTIONS * kMB];  // a slice per wave
+  __shared__ GasSel stage[kTpb / 64][kPacked * kMB];  // a slice per wave
   __shared__ int32_t stage_w[kTpb / 64][kMB];
   const BlockTile bt = block_tile(chunks);
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
@@ -870,10 +873,150 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   const int32_t nc = valid ? n_cards[n] : 0;
   int64_t free[kMaxCards][Q];
   load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
-  const uint32_t node_ok = nc > 0 ? 0x80000000u : 0u;
+  // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
+  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   multi_lists<Q, kBits>(free, stage[wave], stage_w[wave], node_ok, N, n, valid, P, multi, sels,
                         counts, bt, res, fit);
+}
+
+// ---------------------------------------------------------------------------- generic path
+//
+// (pod, node) pairs outside the fast kernels' shapes: pods with more than 8 selections
+// (every node) and nodes with more than 8 cards (every other pod).  One thread per pair runs
+// runSchedulingLogic (scheduler.go:280-338) as the reference writes it: per container
+// getPerGPUResourceRequest, then per gpuNum the first card in lexicographic order passing
+// checkResourceCapacity (:341-383) on the usage with the pod's earlier takes (addRM), no
+// limit but PAS_GAS_MAX_SELECTIONS / PAS_GAS_MAX_CARDS.  The state is private (KMAX cards;
+// 64-card snapshots put it in scratch): this is the rare path, not a hot kernel.  Words
+// overwrite the fast kernels' zeros; bitmap bits are or-ed in; selections that do not pack
+// go to the side buffer.
+struct GenericArgs {
+  int32_t N, K, Q, C, i915;
+  const int32_t* n_cards;
+  const int64_t* cap;
+  const int64_t* used;
+  const int64_t* req;
+  const uint32_t* mask;
+  const int32_t* ncont;
+  const int32_t* big_pods;
+  const int32_t* n_big_pods;
+  const int32_t* big_nodes;
+  const int32_t* n_big_nodes;
+  const int32_t* pod_steps;
+  int32_t n_pods;
+  uint32_t* res;
+  uint64_t* fit;
+  pas_gas_selection* side;
+  int64_t side_cap;
+  unsigned long long* side_count;
+  unsigned long long* limit_count;
+};
+
+__device__ __forceinline__ bool kind_fits(int64_t need, int64_t cap, int64_t used) {
+  if (need < 0 || cap <= 0 || used < 0) return false;
+  const int64_t sum = (int64_t)((uint64_t)used + (uint64_t)need);
+  return sum >= 0 && cap >= sum;
+}
+
+template <int KMAX>
+__device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
+  const int32_t Q = a.Q;
+  uint32_t word = 0u;
+  uint8_t sel[PAS_GAS_MAX_SELECTIONS];
+  int32_t nsel = 0;
+  bool fits = false;
+  const int32_t nc = a.n_cards[n];
+  if (nc > 0) {  // FetchNode error / no cards label (:282-298)
+    fits = true;
+    const int32_t ncard = min(nc, min(a.K, KMAX));
+    int64_t w[KMAX][PAS_GAS_MAX_RES];  // readNodeResources copy (node_resource_cache.go:474-491)
+    int64_t cap[PAS_GAS_MAX_RES];
+    for (int q = 0; q < Q; ++q) cap[q] = a.cap[(int64_t)n * Q + q];
+    for (int k = 0; k < ncard; ++k)
+      for (int q = 0; q < Q; ++q) w[k][q] = a.used[((int64_t)n * a.K + k) * Q + q];
+    for (int32_t c = 0; fits && c < a.ncont[p]; ++c) {
+      const int64_t b = (int64_t)p * a.C + c;
+      const uint32_t m = a.mask[b];
+      if (m == 0u) continue;  // no GPU resources: no cards (:206-208)
+      int64_t r[PAS_GAS_MAX_RES];
+      for (int q = 0; q < Q; ++q) r[q] = a.req[b * Q + q];
+      int64_t num = 0;  // getNumI915 (:192-198)
+      if (a.i915 >= 0 && ((m >> a.i915) & 1u) && r[a.i915] > 0) num = r[a.i915];
+      if (num > 1)
+        for (int q = 0; q < Q; ++q) r[q] /= num;  // getPerGPUResourceRequest (:180-190)
+      for (int64_t g = 0; g < num; ++g) {
+        int chosen = -1;
+        for (int k = 0; k < ncard && chosen < 0; ++k) {
+          bool ok = true;
+          for (int q = 0; q < Q; ++q)
+            if ((m >> q) & 1u) ok = ok && kind_fits(r[q], cap[q], w[k][q]);
+          if (ok) chosen = k;
+        }
+        if (chosen < 0) {  // errWontFit (:249-253)
+          fits = false;
+          break;
+        }
+        for (int q = 0; q < Q; ++q)
+          if ((m >> q) & 1u) w[chosen][q] += r[q];  // addRM after a passing check
+        sel[nsel++] = (uint8_t)chosen;
+      }
+    }
+  }
+  if (fits) {
+    bool packable = nsel <= kPacked;
+    for (int32_t j = 0; j < nsel; ++j) packable = packable && sel[j] < kMaxCards;
+    if (packable) {
+      word = 0x80000000u | ((uint32_t)nsel << 24);
+      for (int32_t j = 0; j < nsel; ++j) word |= (uint32_t)sel[j] << (3 * j);
+    } else {
+      word = 0x80000000u | ((uint32_t)PAS_GAS_SEL_EXTENDED << 24);
+      if (a.side_count) {
+        const unsigned long long slot = atomicAdd(a.side_count, 1ull);
+        if ((int64_t)slot < a.side_cap) {
+          pas_gas_selection& rec = a.side[slot];
+          rec.pod = p;
+          rec.node = n;
+          rec.n_sel = nsel;
+          rec.reserved = 0;
+          for (int32_t j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) rec.card[j] = j < nsel ? sel[j] : 0;
+        }
+      }
+    }
+  }
+  if (a.fit) {
+    if (fits)
+      atomicOr(reinterpret_cast<unsigned long long*>(a.fit) + (int64_t)p * ((a.N + 63) / 64) +
+                   (n >> 6),
+               1ull << (n & 63));
+  } else {
+    a.res[(int64_t)p * a.N + n] = word;
+  }
+}
+
+template <int KMAX>
+__global__ __launch_bounds__(64) void gas_fit_generic_kernel(GenericArgs a) {
+  const int64_t nbp = *a.n_big_pods, nbn = *a.n_big_nodes;
+  const int64_t seg_a = nbp * a.N, total = seg_a + (int64_t)a.n_pods * nbn;
+  for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * 64) {
+    int32_t p, n;
+    if (i < seg_a) {  // a pod with more than 8 selections, every node
+      p = a.big_pods[i / a.N];
+      n = (int32_t)(i % a.N);
+      if (a.pod_steps[p] > PAS_GAS_MAX_SELECTIONS) {  // beyond the documented limit
+        if (!a.fit) a.res[(int64_t)p * a.N + n] = (uint32_t)PAS_GAS_SEL_LIMIT << 24;
+        if (n == 0) atomicAdd(a.limit_count, 1ull);
+        continue;
+      }
+    } else {  // a node with more than 8 cards, every pod the fast kernels evaluated
+      const int64_t j = i - seg_a;
+      p = (int32_t)(j / nbn);
+      n = a.big_nodes[j % nbn];
+      if (a.pod_steps[p] > kPacked) continue;  // done in the first segment
+    }
+    fit_pair<KMAX>(a, p, n);
+  }
 }
 
 }  // namespace
@@ -881,22 +1024,35 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
                    const int32_t* d_n_containers, uint32_t* d_res, uint64_t* d_fit,
+                   pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
                    hipStream_t s) {
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
-  if (N == 0 || n_pods == 0) return PAS_OK;
+  if (!ctx->gas_limit) {
+    PAS_HIP(ctx, hipMalloc(&ctx->gas_limit, sizeof(int64_t)));
+    PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_limit_ev, hipEventDisableTiming));
+  }
+  PAS_HIP(ctx, hipMemsetAsync(ctx->gas_limit, 0, sizeof(int64_t), s));
+  if (d_side_count) PAS_HIP(ctx, hipMemsetAsync(d_side_count, 0, sizeof(int64_t), s));
+  if (N == 0 || n_pods == 0) {
+    PAS_HIP(ctx, hipEventRecord(ctx->gas_limit_ev, s));
+    return PAS_OK;
+  }
   // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][P] | their
-  // selection rows [Q+1][P][8] | the flipped kind minima [4] and counts [2(Q+1)] (zeroed
-  // together)
+  // selection rows [Q+1][P][8] | the generic path's pods [P], nodes [N] and per-pod
+  // selection counts [P] | the flipped kind minima [4], list counts [2(Q+1)] and the generic
+  // list counts [2] (zeroed together)
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   const int32_t NL = Q + 1;
-  const size_t b_single = (sizeof(GasSingle) * (size_t)NL * n_pods + 255) & ~size_t(255);
-  const size_t b_multi = (sizeof(int32_t) * (size_t)NL * n_pods + 255) & ~size_t(255);
-  const size_t b_sels =
-      (sizeof(GasSel) * PAS_GAS_MAX_SELECTIONS * (size_t)NL * n_pods + 255) & ~size_t(255);
-  constexpr size_t b_tail = 2 * (PAS_GAS_MAX_RES + 1) * sizeof(int32_t) +
-                            PAS_GAS_MAX_RES * sizeof(unsigned long long);
-  const size_t need = b_single + b_multi + b_sels + b_tail;
+  auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
+  const size_t b_single = al(sizeof(GasSingle) * (size_t)NL * n_pods);
+  const size_t b_multi = al(sizeof(int32_t) * (size_t)NL * n_pods);
+  const size_t b_sels = al(sizeof(GasSel) * kPacked * (size_t)NL * n_pods);
+  const size_t b_pods = al(sizeof(int32_t) * (size_t)n_pods);
+  const size_t b_nodes = al(sizeof(int32_t) * (size_t)N);
+  constexpr size_t b_tail = PAS_GAS_MAX_RES * sizeof(unsigned long long) +
+                            (2 * (PAS_GAS_MAX_RES + 1) + 2) * sizeof(int32_t);
+  const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_nodes + b_tail;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -909,19 +1065,28 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   }
   char* base = static_cast<char*>(ctx->aux);
   GasSingle* single = reinterpret_cast<GasSingle*>(base);
-  int32_t* multi = reinterpret_cast<int32_t*>(base + b_single);
-  GasSel* sels = reinterpret_cast<GasSel*>(base + b_single + b_multi);
-  unsigned long long* gflip =
-      reinterpret_cast<unsigned long long*>(base + b_single + b_multi + b_sels);
+  base += b_single;
+  int32_t* multi = reinterpret_cast<int32_t*>(base);
+  base += b_multi;
+  GasSel* sels = reinterpret_cast<GasSel*>(base);
+  base += b_sels;
+  int32_t* big_pods = reinterpret_cast<int32_t*>(base);
+  base += b_pods;
+  int32_t* pod_steps = reinterpret_cast<int32_t*>(base);
+  base += b_pods;
+  int32_t* big_nodes = reinterpret_cast<int32_t*>(base);
+  base += b_nodes;
+  unsigned long long* gflip = reinterpret_cast<unsigned long long*>(base);
   int32_t* counts = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
+  int32_t* n_big = counts + 2 * (PAS_GAS_MAX_RES + 1);  // {pods, nodes}
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
   PAS_HIP(ctx, hipMemsetAsync(gflip, 0, b_tail, s));
   gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
-                                                           gflip);
+                                                           gflip, big_nodes, n_big + 1);
   gas_prep_kernel<<<(n_pods + kTpb - 1) / kTpb, kTpb, 0, s>>>(
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
-      multi, sels, counts);
+      multi, sels, counts, big_pods, n_big, pod_steps);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   // grids: (node block, pod chunk) pairs, ~4096 blocks; each kernel splits each of its
@@ -943,8 +1108,42 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
 #undef PAS_GAS_CASE
     default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   }
+  // the wide shapes: the lists' lengths are on the device, so the grid is fixed and threads
+  // past the work return at once
+  GenericArgs ga;
+  ga.N = N;
+  ga.K = K;
+  ga.Q = Q;
+  ga.C = max_containers;
+  ga.i915 = i915_index;
+  ga.n_cards = g.n_cards;
+  ga.cap = g.cap;
+  ga.used = g.used;
+  ga.req = d_req;
+  ga.mask = d_req_mask;
+  ga.ncont = d_n_containers;
+  ga.big_pods = big_pods;
+  ga.n_big_pods = n_big;
+  ga.big_nodes = big_nodes;
+  ga.n_big_nodes = n_big + 1;
+  ga.pod_steps = pod_steps;
+  ga.n_pods = n_pods;
+  ga.res = d_res;
+  ga.fit = d_fit;
+  ga.side = d_side;
+  ga.side_cap = d_side ? side_cap : 0;
+  ga.side_count = reinterpret_cast<unsigned long long*>(d_side_count);
+  ga.limit_count = reinterpret_cast<unsigned long long*>(ctx->gas_limit);
+  constexpr int kGenericBlocks = 512;
+  if (K <= 8)
+    gas_fit_generic_kernel<8><<<kGenericBlocks, 64, 0, s>>>(ga);
+  else if (K <= 16)
+    gas_fit_generic_kernel<16><<<kGenericBlocks, 64, 0, s>>>(ga);
+  else
+    gas_fit_generic_kernel<PAS_GAS_MAX_CARDS><<<kGenericBlocks, 64, 0, s>>>(ga);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
+  PAS_HIP(ctx, hipEventRecord(ctx->gas_limit_ev, s));
   return PAS_OK;
 }
 

@@ -188,6 +188,8 @@ void pas_destroy(pas_ctx* ctx) {
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->aux) (void)hipFree(ctx->aux);
   if (ctx->label_part) (void)hipFree(ctx->label_part);
+  if (ctx->gas_limit) (void)hipFree(ctx->gas_limit);
+  if (ctx->gas_limit_ev) (void)hipEventDestroy(ctx->gas_limit_ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -506,7 +508,7 @@ static int gas_shape_ok(pas_ctx* ctx, int32_t n_nodes, int32_t max_cards, int32_
     return set_error(ctx, PAS_EINVAL, "pas_gas_snapshot_set: bad shape");
   if (max_cards > PAS_GAS_MAX_CARDS || n_res > PAS_GAS_MAX_RES)
     return set_error(ctx, PAS_ECAPACITY,
-                     "pas_gas_snapshot_set: max_cards <= 8 and n_res <= 4 supported");
+                     "pas_gas_snapshot_set: max_cards <= 64 and n_res <= 4 supported");
   return PAS_OK;
 }
 
@@ -579,8 +581,9 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
                       int32_t n_ops, const int32_t* op_pod, const int32_t* op_node,
                       int32_t n_pods, int32_t max_containers, int32_t i915_index,
                       const int64_t* req, const uint32_t* req_mask, const int32_t* n_containers,
-                      const int32_t* cpc, const int32_t* cards, uint32_t* res_out,
-                      int32_t* status_out, const char* fn) {
+                      const int32_t* cpc, const int32_t* cards, int32_t cards_stride,
+                      uint32_t* res_out, int32_t* status_out, uint8_t* cards_out,
+                      int32_t* nsel_out, const char* fn) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_gas_gen(ctx, gen_from);
   if (rc) return rc;
@@ -600,22 +603,25 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
     const int32_t p = op_pod[i];
     if (n_containers[p] < 0 || n_containers[p] > max_containers)
       return set_error(ctx, PAS_EINVAL, std::string(fn) + ": n_containers out of range");
+    // selections (bind) / annotation cards (release), saturating past the limit
+    const int64_t limit = release ? cards_stride : PAS_GAS_MAX_SELECTIONS;
     int64_t sel = 0;
     for (int32_t c = 0; c < n_containers[p]; ++c) {
       const int64_t b = (int64_t)p * max_containers + c;
       if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
+      int64_t v = 0;
       if (release) {
-        const int32_t k = cpc[(int64_t)i * max_containers + c];
-        if (k < 0) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": negative card count");
-        sel += k;
+        v = cpc[(int64_t)i * max_containers + c];
+        if (v < 0) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": negative card count");
       } else if (i915_index >= 0 && req_mask[b] && (req_mask[b] >> i915_index & 1u)) {
-        const int64_t v = req[b * Q + i915_index];
-        if (v > 0) sel += v;
+        v = std::max<int64_t>(req[b * Q + i915_index], 0);
       }
+      sel = std::min(sel + std::min(v, limit + 1), limit + 1);
     }
-    if (sel > PAS_GAS_MAX_SELECTIONS)
+    if (sel > limit)
       return set_error(ctx, release ? PAS_EINVAL : PAS_ECAPACITY,
-                       std::string(fn) + ": more than 8 cards for one pod");
+                       std::string(fn) + ": more than " + std::to_string(limit) +
+                           " cards for one pod");
   }
   std::stable_sort(order.begin(), order.end(),
                    [&](int32_t a, int32_t b) { return op_node[a] < op_node[b]; });
@@ -632,9 +638,11 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
   const size_t b_req = sizeof(int64_t) * pods * C * Q, b_mask = sizeof(uint32_t) * pods * C;
   const size_t b_nc = sizeof(int32_t) * pods, b_op = sizeof(int32_t) * ops;
   const size_t b_seg = sizeof(int32_t) * (size_t)(n_seg + 1);
-  const size_t b_cpc = sizeof(int32_t) * ops * C, b_cards = sizeof(int32_t) * ops * 8;
+  const size_t b_cpc = sizeof(int32_t) * ops * C;
+  const size_t b_cards = sizeof(int32_t) * ops * (size_t)cards_stride;
+  const size_t b_sel = cards_out ? ops * PAS_GAS_MAX_SELECTIONS : 1;
   if ((rc = ensure_scratch(ctx, carve_size({b_req, b_mask, b_nc, b_op, b_op, b_op, b_seg, b_cpc,
-                                            b_cards, b_op, b_op}))))
+                                            b_cards, b_op, b_op, b_sel, b_op}))))
     return rc;
   Carve cv{static_cast<char*>(ctx->scratch)};
   int64_t* d_req = cv.take<int64_t>(pods * C * Q);
@@ -645,9 +653,11 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
   int32_t* d_order = cv.take<int32_t>(ops);
   int32_t* d_seg = cv.take<int32_t>((size_t)n_seg + 1);
   int32_t* d_cpc = cv.take<int32_t>(ops * C);
-  int32_t* d_cards = cv.take<int32_t>(ops * 8);
+  int32_t* d_cards = cv.take<int32_t>(ops * (size_t)cards_stride);
   uint32_t* d_res = cv.take<uint32_t>(ops);
   int32_t* d_status = cv.take<int32_t>(ops);
+  uint8_t* d_sel = cv.take<uint8_t>(b_sel);
+  int32_t* d_nsel = cv.take<int32_t>(ops);
   hipStream_t s = ctx->stream;
   if (n_ops > 0) {
     if (max_containers > 0 && n_pods > 0) {
@@ -666,15 +676,19 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
       if (max_containers > 0)
         PAS_HIP(ctx, hipMemcpyAsync(d_cpc, cpc, sizeof(int32_t) * n_ops * max_containers,
                                     hipMemcpyHostToDevice, s));
-      PAS_HIP(ctx, hipMemcpyAsync(d_cards, cards, sizeof(int32_t) * n_ops * 8,
-                                  hipMemcpyHostToDevice, s));
+      PAS_HIP(ctx, hipMemcpyAsync(d_cards, cards, b_cards, hipMemcpyHostToDevice, s));
     }
     if ((rc = gas_commit_launch(ctx, release, n_seg, max_containers, i915_index, d_order, d_seg,
-                                d_pod, d_node, d_req, d_mask, d_nc, d_cpc, d_cards, d_res,
-                                d_status, s)))
+                                d_pod, d_node, d_req, d_mask, d_nc, d_cpc, d_cards,
+                                cards_stride, d_res, d_status, cards_out ? d_sel : nullptr,
+                                cards_out ? d_nsel : nullptr, s)))
       return rc;
     if (!release)
       PAS_HIP(ctx, hipMemcpyAsync(res_out, d_res, b_op, hipMemcpyDeviceToHost, s));
+    if (cards_out) {
+      PAS_HIP(ctx, hipMemcpyAsync(cards_out, d_sel, b_sel, hipMemcpyDeviceToHost, s));
+      PAS_HIP(ctx, hipMemcpyAsync(nsel_out, d_nsel, b_op, hipMemcpyDeviceToHost, s));
+    }
     PAS_HIP(ctx, hipMemcpyAsync(status_out, d_status, b_op, hipMemcpyDeviceToHost, s));
   }
   PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -689,7 +703,21 @@ int pas_gas_bind(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_bin
                  int32_t* status_out) {
   return gas_commit(ctx, false, gen_from, gen_to, n_binds, bind_pod, bind_node, n_pods,
                     max_containers, i915_index, req, req_mask, n_containers, nullptr, nullptr,
-                    res_out, status_out, "pas_gas_bind");
+                    PAS_GAS_PACKED, res_out, status_out, nullptr, nullptr, "pas_gas_bind");
+}
+
+int pas_gas_bind_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
+                    const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
+                    int32_t max_containers, int32_t i915_index, const int64_t* req,
+                    const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
+                    int32_t* status_out, uint8_t* cards_out, int32_t* n_sel_out) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_binds > 0 && (!cards_out || !n_sel_out))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_bind_ex: null input");
+  return gas_commit(ctx, false, gen_from, gen_to, n_binds, bind_pod, bind_node, n_pods,
+                    max_containers, i915_index, req, req_mask, n_containers, nullptr, nullptr,
+                    PAS_GAS_PACKED, res_out, status_out, n_binds > 0 ? cards_out : nullptr,
+                    n_sel_out, "pas_gas_bind_ex");
 }
 
 int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
@@ -699,7 +727,18 @@ int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_
                     const int32_t* cards, int32_t* status_out) {
   return gas_commit(ctx, true, gen_from, gen_to, n_releases, rel_pod, rel_node, n_pods,
                     max_containers, -1, req, req_mask, n_containers, cards_per_container, cards,
-                    nullptr, status_out, "pas_gas_release");
+                    PAS_GAS_PACKED, nullptr, status_out, nullptr, nullptr, "pas_gas_release");
+}
+
+int pas_gas_release_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
+                       const int32_t* rel_pod, const int32_t* rel_node, int32_t n_pods,
+                       int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
+                       const int32_t* n_containers, const int32_t* cards_per_container,
+                       const int32_t* cards, int32_t* status_out) {
+  return gas_commit(ctx, true, gen_from, gen_to, n_releases, rel_pod, rel_node, n_pods,
+                    max_containers, -1, req, req_mask, n_containers, cards_per_container, cards,
+                    PAS_GAS_MAX_SELECTIONS, nullptr, status_out, nullptr, nullptr,
+                    "pas_gas_release_ex");
 }
 
 int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out) {
@@ -716,34 +755,43 @@ int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out) {
   return PAS_OK;
 }
 
-int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
-                int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
-                const int32_t* n_containers, uint32_t* res_out) {
+// Host path of pas_gas_fit / pas_gas_fit_ex: validates, uploads the batch, runs the fit and
+// copies the words (and side records) back.
+static int gas_fit_host(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                        int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                        const int32_t* n_containers, uint32_t* res_out,
+                        pas_gas_selection* side, int64_t side_cap, int64_t* side_count,
+                        const char* fn) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_gas_gen(ctx, gen);
   if (rc) return rc;
   const int32_t Q = ctx->gas.n_res;
-  if (n_pods < 0 || max_containers < 0 || i915_index >= Q || i915_index < -1)
-    return set_error(ctx, PAS_EINVAL, "pas_gas_fit: bad shape");
+  if (n_pods < 0 || max_containers < 0 || i915_index >= Q || i915_index < -1 || side_cap < 0)
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad shape");
+  if (side_count) *side_count = 0;
   if (n_pods == 0) return PAS_OK;
-  if (!n_containers || !res_out || (max_containers > 0 && (!req || !req_mask)))
-    return set_error(ctx, PAS_EINVAL, "pas_gas_fit: null input");
-  // Validate the packed-annotation capacity (sum of i915 counts per pod).
+  if (!n_containers || !res_out || (max_containers > 0 && (!req || !req_mask)) ||
+      (side_cap > 0 && !side))
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
+  // Validate the batch; the selections (sum of i915 counts, saturating) bound the
+  // documented limit.
   for (int32_t p = 0; p < n_pods; ++p) {
     if (n_containers[p] < 0 || n_containers[p] > max_containers)
-      return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_containers out of range");
+      return set_error(ctx, PAS_EINVAL, std::string(fn) + ": n_containers out of range");
     int64_t sel = 0;
     for (int32_t c = 0; c < n_containers[p]; ++c) {
       const int64_t b = (int64_t)p * max_containers + c;
-      if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, "pas_gas_fit: mask bit >= n_res");
+      if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
       if (i915_index >= 0 && (req_mask[b] >> i915_index & 1u)) {
-        const int64_t v = req[b * Q + i915_index];
-        if (v > 0) sel += v;
+        const int64_t v = std::max<int64_t>(req[b * Q + i915_index], 0);
+        sel = std::min<int64_t>(sel + std::min<int64_t>(v, PAS_GAS_MAX_SELECTIONS + 1),
+                                PAS_GAS_MAX_SELECTIONS + 1);
       }
     }
     if (sel > PAS_GAS_MAX_SELECTIONS)
-      return set_error(ctx, PAS_ECAPACITY, "pod " + std::to_string(p) +
-                                               " needs more than 8 card selections");
+      return set_error(ctx, PAS_ECAPACITY,
+                       "pod " + std::to_string(p) + " needs more than " +
+                           std::to_string(PAS_GAS_MAX_SELECTIONS) + " card selections");
   }
   if ((rc = activate(ctx))) return rc;
   const int64_t N = ctx->gas.n_nodes;
@@ -752,12 +800,15 @@ int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containe
   const size_t b_mask = sizeof(uint32_t) * (size_t)n_pods * C;
   const size_t b_nc = sizeof(int32_t) * (size_t)n_pods;
   const size_t b_res = sizeof(uint32_t) * (size_t)n_pods * (size_t)N;
-  if ((rc = ensure_scratch(ctx, carve_size({b_req, b_mask, b_nc, b_res})))) return rc;
+  const size_t b_side = sizeof(pas_gas_selection) * (size_t)side_cap;
+  if ((rc = ensure_scratch(ctx, carve_size({b_req, b_mask, b_nc, b_res, b_side, 8})))) return rc;
   Carve cv{static_cast<char*>(ctx->scratch)};
   int64_t* d_req = cv.take<int64_t>((size_t)n_pods * C * Q);
   uint32_t* d_mask = cv.take<uint32_t>((size_t)n_pods * C);
   int32_t* d_nc = cv.take<int32_t>(n_pods);
   uint32_t* d_res = cv.take<uint32_t>((size_t)n_pods * N);
+  pas_gas_selection* d_side = cv.take<pas_gas_selection>((size_t)side_cap);
+  int64_t* d_count = cv.take<int64_t>(1);
   hipStream_t s = ctx->stream;
   if (max_containers > 0) {
     PAS_HIP(ctx, hipMemcpyAsync(d_req, req, b_req, hipMemcpyHostToDevice, s));
@@ -765,27 +816,94 @@ int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containe
   }
   PAS_HIP(ctx, hipMemcpyAsync(d_nc, n_containers, b_nc, hipMemcpyHostToDevice, s));
   rc = gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_mask, d_nc, d_res,
-                      nullptr, s);
+                      nullptr, side_cap > 0 ? d_side : nullptr, side_cap,
+                      side_count ? d_count : nullptr, s);
   if (rc) return rc;
   if (b_res) PAS_HIP(ctx, hipMemcpyAsync(res_out, d_res, b_res, hipMemcpyDeviceToHost, s));
+  int64_t count = 0;
+  if (side_count)
+    PAS_HIP(ctx, hipMemcpyAsync(&count, d_count, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   PAS_HIP(ctx, hipStreamSynchronize(s));
+  if (side_count) {
+    *side_count = count;
+    const int64_t got = std::min(count, side_cap);
+    if (got > 0)
+      PAS_HIP(ctx, hipMemcpy(side, d_side, sizeof(pas_gas_selection) * (size_t)got,
+                             hipMemcpyDeviceToHost));
+  }
   return PAS_OK;
+}
+
+int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                const int32_t* n_containers, uint32_t* res_out) {
+  return gas_fit_host(ctx, gen, n_pods, max_containers, i915_index, req, req_mask, n_containers,
+                      res_out, nullptr, 0, nullptr, "pas_gas_fit");
+}
+
+int pas_gas_fit_ex(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                   int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
+                   const int32_t* n_containers, uint32_t* res_out, pas_gas_selection* side,
+                   int64_t side_cap, int64_t* side_count) {
+  if (!ctx) return PAS_EINVAL;
+  if (!side_count) return set_error(ctx, PAS_EINVAL, "pas_gas_fit_ex: null side_count");
+  return gas_fit_host(ctx, gen, n_pods, max_containers, i915_index, req, req_mask, n_containers,
+                      res_out, side, side_cap, side_count, "pas_gas_fit_ex");
+}
+
+static int gas_fit_device_common(pas_ctx* ctx, uint64_t gen, int32_t n_pods,
+                                 int32_t max_containers, int32_t i915_index,
+                                 const int64_t* d_req, const uint32_t* d_req_mask,
+                                 const int32_t* d_n_containers, uint32_t* d_res_out,
+                                 uint64_t* d_fit_out, pas_gas_selection* d_side, int64_t side_cap,
+                                 int64_t* d_side_count, void* hip_stream, const char* fn) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_gas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_pods < 0 || max_containers < 0 || i915_index >= ctx->gas.n_res || i915_index < -1 ||
+      side_cap < 0)
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad shape");
+  if (n_pods > 0 && (!d_n_containers || (!d_res_out && !d_fit_out) ||
+                     (max_containers > 0 && (!d_req || !d_req_mask)) || (side_cap > 0 && !d_side)))
+    return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
+  if ((rc = activate(ctx))) return rc;
+  return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                        d_n_containers, d_res_out, d_fit_out, side_cap > 0 ? d_side : nullptr,
+                        side_cap, d_side_count, pick_stream(ctx, hip_stream));
 }
 
 int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
                        int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
                        const int32_t* d_n_containers, uint32_t* d_res_out, void* hip_stream) {
-  if (!ctx) return PAS_EINVAL;
-  int rc = check_gas_gen(ctx, gen);
-  if (rc) return rc;
-  if (n_pods < 0 || max_containers < 0 || i915_index >= ctx->gas.n_res || i915_index < -1)
-    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_device: bad shape");
-  if (n_pods == 0) return PAS_OK;
-  if (!d_n_containers || !d_res_out || (max_containers > 0 && (!d_req || !d_req_mask)))
+  if (ctx && !d_res_out && n_pods > 0)
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_device: null input");
-  if ((rc = activate(ctx))) return rc;
-  return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                        d_n_containers, d_res_out, nullptr, pick_stream(ctx, hip_stream));
+  return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                               d_n_containers, d_res_out, nullptr, nullptr, 0, nullptr,
+                               hip_stream, "pas_gas_fit_device");
+}
+
+int pas_gas_fit_ex_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                          int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
+                          const int32_t* d_n_containers, uint32_t* d_res_out,
+                          pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
+                          void* hip_stream) {
+  if (ctx && ((!d_res_out && n_pods > 0) || !d_side_count))
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_ex_device: null input");
+  return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                               d_n_containers, d_res_out, nullptr, d_side, side_cap,
+                               d_side_count, hip_stream, "pas_gas_fit_ex_device");
+}
+
+int pas_gas_limit_count(pas_ctx* ctx, int64_t* n_pods_out) {
+  if (!ctx) return PAS_EINVAL;
+  if (!n_pods_out) return set_error(ctx, PAS_EINVAL, "pas_gas_limit_count: null output");
+  *n_pods_out = 0;
+  if (!ctx->gas_limit) return PAS_OK;  // no fit on this context yet
+  int rc = activate(ctx);
+  if (rc) return rc;
+  PAS_HIP(ctx, hipEventSynchronize(ctx->gas_limit_ev));
+  PAS_HIP(ctx, hipMemcpy(n_pods_out, ctx->gas_limit, sizeof(int64_t), hipMemcpyDeviceToHost));
+  return PAS_OK;
 }
 
 int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
@@ -797,12 +915,11 @@ int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_
   if (rc) return rc;
   if (n_pods < 0 || max_containers < 0 || i915_index >= ctx->gas.n_res || i915_index < -1)
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_bitmap_device: bad shape");
-  if (n_pods == 0) return PAS_OK;
-  if (!d_n_containers || !d_fit_out || (max_containers > 0 && (!d_req || !d_req_mask)))
+  if (n_pods > 0 && !d_fit_out)
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_bitmap_device: null input");
-  if ((rc = activate(ctx))) return rc;
-  return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                        d_n_containers, nullptr, d_fit_out, pick_stream(ctx, hip_stream));
+  return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                               d_n_containers, nullptr, d_fit_out, nullptr, 0, nullptr,
+                               hip_stream, "pas_gas_fit_bitmap_device");
 }
 
 // --------------------------------------------------------------------------- deschedule labels

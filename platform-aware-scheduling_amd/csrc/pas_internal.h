@@ -97,6 +97,8 @@ struct pas_ctx {
   void* aux = nullptr;  // per-call device table: TAS rule ranges / GAS container steps
   size_t aux_bytes = 0;
   int64_t* label_part = nullptr;  // per-workgroup partial counts of the label plan
+  int64_t* gas_limit = nullptr;     // pods of the last GAS fit past PAS_GAS_MAX_SELECTIONS
+  hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;
@@ -142,6 +144,7 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
                    const int32_t* d_n_containers, uint32_t* d_res, uint64_t* d_fit,
+                   pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
                    hipStream_t s);
 int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
@@ -156,7 +159,8 @@ int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_con
                       int32_t i915_index, const int32_t* d_order, const int32_t* d_seg_off,
                       const int32_t* d_pod, const int32_t* d_node, const int64_t* d_req,
                       const uint32_t* d_mask, const int32_t* d_ncont, const int32_t* d_cpc,
-                      const int32_t* d_cards, uint32_t* d_res, int32_t* d_status,
+                      const int32_t* d_cards, int32_t cards_stride, uint32_t* d_res,
+                      int32_t* d_status, uint8_t* d_cards_out, int32_t* d_nsel_out,
                       hipStream_t s);
 int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
                       const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,

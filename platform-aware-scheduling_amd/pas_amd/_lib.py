@@ -8,6 +8,8 @@ from __future__ import annotations
 
 import ctypes
 import os
+
+import numpy as np
 from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint32, c_uint64, c_void_p
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
@@ -41,9 +43,12 @@ PAS_OP_EQUALS = 2
 PAS_TAS_FILTER = 1
 PAS_TAS_PRIORITIZE = 2
 
-PAS_GAS_MAX_CARDS = 8
+PAS_GAS_MAX_CARDS = 64
 PAS_GAS_MAX_RES = 4
-PAS_GAS_MAX_SELECTIONS = 8
+PAS_GAS_MAX_SELECTIONS = 64
+PAS_GAS_PACKED = 8
+PAS_GAS_SEL_EXTENDED = 15
+PAS_GAS_SEL_LIMIT = 14
 
 PAS_GAS_OK = 0
 PAS_GAS_WONT_FIT = 1
@@ -76,6 +81,12 @@ class PasError(RuntimeError):
 
 class PasConfig(ctypes.Structure):
     _fields_ = [("device", c_int32), ("reserved", c_int32)]
+
+
+# pas_gas_selection (include/pas.h) as a numpy record: the side buffer of pas_gas_fit_ex.
+GAS_SELECTION_DTYPE = np.dtype([("pod", np.int32), ("node", np.int32), ("n_sel", np.int32),
+                                ("reserved", np.int32), ("card", np.uint8, (PAS_GAS_MAX_SELECTIONS,))])
+assert GAS_SELECTION_DTYPE.itemsize == 16 + PAS_GAS_MAX_SELECTIONS
 
 
 # Every exported symbol with (restype, argtypes); tests check this list against pas.h.
@@ -119,6 +130,15 @@ SIGNATURES = {
         c_int,
         [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
     ),
+    "pas_gas_fit_ex": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_int64, POINTER(c_int64)],
+    ),
+    "pas_gas_fit_ex_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P],
+    ),
+    "pas_gas_limit_count": (c_int, [_P, POINTER(c_int64)]),
     "pas_gas_fit_bitmap_device": (
         c_int,
         [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
@@ -127,7 +147,16 @@ SIGNATURES = {
         c_int,
         [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P],
     ),
+    "pas_gas_bind_ex": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P,
+         _P, _P],
+    ),
     "pas_gas_release": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, _P, _P, _P, _P, _P, _P],
+    ),
+    "pas_gas_release_ex": (
         c_int,
         [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, _P, _P, _P, _P, _P, _P],
     ),

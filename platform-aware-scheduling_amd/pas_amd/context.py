@@ -304,10 +304,51 @@ class Context:
         self._check(rc, "pas_gas_fit")
         return out
 
+    def gas_fit_ex(self, gen: int, req: np.ndarray, req_mask: np.ndarray,
+                   n_containers: np.ndarray, i915_index: int, side_cap: int = 1024):
+        """pas_gas_fit_ex: (words [P][N], side records) — one GAS_SELECTION_DTYPE record per
+        PAS_GAS_SEL_EXTENDED word (sorted by pod, node).  A side buffer that was too small is
+        grown to the reported count and the call repeated."""
+        req = np.ascontiguousarray(req, dtype=np.int64)
+        p, c, q = req.shape
+        req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
+        n_containers = np.ascontiguousarray(n_containers, dtype=np.int32)
+        assert req_mask.shape == (p, c) and n_containers.shape == (p,)
+        out = np.zeros((p, self.gas_shape[0]), np.uint32)
+        while True:
+            side = np.zeros(max(side_cap, 1), _lib.GAS_SELECTION_DTYPE)
+            count = c_int64(0)
+            rc = self._l.pas_gas_fit_ex(self._h, gen, p, c, i915_index, _ptr(req), _ptr(req_mask),
+                                        _ptr(n_containers), _ptr(out), _ptr(side), side_cap,
+                                        byref(count))
+            self._check(rc, "pas_gas_fit_ex")
+            if count.value <= side_cap:
+                break
+            side_cap = count.value
+        side = side[:count.value]
+        return out, side[np.lexsort((side["node"], side["pod"]))]
+
+    def gas_fit_ex_device(self, gen: int, n_pods: int, max_containers: int, i915_index: int,
+                          req_t, mask_t, ncont_t, res_t, side_t, side_cap: int, count_t,
+                          stream=None):
+        rc = self._l.pas_gas_fit_ex_device(self._h, gen, n_pods, max_containers, i915_index,
+                                           _dptr(req_t), _dptr(mask_t), _dptr(ncont_t),
+                                           _dptr(res_t), _dptr(side_t), side_cap, _dptr(count_t),
+                                           _stream(stream))
+        self._check(rc, "pas_gas_fit_ex_device")
+
+    def gas_limit_count(self) -> int:
+        """Pods of the last GAS fit beyond PAS_GAS_MAX_SELECTIONS (pas_gas_limit_count)."""
+        v = c_int64(0)
+        self._check(self._l.pas_gas_limit_count(self._h, byref(v)), "pas_gas_limit_count")
+        return v.value
+
     def gas_bind(self, gen_from: int, gen_to: int, pods, nodes, req: np.ndarray,
-                 req_mask: np.ndarray, n_containers: np.ndarray, i915_index: int):
+                 req_mask: np.ndarray, n_containers: np.ndarray, i915_index: int,
+                 selections: bool = False):
         """GASExtender.bindNode for binds (pods[b] -> nodes[b]) in order, committed into the
-        resident usage.  Returns (result words, statuses)."""
+        resident usage.  Returns (result words, statuses), plus (cards [B][64], n_sel [B]) with
+        selections=True (pas_gas_bind_ex)."""
         req = np.ascontiguousarray(req, dtype=np.int64)
         p, c, q = req.shape
         req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
@@ -316,16 +357,26 @@ class Context:
         nodes = np.ascontiguousarray(nodes, dtype=np.int32)
         res = np.zeros(len(pods), np.uint32)
         st = np.zeros(len(pods), np.int32)
-        rc = self._l.pas_gas_bind(self._h, gen_from, gen_to, len(pods), _ptr(pods), _ptr(nodes),
-                                  p, c, i915_index, _ptr(req), _ptr(req_mask),
-                                  _ptr(n_containers), _ptr(res), _ptr(st))
-        self._check(rc, "pas_gas_bind")
-        return res, st
+        if not selections:
+            rc = self._l.pas_gas_bind(self._h, gen_from, gen_to, len(pods), _ptr(pods),
+                                      _ptr(nodes), p, c, i915_index, _ptr(req), _ptr(req_mask),
+                                      _ptr(n_containers), _ptr(res), _ptr(st))
+            self._check(rc, "pas_gas_bind")
+            return res, st
+        cards = np.zeros((len(pods), _lib.PAS_GAS_MAX_SELECTIONS), np.uint8)
+        nsel = np.zeros(len(pods), np.int32)
+        rc = self._l.pas_gas_bind_ex(self._h, gen_from, gen_to, len(pods), _ptr(pods),
+                                     _ptr(nodes), p, c, i915_index, _ptr(req), _ptr(req_mask),
+                                     _ptr(n_containers), _ptr(res), _ptr(st), _ptr(cards),
+                                     _ptr(nsel))
+        self._check(rc, "pas_gas_bind_ex")
+        return res, st, cards, nsel
 
     def gas_release(self, gen_from: int, gen_to: int, pods, nodes, req: np.ndarray,
                     req_mask: np.ndarray, n_containers: np.ndarray, cards_per_container,
                     cards) -> np.ndarray:
-        """adjustPodResources(remove) for pods leaving nodes; returns statuses."""
+        """adjustPodResources(remove) for pods leaving nodes; returns statuses.  cards is
+        [R][8] (pas_gas_release) or [R][64] (pas_gas_release_ex)."""
         req = np.ascontiguousarray(req, dtype=np.int64)
         p, c, q = req.shape
         req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
@@ -333,12 +384,14 @@ class Context:
         pods = np.ascontiguousarray(pods, dtype=np.int32)
         nodes = np.ascontiguousarray(nodes, dtype=np.int32)
         cpc = np.ascontiguousarray(cards_per_container, dtype=np.int32).reshape(len(pods), c)
-        cards = np.ascontiguousarray(cards, dtype=np.int32).reshape(len(pods), 8)
+        cards = np.ascontiguousarray(cards, dtype=np.int32)
+        ex = cards.size == len(pods) * _lib.PAS_GAS_MAX_SELECTIONS and cards.size > 0
+        cards = cards.reshape(len(pods), _lib.PAS_GAS_MAX_SELECTIONS if ex else _lib.PAS_GAS_PACKED)
         st = np.zeros(len(pods), np.int32)
-        rc = self._l.pas_gas_release(self._h, gen_from, gen_to, len(pods), _ptr(pods),
-                                     _ptr(nodes), p, c, _ptr(req), _ptr(req_mask),
-                                     _ptr(n_containers), _ptr(cpc), _ptr(cards), _ptr(st))
-        self._check(rc, "pas_gas_release")
+        fn = self._l.pas_gas_release_ex if ex else self._l.pas_gas_release
+        rc = fn(self._h, gen_from, gen_to, len(pods), _ptr(pods), _ptr(nodes), p, c, _ptr(req),
+                _ptr(req_mask), _ptr(n_containers), _ptr(cpc), _ptr(cards), _ptr(st))
+        self._check(rc, "pas_gas_release_ex" if ex else "pas_gas_release")
         return st
 
     def gas_snapshot_get(self):

@@ -114,8 +114,6 @@ class MetricsExtender:
         items, idx = self._request_nodes(nodes)
         if policy is None or not rules or len(items) == 0:
             return 404, b"null\n"  # nil FilterResult (:189-203)
-        if (idx < 0).any():
-            raise KeyError("request node not in the snapshot")
         r = self._rules(rules)
         pass_out, _, _ = self.ctx.tas_eval(self.gen, r, np.array([0, len(r)], np.int32),
                                            make_rules([-1], [0], [0]), self._cand(idx),
@@ -123,10 +121,12 @@ class MetricsExtender:
         blobs = [json.dumps(it, separators=(",", ":")).encode() for it in items]
         table = wire.NodeTable([_node_name(it) for it in items], blobs)
         order = np.arange(len(items), dtype=np.int32)
-        # the pass row re-indexed to the request's own order (duplicates keep their verdict)
+        # the pass row re-indexed to the request's own order (duplicates keep their verdict);
+        # a node without metrics in the snapshot is in no violating set, so it passes
+        # (dontschedule/strategy.go:25-44 only ranges over the metric cache's nodes)
         row = np.zeros(w64(len(items)), np.uint64)
         for j, i in enumerate(idx):
-            if (int(pass_out[0, i >> 6]) >> (int(i) & 63)) & 1:
+            if i < 0 or (int(pass_out[0, i >> 6]) >> (int(i) & 63)) & 1:
                 row[j >> 6] |= np.uint64(1 << (j & 63))
         return 200, wire.tas_filter_result(order, row, table)
 
@@ -154,8 +154,8 @@ class MetricsExtender:
             return status, b"[]\n"
         if prio[0][0] not in self.metric_index:  # ReadMetric error -> [] (:130-133)
             return status, b"[]\n"
-        if (idx < 0).any():
-            raise KeyError("request node not in the snapshot")
+        # nodes without metrics in the snapshot are left out, as filteredNodeData keeps only
+        # nodes with a metric (telemetryscheduler.go:128-149): _cand skips them
         code = parse_operator(prio[0][1])
         p = make_rules([self.metric_index[prio[0][0]]], [code if code >= 0 else 3],
                        [int(prio[0][2])])
@@ -242,14 +242,15 @@ class GASExtender:
         req, mask, ncont, per_container = self._requests(pod)
         if node is None:  # runSchedulingLogic -> FetchNode error (:282-288)
             return 404, self._error(f'node "{node_name}" not found')
-        res, st = self.ctx.gas_bind(self.gen, self.gen + 1, [0], [node], req, mask, ncont,
-                                    self.i915)
+        res, st, cards, nsel = self.ctx.gas_bind(self.gen, self.gen + 1, [0], [node], req, mask,
+                                                 ncont, self.i915, selections=True)
         self.gen += 1
         if st[0] != _lib.PAS_GAS_OK:
             return 404, self._error("will not fit")  # errWontFit (:49)
         from .snapshot import annotation
         pod.setdefault("metadata", {}).setdefault("annotations", {})[
-            "gas-container-cards"] = annotation(int(res[0]), per_container, self.card_names[node])
+            "gas-container-cards"] = annotation(int(res[0]), per_container, self.card_names[node],
+                                                cards[0, : nsel[0]])
         return 200, wire.binding_result("")
 
     def prioritize(self, body: bytes) -> Tuple[int, bytes]:

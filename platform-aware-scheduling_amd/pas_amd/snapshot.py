@@ -68,31 +68,32 @@ def gas_snapshot_from_nodes(nodes: Sequence[Optional[dict]], kinds: Sequence[str
     """(n_cards [N] int32, cap_per_gpu [N][Q] int64, used [N][K][Q] int64, card_names) from
     per-node dicts {"labels": {...}, "allocatable": {resource: quantity}, "usage":
     {card: {resource: int}}}, or None for a node the lister does not know.  card_names[n]
-    lists the node's cards in rank order (rank = the 3-bit index in a pas_gas_fit word)."""
+    lists the node's cards in rank order (rank = the 3-bit index in a pas_gas_fit word, or the
+    byte of a pas_gas_selection record).  K is the largest card count of the nodes (at least
+    1); a node with more than max_cards cards is PAS_ECAPACITY."""
     q = len(kinds)
-    k_max = max_cards
     n = len(nodes)
     n_cards = np.zeros(n, np.int32)
-    cap = np.zeros((n, q), np.int64)
-    used = np.zeros((n, k_max, q), np.int64)
     card_names: List[List[str]] = []
     for i, node in enumerate(nodes):
-        if node is None:
-            n_cards[i] = -1
+        labels = (node.get("labels") or {}) if node is not None else {}
+        if node is None or GPU_LIST_LABEL not in labels:
+            n_cards[i] = -1 if node is None else 0
             card_names.append([])
             continue
-        labels = node.get("labels") or {}
-        if GPU_LIST_LABEL not in labels:
-            card_names.append([])
-            continue
-        gpus = labels[GPU_LIST_LABEL].split(".")
-        gpu_count = len(gpus)
-        cards = go_sort_strings(set(gpus))
-        if len(cards) > k_max:
+        cards = go_sort_strings(set(labels[GPU_LIST_LABEL].split(".")))
+        if len(cards) > max_cards:
             raise _lib.PasError(_lib.PAS_ECAPACITY,
-                                f"node {i}: {len(cards)} cards > {k_max} (PAS_GAS_MAX_CARDS)")
+                                f"node {i}: {len(cards)} cards > {max_cards} (PAS_GAS_MAX_CARDS)")
         n_cards[i] = len(cards)
         card_names.append(cards)
+    k = max([1] + [len(c) for c in card_names])
+    cap = np.zeros((n, q), np.int64)
+    used = np.zeros((n, k, q), np.int64)
+    for i, node in enumerate(nodes):
+        if n_cards[i] <= 0:
+            continue
+        gpu_count = len(node["labels"][GPU_LIST_LABEL].split("."))
         alloc = node.get("allocatable") or {}
         for j, kind in enumerate(kinds):
             if kind in alloc and kind.startswith(RESOURCE_PREFIX):
@@ -101,17 +102,25 @@ def gas_snapshot_from_nodes(nodes: Sequence[Optional[dict]], kinds: Sequence[str
                 share = abs(value) // gpu_count
                 cap[i, j] = -share if value < 0 else share
         usage: Dict[str, Dict[str, int]] = node.get("usage") or {}
-        for r, card in enumerate(cards):
+        for r, card in enumerate(card_names[i]):
             for j, kind in enumerate(kinds):
                 used[i, r, j] = int(usage.get(card, {}).get(kind, 0))
     return n_cards, cap, used, card_names
 
 
-def annotation(word: int, container_i915: Sequence[int], card_names: Sequence[str]) -> str:
+def annotation(word: int, container_i915: Sequence[int], card_names: Sequence[str],
+               selection=None) -> str:
     """The "gas-container-cards" annotation (scheduler.go:317-335) of a pas_gas_fit word:
     container c takes its next container_i915[c] selections; cards joined by ",", containers
-    by "|"."""
-    ranks = [(int(word) >> (3 * s)) & 7 for s in range((int(word) >> 24) & 15)]
+    by "|".  A PAS_GAS_SEL_EXTENDED word needs its selection (the card ranks of its
+    pas_gas_selection record, or of pas_gas_bind_ex)."""
+    s_field = (int(word) >> 24) & 15
+    if selection is not None:
+        ranks = [int(r) for r in selection]
+    elif s_field == _lib.PAS_GAS_SEL_EXTENDED:
+        raise ValueError("PAS_GAS_SEL_EXTENDED word: pass its selection record")
+    else:
+        ranks = [(int(word) >> (3 * s)) & 7 for s in range(s_field)]
     out, pos = [], 0
     for n in container_i915:
         out.append(",".join(card_names[r] for r in ranks[pos:pos + n]))

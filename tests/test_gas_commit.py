@@ -195,8 +195,8 @@ def test_bind_errors(ctx):
         with pytest.raises(pas_amd.PasError) as e:
             ctx.gas_bind(kw["gen_from"], gen + 1, [0], kw["nodes"], req, mask, one, 0)
         assert e.value.code == code
-    # more than 8 selections -> capacity
+    # more than 64 selections -> capacity
     with pytest.raises(pas_amd.PasError) as e:
-        ctx.gas_bind(gen, gen + 1, [0], [0], req, mask, one, 0)
+        ctx.gas_bind(gen, gen + 1, [0], [0], np.array([[[65]]], np.int64), mask, one, 0)
     assert e.value.code == pas_amd._lib.PAS_ECAPACITY
     assert ctx.gas_snapshot_get()[0] == gen

@@ -96,7 +96,7 @@ def test_c3_shape_pod_sample(ctx, oracle):
 
 def test_selection_capacity_error(ctx):
     req = np.zeros((1, 2, 1), np.int64)
-    req[0, :, 0] = 5  # 10 selections
+    req[0, :, 0] = [40, 25]  # 65 selections: past PAS_GAS_MAX_SELECTIONS
     with pytest.raises(pas_amd.PasError) as e:
         gpu_fit(ctx, np.array([8], np.int32), np.full((1, 1), 100, np.int64),
                 np.zeros((1, 8, 1), np.int64), req, np.ones((1, 2), np.uint32),
