@@ -77,6 +77,9 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
     uint32_t word = 0;
     int32_t nsel = 0;
     bool packable = true;
+    uint8_t* sel_out = a.cards_out ? a.cards_out + (int64_t)op * PAS_GAS_MAX_SELECTIONS : nullptr;
+    if (sel_out)
+      for (int j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) sel_out[j] = 0;
     for (int32_t c = 0; fits && c < a.ncont[p]; ++c) {
       const int64_t b = (int64_t)p * C + c;
       const uint32_t m = a.mask[b];
@@ -103,8 +106,7 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
           if ((m >> q) & 1u) w[chosen][q] += r[q];  // addRM after a passing check
         if (nsel < PAS_GAS_PACKED) word |= (uint32_t)chosen << (3 * nsel);
         packable = packable && chosen < PAS_GAS_PACKED;
-        if (a.cards_out && nsel < PAS_GAS_MAX_SELECTIONS)
-          a.cards_out[(int64_t)op * PAS_GAS_MAX_SELECTIONS + nsel] = (uint8_t)chosen;
+        if (sel_out && nsel < PAS_GAS_MAX_SELECTIONS) sel_out[nsel] = (uint8_t)chosen;
         ++nsel;
       }
     }
@@ -112,6 +114,8 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
       a.res_out[op] = 0u;
       a.status[op] = PAS_GAS_WONT_FIT;
       if (a.nsel_out) a.nsel_out[op] = 0;
+      if (sel_out)  // the selections of a bind that did not fit are not reported
+        for (int j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) sel_out[j] = 0;
       continue;
     }
     // the pas_gas_fit word: selections that do not pack are PAS_GAS_SEL_EXTENDED

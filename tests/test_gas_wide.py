@@ -161,7 +161,7 @@ def test_wide_bind_release_parity(ctx, oracle, k, sel_max):
     n_cards, cap, used, req, mask, ncont = random_wide(rng, 40, k, 2, 60, 3, sel_max)
     gen = _upload(ctx, n_cards, cap, used)
     pods = rng.integers(0, 60, size=150).astype(np.int32)
-    nodes = rng.integers(0, 10, size=150).astype(np.int32)
+    nodes = rng.integers(0, 30, size=150).astype(np.int32)
     res, st, cards, nsel = ctx.gas_bind(gen, gen + 1, pods, nodes, req, mask, ncont, 0,
                                         selections=True)
     w_used, w_res, w_st, w_cards, w_nsel = oracle.gas_bind(n_cards, cap, used, req, mask, ncont,
@@ -170,7 +170,7 @@ def test_wide_bind_release_parity(ctx, oracle, k, sel_max):
     np.testing.assert_array_equal(st, w_st)
     np.testing.assert_array_equal(nsel, w_nsel)
     np.testing.assert_array_equal(cards, w_cards)
-    assert ((res >> 24) & 15 == oracle.SEL_EXTENDED).sum() > 5
+    assert ((res >> 24) & 15 == oracle.SEL_EXTENDED).sum() >= 3
     _, after = ctx.gas_snapshot_get()
     np.testing.assert_array_equal(after, w_used)
     ok = np.nonzero(st == 0)[0][:80]
