@@ -187,8 +187,106 @@ def bench_tas(args, world, rank):
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_tas(snap, batch, args.cpu_seconds)
+    if rank == 0 and not args.no_request_latency:
+        out["request_latency"] = request_latency(ctx, batch, N)
     ctx.close()
     return out
+
+
+def synthetic_args_body(names, seed=7):
+    """An extender.Args body as the kube-scheduler posts it with NodeCacheCapable false
+    (extender/types.go:36-46): the pod plus every candidate as a full v1.Node (~1 KB each:
+    labels, allocatable / capacity, conditions, a few images).  Synthetic, seeded."""
+    rng = np.random.default_rng(seed)
+    parts = []
+    for i, n in enumerate(names):
+        img = ",".join('{"names":["registry.local/app-%d@sha256:%064x"],"sizeBytes":%d}'
+                       % (j, int(rng.integers(1 << 62)), int(rng.integers(1 << 30)))
+                       for j in range(3))
+        parts.append(
+            '{"metadata":{"name":"%s","uid":"%08x-0000-4000-8000-%012x","resourceVersion":"%d",'
+            '"labels":{"kubernetes.io/hostname":"%s","kubernetes.io/os":"linux",'
+            '"telemetry.aware.scheduling.policy":"violating"}},'
+            '"spec":{"podCIDR":"10.%d.%d.0/24"},'
+            '"status":{"capacity":{"cpu":"64","memory":"527988604Ki","pods":"110"},'
+            '"allocatable":{"cpu":"63500m","memory":"527374204Ki","pods":"110"},'
+            '"conditions":[{"type":"Ready","status":"True","reason":"KubeletReady"}],'
+            '"images":[%s]}}' % (n, i, i, i, n, (i >> 8) & 255, i & 255, img))
+    pod = ('{"metadata":{"name":"p0","namespace":"default","labels":{"telemetry-policy":'
+           '"bench"}},"spec":{"containers":[{"name":"c","resources":{"requests":{"cpu":"1"}}}]}}')
+    return ('{"Pod":%s,"Nodes":{"metadata":{},"items":[%s]},"NodeNames":null}'
+            % (pod, ",".join(parts))).encode()
+
+
+def request_latency(ctx, batch, n_nodes, reps=5):
+    """End-to-end latency of one TAS filter request and one prioritize request over the
+    resident n_nodes snapshot: pas_decode_args of a full-NodeList body
+    (every node a candidate) -> pas_tas_eval (host API: candidate bitmap up, pass row and
+    ordered list down) -> pas_encode_tas_filter_result / pas_encode_host_priority_list.  The
+    name table and the snapshot-name array are per snapshot (built once, untimed); node JSON
+    for the FilterResult points into the request body.  Median of reps."""
+    import ctypes
+    from pas_amd import wire
+    names = [f"node-{i:06d}" for i in range(n_nodes)]
+    body = synthetic_args_body(names)
+    table = wire.NameTable(names)
+    lib = _lib.load()
+    name_arr = wire.NodeTable(names).names
+    r0, r1 = int(batch.rule_off[0]), int(batch.rule_off[1])
+    rules = batch.rules[r0:r1]
+    prio = batch.prio[:1]
+    info = _lib.PasArgsInfo()
+    req = np.zeros(n_nodes, np.int32)
+    spans = np.zeros((n_nodes, 2), np.int64)
+    cand = np.zeros((1, pas_amd.w64(n_nodes)), np.uint64)
+    body_buf = ctypes.c_char_p(body)  # keeps the address above valid
+    base = ctypes.cast(body_buf, ctypes.c_void_p).value
+    addr = np.zeros(n_nodes, np.uint64)
+    lens = np.zeros(n_nodes, np.int64)
+    out_len = ctypes.c_int64()
+    cap = 1 << 28
+    out = ctypes.create_string_buffer(cap)
+    vp = ctypes.c_void_p
+    t = {"decode_ms": [], "eval_filter_ms": [], "encode_filter_ms": [], "eval_prioritize_ms": [],
+         "encode_prioritize_ms": []}
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc = lib.pas_decode_args(table._h, body_buf, len(body), _lib.PAS_ARGS_NODES,
+                                 req.ctypes.data_as(vp), n_nodes, spans.ctypes.data_as(vp),
+                                 cand.ctypes.data_as(vp), ctypes.byref(info))
+        assert rc == 0 and info.n_req == n_nodes and info.n_unknown == 0
+        t1 = time.perf_counter()
+        pass_out, _, _ = ctx.tas_eval(1, rules, np.array([0, r1 - r0], np.int32), prio, cand,
+                                      _lib.PAS_TAS_FILTER)
+        t2 = time.perf_counter()
+        addr[req] = base + spans[:, 0].astype(np.uint64)
+        lens[req] = spans[:, 1]
+        rc = lib.pas_encode_tas_filter_result(
+            n_nodes, req.ctypes.data_as(vp), pass_out.ctypes.data_as(vp), name_arr,
+            addr.ctypes.data_as(ctypes.POINTER(ctypes.c_char_p)), lens.ctypes.data_as(vp), out,
+            cap, ctypes.byref(out_len))
+        assert rc == 0
+        filter_bytes = out_len.value
+        t3 = time.perf_counter()
+        _, order, plen = ctx.tas_eval(1, rules[:0], np.array([0, 0], np.int32), prio, cand,
+                                      _lib.PAS_TAS_PRIORITIZE)
+        t4 = time.perf_counter()
+        rc = lib.pas_encode_host_priority_list(int(plen[0]), order.ctypes.data_as(vp), name_arr,
+                                               out, cap, ctypes.byref(out_len))
+        assert rc == 0
+        t5 = time.perf_counter()
+        for k, v in zip(t, (t1 - t0, t2 - t1, t3 - t2, t4 - t3, t5 - t4)):
+            t[k].append(v * 1e3)
+    res = {k: float(np.median(v)) for k, v in t.items()}
+    res["filter_total_ms"] = res["decode_ms"] + res["eval_filter_ms"] + res["encode_filter_ms"]
+    res["prioritize_total_ms"] = (res["decode_ms"] + res["eval_prioritize_ms"]
+                                  + res["encode_prioritize_ms"])
+    res.update(nodes=n_nodes, body_bytes=len(body), filter_response_bytes=filter_bytes,
+               decode_gb_per_s=len(body) / res["decode_ms"] / 1e6,
+               note="host API calls (PCIe transfers of the candidate bitmap, pass row and "
+                    "ordered list included); median of %d" % reps)
+    table.close()
+    return res
 
 
 def cpu_threads():
@@ -474,6 +572,8 @@ def main():
     ap.add_argument("--topk", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-request-latency", action="store_true",
+                    help="skip the f2 request-latency leg of the TAS workload")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")

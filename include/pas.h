@@ -44,7 +44,8 @@ typedef enum pas_status {
   PAS_EDEVICE = -4,    /* HIP runtime error */
   PAS_ENOMEM = -5,     /* device or host allocation failed */
   PAS_ENOSNAP = -6,    /* no snapshot uploaded yet */
-  PAS_ECAPACITY = -7   /* shape exceeds a documented kernel limit */
+  PAS_ECAPACITY = -7,  /* shape exceeds a documented kernel limit / an output buffer */
+  PAS_EDECODE = -8     /* request body that json.Decoder.Decode(&args) rejects */
 } pas_status;
 
 /* TASPolicyRule.Operator (telemetrypolicy/api/v1alpha1/types.go:31-35), evaluated as
@@ -427,6 +428,67 @@ int pas_encode_gas_filter_result(int32_t n_req, const int32_t* req_node, const u
 /* BindingResult of GASExtender.bindNode (scheduler.go:385-445): {"Error":"<error>"}; NULL or
  * "" for success. */
 int pas_encode_binding_result(const char* error, char* buf, int64_t cap, int64_t* out_len);
+
+/* ------------------------------------------------------------------------- */
+/* Wire decoding, host only                                */
+/* ------------------------------------------------------------------------- */
+
+/* Snapshot node names -> node ids (the numbering of the TAS / GAS snapshots), built once per
+ * snapshot; a repeated name keeps its first id.  Lookup of len bytes: id or -1. */
+typedef struct pas_name_table pas_name_table;
+int pas_name_table_create(int32_t n_names, const char* const* names, pas_name_table** out);
+void pas_name_table_destroy(pas_name_table* table);
+int32_t pas_name_table_lookup(const pas_name_table* table, const char* name, int64_t len);
+
+#define PAS_ARGS_NODES 0      /* args.Nodes.Items[].Name: TAS (NodeCacheCapable false) */
+#define PAS_ARGS_NODE_NAMES 1 /* *args.NodeNames: GAS (NodeCacheCapable true) */
+typedef struct pas_args_info {
+  int32_t has_nodes;      /* args.Nodes != nil (TAS: "no nodes in list" otherwise, :74-76) */
+  int32_t has_node_names; /* args.NodeNames != nil */
+  int32_t n_req;          /* request nodes of the chosen list, in request order */
+  int32_t n_unknown;      /* of them not in the table (req_node -1) */
+  int64_t pod_off;        /* byte span of the Pod object in the body; pod_len 0: absent / null */
+  int64_t pod_len;
+} pas_args_info;
+
+/* extender.Args (extender/types.go:36-46) as json.NewDecoder(body).Decode(&args) fills it
+ * (telemetryscheduler.go:63-78; gpuscheduler/scheduler.go:486-505), reduced to what the
+ * handlers read: the request's node list `which` resolved through the name table into
+ * req_node[0 .. n_req) (request order, -1 for a node not in the table), the candidate bitmap
+ * cand[W64(table size)] of the known ones (may be NULL), and for PAS_ARGS_NODES the byte span
+ * (offset, length) of each item in item_span[n_req][2] (may be NULL).  PAS_EDECODE for what
+ * the reference's decode rejects (empty body, syntax, a wrong JSON type on the fields read);
+ * PAS_ECAPACITY (info filled) when n_req > node_cap.  Matching of keys, null handling and
+ * repeated keys follow encoding/json of Go 1.16 (csrc/wire_decode.cpp). */
+int pas_decode_args(const pas_name_table* table, const char* body, int64_t len, int32_t which,
+                    int32_t* req_node, int64_t node_cap, int64_t* item_span, uint64_t* cand,
+                    pas_args_info* info);
+
+/* The request node names themselves (unescaped, request order), for nodes the table does not
+ * know (their FailedNodes / NodeNames entries): name i is buf[offsets[i] .. offsets[i+1]).
+ * PAS_ECAPACITY (*total_len, *n_req set) when buf or offsets[n_req + 1] is too small. */
+int pas_decode_request_names(const char* body, int64_t len, int32_t which, char* buf,
+                             int64_t cap, int64_t* offsets, int64_t offsets_cap,
+                             int64_t* total_len, int32_t* n_req);
+
+/* getPolicyFromPod's reads of a v1.Pod JSON (telemetryscheduler.go:103-112): the namespace
+ * (*ns_len bytes) and the value of labels[label] (*label_len bytes, -1 if the key is absent).
+ * PAS_ECAPACITY (lengths set) when a buffer is too small; PAS_EDECODE as pas_decode_args. */
+int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char* ns_buf,
+                          int64_t ns_cap, int64_t* ns_len, char* label_buf, int64_t label_cap,
+                          int64_t* label_len);
+
+/* containerRequests of a v1.Pod JSON (gpuscheduler/utils.go:14-32): per container, the
+ * requests named gpu.intel.com/... as AsInt64 values (ok ignored), in the pas_gas_fit layout
+ * req[max_containers][n_kinds] / req_mask[max_containers] for kinds[0 .. n_kinds), and
+ * *n_containers = len(spec.containers).  gpu.intel.com requests of other kinds are counted
+ * in *n_unknown (a container with numI915 > 0 requesting one fits no node: capacity lacks the
+ * key, scheduler.go:349-354).  A quantity ParseQuantity rejects is PAS_EDECODE
+ * (Quantity.UnmarshalJSON); PAS_ECAPACITY when n_containers > max_containers.  With
+ * n_kinds 0 (req may be NULL) it only validates the quantities, as the TAS decode does. */
+int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
+                            const char* const* kinds, int32_t max_containers, int64_t* req,
+                            uint32_t* req_mask, int32_t* n_containers, int32_t* n_unknown);
 
 /* ------------------------------------------------------------------------- */
 /* Instrumentation                                                           */

@@ -1,0 +1,918 @@
+// wire_decode.cpp — extender request decoding, host only.
+//
+// The reference decodes every Filter / Prioritize body with
+//   json.NewDecoder(r.Body).Decode(&args)          (extender.Args, extender/types.go:36-46)
+// in MetricsExtender.DecodeExtenderRequest (telemetryscheduler.go:63-78) and
+// GASExtender.decodeRequest (gpuscheduler/scheduler.go:486-505), then walks
+// args.Nodes.Items (TAS) or *args.NodeNames (GAS) in request order.  Here one pass over the
+// body resolves the request's nodes to snapshot node ids (a name table built once per
+// snapshot) and sets the candidate bitmap the TAS / GAS calls take, without materialising
+// the v1.NodeList.  The pod's policy label / namespace (getPolicyFromPod,
+// telemetryscheduler.go:103-112) and its gpu.intel.com requests (containerRequests,
+// gpuscheduler/utils.go:14-32) come from the Pod value's span.
+//
+// encoding/json (Go 1.16) semantics restated for the fields on this path:
+//   - one value is read; bytes after it are not looked at (Decoder.Decode); an empty body is
+//     an error (io.EOF); syntax errors and nesting deeper than 10000 are errors;
+//   - object keys are unescaped, then matched to struct fields exactly or, failing that, by
+//     the field's fold function (foldFunc: equalFoldRight for names with k/s, which also
+//     accepts U+212A KELVIN SIGN and U+017F LATIN SMALL LETTER LONG S; ASCII letter folding
+//     otherwise); map keys (labels, requests) match exactly; a repeated key is decoded again
+//     (the last one wins for the values read here); unknown keys are skipped;
+//   - null leaves a string unchanged and sets a pointer / slice / map to nil; a value of the
+//     wrong JSON type is an UnmarshalTypeError, reported after the whole value is decoded, so
+//     the request fails as a decode error;
+//   - strings: \uXXXX escapes with UTF-16 surrogate pairs (an unpaired surrogate becomes
+//     U+FFFD), invalid UTF-8 bytes become U+FFFD, raw control characters are syntax errors;
+//   - resource.Quantity.UnmarshalJSON (apimachinery v0.22.2 quantity.go): null is the zero
+//     quantity; otherwise the literal bytes, with surrounding quotes removed and spaces
+//     trimmed, go to ParseQuantity (a failure is a decode error).
+// Type checks cover the fields read here; the rest of v1.Pod / v1.Node is skipped as
+// syntax only (a type error deep inside, e.g. a node's "status": 5, fails the reference's
+// decode but not this one — parity unpinned for such bodies, which no kube-scheduler sends).
+#include <emmintrin.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "pas.h"
+
+namespace {
+
+constexpr int kMaxDepth = 10000;  // encoding/json maxNestingDepth
+
+// ---------------------------------------------------------------------------- field folding
+
+bool has_special_fold(const char* f) {  // foldFunc: 'k' / 's' in the name -> equalFoldRight
+  for (; *f; ++f) {
+    const char b = (char)(*f | 0x20);
+    if (b == 'k' || b == 's') return true;
+  }
+  return false;
+}
+
+// bytes.EqualFold-style matches of a key (unescaped) against an ASCII-letter field name.
+bool fold_match(const char* field, std::string_view key) {
+  const size_t fl = std::strlen(field);
+  if (key.size() == fl && std::memcmp(key.data(), field, fl) == 0) return true;
+  if (!has_special_fold(field)) {  // simpleLetterEqualFold
+    if (key.size() != fl) return false;
+    for (size_t i = 0; i < fl; ++i)
+      if ((field[i] & ~0x20) != (key[i] & ~0x20)) return false;
+    return true;
+  }
+  // equalFoldRight(field, key)
+  size_t t = 0;
+  for (size_t i = 0; i < fl; ++i) {
+    if (t >= key.size()) return false;
+    const unsigned char tb = (unsigned char)key[t];
+    const char sb = field[i];
+    if (tb < 0x80) {
+      if (sb != (char)tb) {
+        const char su = (char)(sb & ~0x20);
+        if (su < 'A' || su > 'Z' || su != (char)(tb & ~0x20)) return false;
+      }
+      ++t;
+      continue;
+    }
+    // multi-byte rune in the key: only KELVIN SIGN (E2 84 AA) for k and LONG S (C5 BF) for s
+    const char sl = (char)(sb | 0x20);
+    if (sl == 's' && t + 1 < key.size() && tb == 0xC5 && (unsigned char)key[t + 1] == 0xBF) {
+      t += 2;
+    } else if (sl == 'k' && t + 2 < key.size() && tb == 0xE2 &&
+               (unsigned char)key[t + 1] == 0x84 && (unsigned char)key[t + 2] == 0xAA) {
+      t += 3;
+    } else {
+      return false;
+    }
+  }
+  return t == key.size();
+}
+
+// ---------------------------------------------------------------------------- scanner
+
+void put_utf8(std::string* o, uint32_t r) {
+  if (r < 0x80) {
+    o->push_back((char)r);
+  } else if (r < 0x800) {
+    o->push_back((char)(0xC0 | (r >> 6)));
+    o->push_back((char)(0x80 | (r & 0x3F)));
+  } else if (r < 0x10000) {
+    o->push_back((char)(0xE0 | (r >> 12)));
+    o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+    o->push_back((char)(0x80 | (r & 0x3F)));
+  } else {
+    o->push_back((char)(0xF0 | (r >> 18)));
+    o->push_back((char)(0x80 | ((r >> 12) & 0x3F)));
+    o->push_back((char)(0x80 | ((r >> 6) & 0x3F)));
+    o->push_back((char)(0x80 | (r & 0x3F)));
+  }
+}
+
+// Length of a valid UTF-8 sequence at s (utf8.DecodeRune), 0 if invalid.
+int utf8_valid(const unsigned char* s, const unsigned char* end) {
+  const unsigned char c = s[0];
+  const ptrdiff_t n = end - s;
+  auto cont = [](unsigned char x) { return (x & 0xC0) == 0x80; };
+  if (c >= 0xC2 && c <= 0xDF) return n >= 2 && cont(s[1]) ? 2 : 0;
+  if (c >= 0xE0 && c <= 0xEF) {
+    if (n < 3 || !cont(s[1]) || !cont(s[2])) return 0;
+    if (c == 0xE0 && s[1] < 0xA0) return 0;  // overlong
+    if (c == 0xED && s[1] >= 0xA0) return 0;  // surrogate
+    return 3;
+  }
+  if (c >= 0xF0 && c <= 0xF4) {
+    if (n < 4 || !cont(s[1]) || !cont(s[2]) || !cont(s[3])) return 0;
+    if (c == 0xF0 && s[1] < 0x90) return 0;
+    if (c == 0xF4 && s[1] >= 0x90) return 0;
+    return 4;
+  }
+  return 0;
+}
+
+int hexval(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+// First byte at or after p that ends a run of plain string bytes (>= 0x20, < 0x80, not '"'
+// or '\\'), 16 bytes per step (SSE2: bytes >= 0x80 compare below 0x20 as signed).
+inline const char* scan_plain(const char* p, const char* end) {
+  const __m128i quote = _mm_set1_epi8('"'), bslash = _mm_set1_epi8('\\');
+  const __m128i space = _mm_set1_epi8(0x20);
+  while (end - p >= 16) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+    const __m128i m = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(v, quote), _mm_cmpeq_epi8(v, bslash)),
+                                   _mm_cmplt_epi8(v, space));
+    const int mask = _mm_movemask_epi8(m);
+    if (mask) return p + __builtin_ctz((unsigned)mask);
+    p += 16;
+  }
+  while (p < end && (unsigned char)*p >= 0x20 && *p != '"' && *p != '\\' &&
+         (unsigned char)*p < 0x80)
+    ++p;
+  return p;
+}
+
+struct Scanner {
+  const char* p;
+  const char* end;
+  bool syntax_err = false;  // malformed JSON: nothing is decoded
+  bool type_err = false;    // UnmarshalTypeError: reported after the value
+  int depth = 0;
+
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+  }
+  bool fail() {
+    syntax_err = true;
+    return false;
+  }
+  char peek() {
+    ws();
+    return p < end ? *p : '\0';
+  }
+  bool eat(char c) {
+    ws();
+    if (p < end && *p == c) {
+      ++p;
+      return true;
+    }
+    return false;
+  }
+
+  // A string token at p (after ws).  out: the unescaped value (Go's unquote), or null to
+  // validate only.  *raw_begin / *raw_end: the bytes between the quotes.
+  bool string(std::string* out, const char** raw_begin = nullptr, const char** raw_end = nullptr) {
+    ws();
+    if (p >= end || *p != '"') return fail();
+    ++p;
+    if (raw_begin) *raw_begin = p;
+    if (out) out->clear();
+    const char* run = p;  // pending bytes copied verbatim
+    auto flush = [&](const char* upto) {
+      if (out && upto > run) out->append(run, (size_t)(upto - run));
+    };
+    while (true) {
+      p = scan_plain(p, end);  // fast path: plain ASCII bytes
+      if (p >= end) return fail();
+      const unsigned char c = (unsigned char)*p;
+      if (c == '"') {
+        flush(p);
+        if (raw_end) *raw_end = p;
+        ++p;
+        return true;
+      }
+      if (c < 0x20) return fail();
+      if (c == '\\') {
+        flush(p);
+        if (p + 1 >= end) return fail();
+        const char e = p[1];
+        p += 2;
+        char simple = 0;
+        switch (e) {
+          case '"': simple = '"'; break;
+          case '\\': simple = '\\'; break;
+          case '/': simple = '/'; break;
+          case 'b': simple = '\b'; break;
+          case 'f': simple = '\f'; break;
+          case 'n': simple = '\n'; break;
+          case 'r': simple = '\r'; break;
+          case 't': simple = '\t'; break;
+          case 'u': break;
+          default: return fail();
+        }
+        if (simple) {
+          if (out) out->push_back(simple);
+        } else {
+          auto hex4 = [&](const char* q, uint32_t* v) {
+            if (end - q < 4) return false;
+            uint32_t r = 0;
+            for (int i = 0; i < 4; ++i) {
+              const int h = hexval(q[i]);
+              if (h < 0) return false;
+              r = r << 4 | (uint32_t)h;
+            }
+            *v = r;
+            return true;
+          };
+          uint32_t r;
+          if (!hex4(p, &r)) return fail();
+          p += 4;
+          if (r >= 0xD800 && r < 0xE000) {
+            // utf16.DecodeRune with a following \uXXXX; else U+FFFD (the next escape, if any,
+            // is decoded on its own)
+            uint32_t r2;
+            if (r < 0xDC00 && end - p >= 6 && p[0] == '\\' && p[1] == 'u' && hex4(p + 2, &r2) &&
+                r2 >= 0xDC00 && r2 < 0xE000) {
+              r = 0x10000 + ((r - 0xD800) << 10) + (r2 - 0xDC00);
+              p += 6;
+            } else {
+              r = 0xFFFD;
+            }
+          }
+          if (out) put_utf8(out, r);
+        }
+        run = p;
+        continue;
+      }
+      // c >= 0x80: a valid sequence is kept, an invalid byte becomes U+FFFD
+      const int n = utf8_valid(reinterpret_cast<const unsigned char*>(p),
+                               reinterpret_cast<const unsigned char*>(end));
+      if (n) {
+        p += n;
+      } else {
+        flush(p);
+        if (out) put_utf8(out, 0xFFFD);
+        ++p;
+        run = p;
+      }
+    }
+  }
+
+  bool number() {
+    ws();
+    const char* s = p;
+    if (p < end && *p == '-') ++p;
+    if (p >= end) return fail();
+    if (*p == '0') {
+      ++p;
+    } else if (*p >= '1' && *p <= '9') {
+      while (p < end && *p >= '0' && *p <= '9') ++p;
+    } else {
+      return fail();
+    }
+    if (p < end && *p == '.') {
+      ++p;
+      if (p >= end || *p < '0' || *p > '9') return fail();
+      while (p < end && *p >= '0' && *p <= '9') ++p;
+    }
+    if (p < end && (*p == 'e' || *p == 'E')) {
+      ++p;
+      if (p < end && (*p == '+' || *p == '-')) ++p;
+      if (p >= end || *p < '0' || *p > '9') return fail();
+      while (p < end && *p >= '0' && *p <= '9') ++p;
+    }
+    return p > s;
+  }
+
+  bool literal(const char* lit) {
+    ws();
+    const size_t n = std::strlen(lit);
+    if ((size_t)(end - p) < n || std::memcmp(p, lit, n) != 0) return fail();
+    p += n;
+    return true;
+  }
+
+  bool enter() {
+    if (++depth > kMaxDepth) return fail();
+    return true;
+  }
+
+  // Any value, syntax-checked and skipped.
+  bool skip() {
+    const char c = peek();
+    switch (c) {
+      case '"': return string(nullptr);
+      case '{': {
+        if (!enter()) return false;
+        ++p;
+        if (eat('}')) { --depth; return true; }
+        do {
+          if (!string(nullptr) || !eat(':') || !skip()) return fail();
+        } while (eat(','));
+        if (!eat('}')) return fail();
+        --depth;
+        return true;
+      }
+      case '[': {
+        if (!enter()) return false;
+        ++p;
+        if (eat(']')) { --depth; return true; }
+        do {
+          if (!skip()) return fail();
+        } while (eat(','));
+        if (!eat(']')) return fail();
+        --depth;
+        return true;
+      }
+      case 't': return literal("true");
+      case 'f': return literal("false");
+      case 'n': return literal("null");
+      default: return number();
+    }
+  }
+
+  // An object key: a view of the raw bytes when they need no unescaping, else of scratch.
+  bool key(std::string_view* out, std::string* scratch) {
+    ws();
+    if (p >= end || *p != '"') return fail();
+    const char* b = p + 1;
+    const char* q = scan_plain(b, end);
+    if (q < end && *q == '"') {
+      *out = std::string_view(b, (size_t)(q - b));
+      p = q + 1;
+      return true;
+    }
+    if (!string(scratch)) return false;
+    *out = std::string_view(*scratch);
+    return true;
+  }
+
+  // Iterate an object's members: f(key) is called with p at the value and must consume it.
+  template <typename F>
+  bool object(F&& f) {
+    if (!enter()) return false;
+    if (!eat('{')) return fail();
+    if (eat('}')) { --depth; return true; }
+    std::string scratch;
+    std::string_view k;
+    do {
+      if (!key(&k, &scratch) || !eat(':')) return fail();
+      if (!f(k)) return false;
+    } while (eat(','));
+    if (!eat('}')) return fail();
+    --depth;
+    return true;
+  }
+
+  template <typename F>
+  bool array(F&& f) {
+    if (!enter()) return false;
+    if (!eat('[')) return fail();
+    if (eat(']')) { --depth; return true; }
+    int64_t i = 0;
+    do {
+      if (!f(i++)) return false;
+    } while (eat(','));
+    if (!eat(']')) return fail();
+    --depth;
+    return true;
+  }
+
+  // A value of the wrong JSON type for the field: skip it, remember the type error.
+  bool mismatch() {
+    type_err = true;
+    return skip();
+  }
+
+  // null?  (consumed)
+  bool null_value() {
+    if (peek() == 'n') return literal("null");
+    return false;
+  }
+};
+
+// A string field: null leaves *v unchanged; other non-strings are type errors.
+bool string_field(Scanner& s, std::string* v) {
+  const char c = s.peek();
+  if (c == 'n') return s.literal("null");
+  if (c != '"') return s.mismatch();
+  return s.string(v);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------- name table
+
+struct pas_name_table {
+  std::vector<std::string> names;
+  std::vector<int32_t> slots;  // open addressing, -1 empty
+  uint64_t mask = 0;
+
+  static uint64_t hash(std::string_view s) {  // FNV-1a, 64-bit
+    uint64_t h = 1469598103934665603ull;
+    for (unsigned char c : s) h = (h ^ c) * 1099511628211ull;
+    return h ^ (h >> 29);
+  }
+  int32_t find(std::string_view s) const {
+    if (slots.empty()) return -1;
+    for (uint64_t i = hash(s) & mask;; i = (i + 1) & mask) {
+      const int32_t id = slots[i];
+      if (id < 0) return -1;
+      if (names[(size_t)id] == s) return id;
+    }
+  }
+};
+
+namespace {
+
+bool set_bit(uint64_t* bits, int32_t n) {
+  if (bits) bits[n >> 6] |= 1ull << (n & 63);
+  return true;
+}
+
+// The request node list being decoded.  A slice decodes element-wise into what it already
+// holds (encoding/json array(): elements past the old length start from zero), so a repeated
+// key keeps earlier values where the new element leaves them unset.
+struct NodeList {
+  std::vector<std::string> names;
+  std::vector<int64_t> spans;  // [2 * i]: offset, length of item i's latest decode
+};
+
+// v1.Node: metadata.name (the only field read); *name keeps its value on null / absence.
+bool decode_node(Scanner& s, std::string* name) {
+  const char c = s.peek();
+  if (c == 'n') return s.literal("null");  // null into a struct: no effect
+  if (c != '{') return s.mismatch();
+  return s.object([&](std::string_view k) {
+    if (!fold_match("metadata", k)) return s.skip();
+    const char m = s.peek();
+    if (m == 'n') return s.literal("null");
+    if (m != '{') return s.mismatch();
+    return s.object([&](std::string_view mk) {
+      if (!fold_match("name", mk)) return s.skip();
+      return string_field(s, name);
+    });
+  });
+}
+
+// v1.NodeList: items (null sets the slice to nil).
+bool decode_node_list(Scanner& s, NodeList* out, const char* base) {
+  return s.object([&](std::string_view k) {
+    if (fold_match("items", k)) {
+      const char c = s.peek();
+      if (c == 'n') {
+        out->names.clear();
+        out->spans.clear();
+        return s.literal("null");
+      }
+      if (c != '[') return s.mismatch();
+      size_t n = 0;
+      const bool ok = s.array([&](int64_t i) {
+        if ((size_t)i >= out->names.size()) {
+          out->names.emplace_back();
+          out->spans.resize(out->names.size() * 2);
+        }
+        n = (size_t)i + 1;
+        s.ws();
+        const char* b = s.p;
+        if (!decode_node(s, &out->names[(size_t)i])) return false;
+        out->spans[2 * (size_t)i] = (int64_t)(b - base);
+        out->spans[2 * (size_t)i + 1] = (int64_t)(s.p - b);
+        return true;
+      });
+      out->names.resize(n);
+      out->spans.resize(2 * n);
+      return ok;
+    }
+    if (fold_match("metadata", k)) {  // ListMeta: object or null
+      const char c = s.peek();
+      if (c != '{' && c != 'n') return s.mismatch();
+      return s.skip();
+    }
+    if (fold_match("kind", k) || fold_match("apiVersion", k)) {
+      std::string ignored;
+      return string_field(s, &ignored);
+    }
+    return s.skip();
+  });
+}
+
+// strings.TrimSpace: ASCII spaces and the Unicode White_Space code points.
+std::string trim_space(const std::string& v) {
+  auto space_at = [&](size_t i, bool back) -> size_t {  // byte length of a space at i, or 0
+    static const char* const kSpaces[] = {" ", "\t", "\n", "\v", "\f", "\r",
+                                          "\xc2\x85", "\xc2\xa0", "\xe1\x9a\x80",
+                                          "\xe2\x80\x80", "\xe2\x80\x81", "\xe2\x80\x82",
+                                          "\xe2\x80\x83", "\xe2\x80\x84", "\xe2\x80\x85",
+                                          "\xe2\x80\x86", "\xe2\x80\x87", "\xe2\x80\x88",
+                                          "\xe2\x80\x89", "\xe2\x80\x8a", "\xe2\x80\xa8",
+                                          "\xe2\x80\xa9", "\xe2\x80\xaf", "\xe2\x81\x9f",
+                                          "\xe3\x80\x80"};
+    for (const char* sp : kSpaces) {
+      const size_t n = std::strlen(sp);
+      if (back) {
+        if (i >= n && v.compare(i - n, n, sp) == 0) return n;
+      } else if (v.compare(i, n, sp) == 0) {
+        return n;
+      }
+    }
+    return 0;
+  };
+  size_t b = 0, e = v.size();
+  for (size_t n; b < e && (n = space_at(b, false));) b += n;
+  for (size_t n; e > b && (n = space_at(e, true));) e -= n;
+  return v.substr(b, e - b);
+}
+
+}  // namespace
+
+extern "C" {
+
+int pas_name_table_create(int32_t n_names, const char* const* names, pas_name_table** out) {
+  if (!out || n_names < 0 || (n_names > 0 && !names)) return PAS_EINVAL;
+  *out = nullptr;
+  for (int32_t i = 0; i < n_names; ++i)
+    if (!names[i]) return PAS_EINVAL;
+  pas_name_table* t = new (std::nothrow) pas_name_table;
+  if (!t) return PAS_ENOMEM;
+  try {
+    t->names.reserve((size_t)n_names);
+    for (int32_t i = 0; i < n_names; ++i) t->names.emplace_back(names[i]);
+    uint64_t cap = 16;
+    while (cap < (uint64_t)n_names * 2) cap <<= 1;
+    t->slots.assign(cap, -1);
+    t->mask = cap - 1;
+    for (int32_t i = 0; i < n_names; ++i) {
+      const std::string& s = t->names[(size_t)i];
+      for (uint64_t h = pas_name_table::hash(s) & t->mask;; h = (h + 1) & t->mask) {
+        const int32_t id = t->slots[h];
+        if (id < 0) {
+          t->slots[h] = i;
+          break;
+        }
+        if (t->names[(size_t)id] == s) break;  // a repeated name keeps its first id
+      }
+    }
+  } catch (...) {
+    delete t;
+    return PAS_ENOMEM;
+  }
+  *out = t;
+  return PAS_OK;
+}
+
+void pas_name_table_destroy(pas_name_table* t) { delete t; }
+
+int32_t pas_name_table_lookup(const pas_name_table* t, const char* name, int64_t len) {
+  if (!t || !name || len < 0) return -1;
+  return t->find(std::string_view(name, (size_t)len));
+}
+
+}  // extern "C"
+
+namespace {
+
+// Decode of extender.Args shared by pas_decode_args / pas_decode_request_names: the chosen
+// list's names (unescaped, request order), the item spans and the Pod span.
+int decode_args_core(const char* body, int64_t len, int32_t which,
+                     std::vector<std::string>* names, std::vector<int64_t>* spans,
+                     pas_args_info* info) {
+  std::memset(info, 0, sizeof *info);
+  Scanner s{body, body + len};
+  NodeList nodes;
+  std::vector<std::string> node_names;
+  bool has_nodes = false, has_names = false;
+  const char* pod_b = nullptr;
+  const char* pod_e = nullptr;
+  s.ws();
+  if (s.p >= s.end) return PAS_EDECODE;  // io.EOF: "request body empty" / errDecode
+  const char c0 = *s.p;
+  bool ok;
+  if (c0 == 'n') {
+    ok = s.literal("null");  // decodes to the zero Args
+  } else if (c0 != '{') {
+    ok = s.skip();
+    s.type_err = true;
+  } else {
+    ok = s.object([&](std::string_view k) {
+      if (fold_match("Pod", k)) {
+        const char c = s.peek();
+        if (c == 'n') return s.literal("null");  // a struct keeps its value
+        if (c != '{') return s.mismatch();
+        pod_b = s.p;
+        if (!s.skip()) return false;
+        pod_e = s.p;
+        return true;
+      }
+      if (fold_match("Nodes", k)) {
+        const char c = s.peek();
+        if (c == 'n') {
+          has_nodes = false;
+          nodes.names.clear();
+          nodes.spans.clear();
+          return s.literal("null");
+        }
+        if (c != '{') return s.mismatch();
+        if (!has_nodes) {  // a new NodeList; a repeated key decodes into the same one
+          nodes.names.clear();
+          nodes.spans.clear();
+        }
+        has_nodes = true;
+        return decode_node_list(s, &nodes, body);
+      }
+      if (fold_match("NodeNames", k)) {
+        const char c = s.peek();
+        if (c == 'n') {
+          has_names = false;
+          node_names.clear();
+          return s.literal("null");
+        }
+        if (c != '[') return s.mismatch();
+        if (!has_names) node_names.clear();
+        has_names = true;
+        size_t n = 0;
+        const bool r = s.array([&](int64_t i) {
+          if ((size_t)i >= node_names.size()) node_names.emplace_back();
+          n = (size_t)i + 1;
+          return string_field(s, &node_names[(size_t)i]);
+        });
+        node_names.resize(n);
+        return r;
+      }
+      return s.skip();
+    });
+  }
+  if (!ok || s.syntax_err || s.type_err) return PAS_EDECODE;
+  info->has_nodes = has_nodes ? 1 : 0;
+  info->has_node_names = has_names ? 1 : 0;
+  if (pod_b) {
+    info->pod_off = (int64_t)(pod_b - body);
+    info->pod_len = (int64_t)(pod_e - pod_b);
+  }
+  if (which == PAS_ARGS_NODES) {
+    *names = std::move(nodes.names);
+    if (spans) *spans = std::move(nodes.spans);
+  } else {
+    *names = std::move(node_names);
+  }
+  info->n_req = (int32_t)names->size();
+  return PAS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int pas_decode_args(const pas_name_table* t, const char* body, int64_t len, int32_t which,
+                    int32_t* req_node, int64_t node_cap, int64_t* item_span, uint64_t* cand,
+                    pas_args_info* info) {
+  if (!t || !info || len < 0 || (len > 0 && !body) || node_cap < 0 ||
+      (node_cap > 0 && !req_node) || (which != PAS_ARGS_NODES && which != PAS_ARGS_NODE_NAMES) ||
+      (item_span && which != PAS_ARGS_NODES))
+    return PAS_EINVAL;
+  std::vector<std::string> names;
+  std::vector<int64_t> spans;
+  const int rc = decode_args_core(body, len, which, &names, item_span ? &spans : nullptr, info);
+  if (rc != PAS_OK) return rc;
+  if (cand) std::memset(cand, 0, sizeof(uint64_t) * ((t->names.size() + 63) / 64));
+  const bool fits = (int64_t)names.size() <= node_cap;
+  for (size_t i = 0; i < names.size(); ++i) {
+    const int32_t id = t->find(names[i]);
+    if (id < 0)
+      ++info->n_unknown;
+    else
+      set_bit(cand, id);
+    if (fits) req_node[i] = id;
+  }
+  if (!fits) return PAS_ECAPACITY;
+  if (item_span && !spans.empty())
+    std::memcpy(item_span, spans.data(), sizeof(int64_t) * spans.size());
+  return PAS_OK;
+}
+
+int pas_decode_request_names(const char* body, int64_t len, int32_t which, char* buf,
+                             int64_t cap, int64_t* offsets, int64_t offsets_cap,
+                             int64_t* total_len, int32_t* n_req) {
+  if (len < 0 || (len > 0 && !body) || cap < 0 || (cap > 0 && !buf) || offsets_cap < 0 ||
+      (offsets_cap > 0 && !offsets) || !total_len || !n_req ||
+      (which != PAS_ARGS_NODES && which != PAS_ARGS_NODE_NAMES))
+    return PAS_EINVAL;
+  std::vector<std::string> names;
+  pas_args_info info;
+  const int rc = decode_args_core(body, len, which, &names, nullptr, &info);
+  if (rc != PAS_OK) return rc;
+  int64_t total = 0;
+  for (const std::string& n : names) total += (int64_t)n.size();
+  *total_len = total;
+  *n_req = (int32_t)names.size();
+  if (total > cap || (int64_t)names.size() + 1 > offsets_cap) return PAS_ECAPACITY;
+  int64_t pos = 0;
+  for (size_t i = 0; i < names.size(); ++i) {
+    offsets[i] = pos;
+    if (!names[i].empty()) std::memcpy(buf + pos, names[i].data(), names[i].size());
+    pos += (int64_t)names[i].size();
+  }
+  offsets[names.size()] = pos;
+  return PAS_OK;
+}
+
+int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char* ns_buf,
+                          int64_t ns_cap, int64_t* ns_len, char* label_buf, int64_t label_cap,
+                          int64_t* label_len) {
+  if (len < 0 || (len > 0 && !pod) || !label || !ns_len || !label_len || ns_cap < 0 ||
+      label_cap < 0 || (ns_cap > 0 && !ns_buf) || (label_cap > 0 && !label_buf))
+    return PAS_EINVAL;
+  std::string ns, value;
+  bool has_label = false;
+  const std::string_view want(label);
+  if (len > 0) {
+    Scanner s{pod, pod + len};
+    const char c = s.peek();
+    bool ok;
+    if (c == 'n') {
+      ok = s.literal("null");
+    } else if (c != '{') {
+      ok = s.skip();
+      s.type_err = true;
+    } else {
+      ok = s.object([&](std::string_view k) {
+        if (!fold_match("metadata", k)) return s.skip();
+        const char m = s.peek();
+        if (m == 'n') return s.literal("null");
+        if (m != '{') return s.mismatch();
+        return s.object([&](std::string_view mk) {
+          if (fold_match("namespace", mk)) return string_field(s, &ns);
+          if (!fold_match("labels", mk)) return s.skip();
+          const char l = s.peek();
+          if (l == 'n') {  // a nil map
+            has_label = false;
+            return s.literal("null");
+          }
+          if (l != '{') return s.mismatch();
+          // a map decodes into the existing map (entries accumulate across repeated keys)
+          return s.object([&](std::string_view lk) {
+            if (lk != want) return s.skip();
+            std::string v;  // a fresh element: null stores ""
+            if (!string_field(s, &v)) return false;
+            has_label = true;
+            value = v;
+            return true;
+          });
+        });
+      });
+    }
+    if (!ok || s.syntax_err || s.type_err) return PAS_EDECODE;
+  }
+  *ns_len = (int64_t)ns.size();
+  *label_len = has_label ? (int64_t)value.size() : -1;
+  if ((int64_t)ns.size() > ns_cap || (has_label && (int64_t)value.size() > label_cap))
+    return PAS_ECAPACITY;
+  if (!ns.empty()) std::memcpy(ns_buf, ns.data(), ns.size());
+  if (has_label && !value.empty()) std::memcpy(label_buf, value.data(), value.size());
+  return PAS_OK;
+}
+
+int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
+                            const char* const* kinds, int32_t max_containers, int64_t* req,
+                            uint32_t* req_mask, int32_t* n_containers, int32_t* n_unknown) {
+  if (len < 0 || (len > 0 && !pod) || n_kinds < 0 || n_kinds > 32 || (n_kinds > 0 && !kinds) ||
+      max_containers < 0 || (max_containers > 0 && ((n_kinds > 0 && !req) || !req_mask)) ||
+      !n_containers ||
+      !n_unknown)
+    return PAS_EINVAL;
+  for (int32_t q = 0; q < n_kinds; ++q)
+    if (!kinds[q]) return PAS_EINVAL;
+  static const char kPrefix[] = "gpu.intel.com/";  // resourcePrefix (utils.go:9-12)
+  struct Container {
+    std::vector<std::string> names;  // requests keys in the map (unique, last value wins)
+    std::vector<int64_t> values;
+  };
+  std::vector<Container> cont;
+  if (len > 0) {
+    Scanner s{pod, pod + len};
+    bool ok;
+    // ResourceList values: Quantity.UnmarshalJSON on the literal bytes
+    auto quantity = [&](int64_t* v) {
+      s.ws();
+      const char* b = s.p;
+      if (!s.skip()) return false;
+      std::string lit(b, (size_t)(s.p - b));
+      if (lit == "null") {
+        *v = 0;
+        return true;
+      }
+      if (lit.size() >= 2 && lit.front() == '"' && lit.back() == '"')
+        lit = lit.substr(1, lit.size() - 2);
+      const std::string q = trim_space(lit);
+      if (q.find('\0') != std::string::npos || pas_quantity_as_int64(q.c_str(), v) != PAS_OK) {
+        s.type_err = true;  // ParseQuantity error -> the decode fails
+      }
+      return true;
+    };
+    auto container = [&](Container* ct) {
+      const char c = s.peek();
+      if (c == 'n') return s.literal("null");
+      if (c != '{') return s.mismatch();
+      return s.object([&](std::string_view k) {
+        if (!fold_match("resources", k)) return s.skip();
+        const char r = s.peek();
+        if (r == 'n') return s.literal("null");
+        if (r != '{') return s.mismatch();
+        return s.object([&](std::string_view rk) {
+          if (!fold_match("requests", rk)) return s.skip();
+          const char m = s.peek();
+          if (m == 'n') {
+            ct->names.clear();
+            ct->values.clear();
+            return s.literal("null");
+          }
+          if (m != '{') return s.mismatch();
+          return s.object([&](std::string_view name) {
+            int64_t v = 0;
+            if (!quantity(&v)) return false;
+            for (size_t i = 0; i < ct->names.size(); ++i)
+              if (ct->names[i] == name) {
+                ct->values[i] = v;
+                return true;
+              }
+            ct->names.emplace_back(name);
+            ct->values.push_back(v);
+            return true;
+          });
+        });
+      });
+    };
+    const char c = s.peek();
+    if (c == 'n') {
+      ok = s.literal("null");
+    } else if (c != '{') {
+      ok = s.skip();
+      s.type_err = true;
+    } else {
+      ok = s.object([&](std::string_view k) {
+        if (!fold_match("spec", k)) return s.skip();
+        const char sp = s.peek();
+        if (sp == 'n') return s.literal("null");
+        if (sp != '{') return s.mismatch();
+        return s.object([&](std::string_view sk) {
+          if (!fold_match("containers", sk)) return s.skip();
+          const char a = s.peek();
+          if (a == 'n') {
+            cont.clear();
+            return s.literal("null");
+          }
+          if (a != '[') return s.mismatch();
+          // the slice is reused: elements keep what an earlier "containers" decoded
+          size_t n = 0;
+          bool r = s.array([&](int64_t i) {
+            if ((size_t)i >= cont.size()) cont.emplace_back();
+            n = (size_t)i + 1;
+            return container(&cont[(size_t)i]);
+          });
+          cont.resize(n);
+          return r;
+        });
+      });
+    }
+    if (!ok || s.syntax_err || s.type_err) return PAS_EDECODE;
+  }
+  *n_containers = (int32_t)cont.size();
+  *n_unknown = 0;
+  if ((int64_t)cont.size() > max_containers) return PAS_ECAPACITY;
+  for (size_t c = 0; c < cont.size(); ++c) {
+    req_mask[c] = 0;
+    for (int32_t q = 0; q < n_kinds; ++q) req[(int64_t)c * n_kinds + q] = 0;
+    for (size_t i = 0; i < cont[c].names.size(); ++i) {
+      const std::string& name = cont[c].names[i];
+      if (name.compare(0, sizeof kPrefix - 1, kPrefix) != 0) continue;
+      int32_t q = 0;
+      while (q < n_kinds && name != kinds[q]) ++q;
+      if (q == n_kinds) {
+        ++*n_unknown;
+        continue;
+      }
+      req[(int64_t)c * n_kinds + q] = cont[c].values[i];
+      req_mask[c] |= 1u << q;
+    }
+  }
+  return PAS_OK;
+}
+
+}  // extern "C"

@@ -24,6 +24,7 @@ PAS_EDEVICE = -4
 PAS_ENOMEM = -5
 PAS_ENOSNAP = -6
 PAS_ECAPACITY = -7
+PAS_EDECODE = -8
 
 STATUS_NAMES = {
     PAS_OK: "PAS_OK",
@@ -34,6 +35,7 @@ STATUS_NAMES = {
     PAS_ENOMEM: "PAS_ENOMEM",
     PAS_ENOSNAP: "PAS_ENOSNAP",
     PAS_ECAPACITY: "PAS_ECAPACITY",
+    PAS_EDECODE: "PAS_EDECODE",
 }
 
 PAS_OP_LESS_THAN = 0
@@ -77,6 +79,15 @@ class PasError(RuntimeError):
     def __init__(self, code: int, message: str):
         super().__init__(f"{STATUS_NAMES.get(code, code)}: {message}")
         self.code = code
+
+
+PAS_ARGS_NODES = 0
+PAS_ARGS_NODE_NAMES = 1
+
+
+class PasArgsInfo(ctypes.Structure):
+    _fields_ = [("has_nodes", c_int32), ("has_node_names", c_int32), ("n_req", c_int32),
+                ("n_unknown", c_int32), ("pod_off", c_int64), ("pod_len", c_int64)]
 
 
 class PasConfig(ctypes.Structure):
@@ -174,6 +185,20 @@ SIGNATURES = {
     "pas_encode_gas_filter_result": (
         c_int, [c_int32, _P, _P, POINTER(c_char_p), c_char_p, c_int64, POINTER(c_int64)]),
     "pas_encode_binding_result": (c_int, [c_char_p, c_char_p, c_int64, POINTER(c_int64)]),
+    "pas_name_table_create": (c_int, [c_int32, POINTER(c_char_p), POINTER(c_void_p)]),
+    "pas_name_table_destroy": (None, [_P]),
+    "pas_name_table_lookup": (c_int32, [_P, c_char_p, c_int64]),
+    "pas_decode_args": (
+        c_int, [_P, c_char_p, c_int64, c_int32, _P, c_int64, _P, _P, POINTER(PasArgsInfo)]),
+    "pas_decode_request_names": (
+        c_int, [c_char_p, c_int64, c_int32, _P, c_int64, _P, c_int64, POINTER(c_int64),
+                POINTER(c_int32)]),
+    "pas_decode_pod_policy": (
+        c_int, [c_char_p, c_int64, c_char_p, _P, c_int64, POINTER(c_int64), _P, c_int64,
+                POINTER(c_int64)]),
+    "pas_decode_pod_requests": (
+        c_int, [c_char_p, c_int64, c_int32, POINTER(c_char_p), c_int32, _P, _P,
+                POINTER(c_int32), POINTER(c_int32)]),
     "pas_set_timing": (c_int, [_P, c_int]),
     "pas_kernel_time": (c_int, [_P, c_int32, POINTER(c_double), POINTER(c_int64)]),
     "pas_reset_timing": (c_int, [_P]),

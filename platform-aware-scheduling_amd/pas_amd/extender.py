@@ -26,8 +26,8 @@ I915 = "gpu.intel.com/i915"
 
 
 def _field(obj, name):
-    """encoding/json field lookup: exact key first, then case-insensitive (Args has no json
-    tags; the kube-scheduler sends "pod", "nodes", "nodenames")."""
+    """encoding/json field lookup for BindingArgs (extender.Args goes through
+    pas_decode_args): exact key first, then case-insensitive."""
     if not isinstance(obj, dict):
         return None
     if name in obj:
@@ -45,10 +45,6 @@ def _decode(body: bytes):
     return json.loads(body)
 
 
-def _node_name(item) -> str:
-    return ((item or {}).get("metadata") or {}).get("name", "")
-
-
 class MetricsExtender:
     """TAS extender: Filter / Prioritize / Bind (telemetryscheduler.go:36-244).
 
@@ -60,19 +56,46 @@ class MetricsExtender:
     def __init__(self, ctx: Context, gen: int, node_names: Sequence[str],
                  metric_names: Sequence[str], policies: Mapping[Tuple[str, str], dict]):
         self.ctx, self.gen = ctx, gen
+        self.node_names = list(node_names)
         self.node_index = {n: i for i, n in enumerate(node_names)}
         self.metric_index = {m: i for i, m in enumerate(metric_names)}
         self.policies = policies
         self.table = wire.NodeTable(node_names)
+        self.name_table = wire.NameTable(node_names)
 
     # -- helpers ------------------------------------------------------------------
-    def _policy(self, pod) -> Optional[dict]:
-        """getPolicyFromPod (:103-112)."""
-        meta = (pod or {}).get("metadata") or {}
-        name = (meta.get("labels") or {}).get(TAS_POLICY_LABEL)
+    def _decode(self, body: bytes):
+        """DecodeExtenderRequest (:63-78) through pas_decode_args: (info, request node ids,
+        candidate bitmap, item spans, (namespace, policy label)).  The pod's quantities are
+        part of the reference's decode, so they are validated too.  Raises ValueError on a
+        decode error or "no nodes in list"."""
+        try:
+            info, idx, cand, spans = wire.decode_args(self.name_table, body, _lib.PAS_ARGS_NODES,
+                                                      spans=True)
+            pod = body[info.pod_off: info.pod_off + info.pod_len]
+            policy_ref = wire.decode_pod_policy(pod, TAS_POLICY_LABEL)
+            wire.decode_pod_requests(pod, [])
+        except _lib.PasError as e:
+            if e.code != _lib.PAS_EDECODE:
+                raise
+            raise ValueError("error decoding request") from e
+        if not info.has_nodes:
+            raise ValueError("no nodes in list")
+        return info, idx, cand, spans, policy_ref
+
+    def _policy(self, policy_ref) -> Optional[dict]:
+        """getPolicyFromPod (:103-112) on the decoded (namespace, label value)."""
+        ns, name = policy_ref
         if name is None:
             return None
-        return self.policies.get((meta.get("namespace", ""), name))
+        return self.policies.get((ns, name))
+
+    def _names(self, body, info, idx):
+        """Request node names in order: snapshot names, or the decoded ones when the request
+        names nodes the snapshot does not hold."""
+        if info.n_unknown:
+            return wire.decode_request_names(body, _lib.PAS_ARGS_NODES)
+        return [self.node_names[i] for i in idx]
 
     def _rules(self, triples):
         metric, op, target = [], [], []
@@ -85,46 +108,30 @@ class MetricsExtender:
             target.append(int(t))
         return make_rules(metric, op, target)
 
-    def _request_nodes(self, nodes):
-        items = nodes.get("items") if isinstance(nodes, dict) else None
-        items = items or []
-        return items, np.array([self.node_index.get(_node_name(it), -1) for it in items],
-                               np.int32)
-
-    def _cand(self, idx):
-        cand = np.zeros((1, w64(len(self.node_index))), np.uint64)
-        for i in idx:
-            if i >= 0:
-                cand[0, i >> 6] |= np.uint64(1 << (int(i) & 63))
-        return cand
-
     # -- verbs --------------------------------------------------------------------
     def filter(self, body: bytes) -> Tuple[int, bytes]:
         """Filter + filterNodes + WriteFilterResponse (:162-244)."""
         try:
-            args = _decode(body)
-            nodes = _field(args, "Nodes")
-            if nodes is None:
-                raise ValueError("no nodes in list")
+            info, idx, cand, spans, policy_ref = self._decode(body)
         except ValueError:
             return 200, b""  # decode error: nothing written (:164-168)
-        pod = _field(args, "Pod")
-        policy = self._policy(pod)
+        policy = self._policy(policy_ref)
         rules = (policy or {}).get("dontschedule") or []
-        items, idx = self._request_nodes(nodes)
-        if policy is None or not rules or len(items) == 0:
+        if policy is None or not rules or info.n_req == 0:
             return 404, b"null\n"  # nil FilterResult (:189-203)
         r = self._rules(rules)
         pass_out, _, _ = self.ctx.tas_eval(self.gen, r, np.array([0, len(r)], np.int32),
-                                           make_rules([-1], [0], [0]), self._cand(idx),
+                                           make_rules([-1], [0], [0]), cand[None, :],
                                            _lib.PAS_TAS_FILTER)
-        blobs = [json.dumps(it, separators=(",", ":")).encode() for it in items]
-        table = wire.NodeTable([_node_name(it) for it in items], blobs)
-        order = np.arange(len(items), dtype=np.int32)
+        # the shim's json.Marshal of each v1.Node (here: the compact re-encoding of the item)
+        blobs = [json.dumps(json.loads(body[o:o + n]), separators=(",", ":")).encode()
+                 for o, n in spans]
+        table = wire.NodeTable(self._names(body, info, idx), blobs)
+        order = np.arange(info.n_req, dtype=np.int32)
         # the pass row re-indexed to the request's own order (duplicates keep their verdict);
         # a node without metrics in the snapshot is in no violating set, so it passes
         # (dontschedule/strategy.go:25-44 only ranges over the metric cache's nodes)
-        row = np.zeros(w64(len(items)), np.uint64)
+        row = np.zeros(w64(info.n_req), np.uint64)
         for j, i in enumerate(idx):
             if i < 0 or (int(pass_out[0, i >> 6]) >> (int(i) & 63)) & 1:
                 row[j >> 6] |= np.uint64(1 << (j & 63))
@@ -133,21 +140,15 @@ class MetricsExtender:
     def prioritize(self, body: bytes) -> Tuple[int, bytes]:
         """Prioritize + prioritizeNodes + WritePrioritizeResponse (:36-158)."""
         try:
-            args = _decode(body)
-            nodes = _field(args, "Nodes")
-            if nodes is None:
-                raise ValueError("no nodes in list")
+            info, idx, cand, _, policy_ref = self._decode(body)
         except ValueError:
             return 200, b""
-        items, idx = self._request_nodes(nodes)
-        if len(items) == 0:
+        if info.n_req == 0:
             return 200, b""  # no nodes: nothing written (:46-49)
-        pod = _field(args, "Pod")
         status = 200
-        labels = (((pod or {}).get("metadata") or {}).get("labels") or {})
-        if TAS_POLICY_LABEL not in labels:
+        if policy_ref[1] is None:
             status = 400  # (:50-53), then the (empty) list is still written
-        policy = self._policy(pod)
+        policy = self._policy(policy_ref)
         prio = (policy or {}).get("scheduleonmetric") or []
         # getSchedulingRule (:115-124): first rule with a metric name; errors -> []
         if policy is None or not prio or not prio[0][0]:
@@ -155,12 +156,13 @@ class MetricsExtender:
         if prio[0][0] not in self.metric_index:  # ReadMetric error -> [] (:130-133)
             return status, b"[]\n"
         # nodes without metrics in the snapshot are left out, as filteredNodeData keeps only
-        # nodes with a metric (telemetryscheduler.go:128-149): _cand skips them
+        # nodes with a metric (telemetryscheduler.go:128-149): the candidate bitmap has no
+        # bit for them
         code = parse_operator(prio[0][1])
         p = make_rules([self.metric_index[prio[0][0]]], [code if code >= 0 else 3],
                        [int(prio[0][2])])
         _, order, lens = self.ctx.tas_eval(self.gen, make_rules([], [], []),
-                                           np.zeros(2, np.int32), p, self._cand(idx),
+                                           np.zeros(2, np.int32), p, cand[None, :],
                                            _lib.PAS_TAS_PRIORITIZE)
         return status, wire.host_priority_list(order[0, : lens[0]], self.table)
 
@@ -179,53 +181,48 @@ class GASExtender:
                  card_names: Sequence[Sequence[str]], kinds: Sequence[str],
                  pods: Optional[Dict[Tuple[str, str], dict]] = None):
         self.ctx, self.gen = ctx, gen
+        self.node_names = list(node_names)
         self.node_index = {n: i for i, n in enumerate(node_names)}
+        self.name_table = wire.NameTable(node_names)
         self.card_names = card_names
         self.kinds = list(kinds)
         self.pods = pods if pods is not None else {}
         self.i915 = self.kinds.index(I915) if I915 in self.kinds else -1
 
-    def _requests(self, pod):
-        """containerRequests (utils.go:14-32): gpu.intel.com/ requests, AsInt64 (ok ignored)."""
-        containers = (((pod or {}).get("spec") or {}).get("containers") or [])
-        c = max(1, len(containers))
-        req = np.zeros((1, c, len(self.kinds)), np.int64)
-        mask = np.zeros((1, c), np.uint32)
+    def _requests(self, pod_json: bytes):
+        """containerRequests (utils.go:14-32) through pas_decode_pod_requests: gpu.intel.com/
+        requests as AsInt64 (ok ignored) in the pas_gas_fit layout, plus each container's
+        numI915 (its annotation segment length)."""
+        req, mask, ncont, unknown = wire.decode_pod_requests(pod_json, self.kinds)
+        if unknown:
+            raise KeyError("a gpu.intel.com resource kind not in the snapshot")
         per_container = []
-        for ci, cont in enumerate(containers):
-            reqs = (((cont or {}).get("resources") or {}).get("requests") or {})
-            i915 = 0
-            for name, q in reqs.items():
-                if not name.startswith("gpu.intel.com/"):
-                    continue
-                if name not in self.kinds:
-                    raise KeyError(f"resource kind {name} not in the snapshot")
-                j = self.kinds.index(name)
-                req[0, ci, j] = quantity_as_int64(q)
-                mask[0, ci] |= 1 << j
-                if name == I915:
-                    i915 = max(int(req[0, ci, j]), 0)
-            per_container.append(i915 if mask[0, ci] else 0)
-        return req, mask, np.array([len(containers)], np.int32), per_container
+        for ci in range(int(ncont[0])):
+            on = self.i915 >= 0 and (int(mask[0, ci]) >> self.i915) & 1
+            per_container.append(max(int(req[0, ci, self.i915]), 0) if on else 0)
+        return req, mask, ncont, per_container
 
     def filter(self, body: bytes) -> Tuple[int, bytes]:
-        """Filter + filterNodes (:449-482, 523-543)."""
+        """Filter + filterNodes (:449-482, 523-543), the body decoded by pas_decode_args."""
         try:
-            args = _decode(body)
-        except ValueError:
-            return 404, b""
-        names = _field(args, "NodeNames") or []
-        table = wire.NodeTable(names)
-        if not names:
-            return 404, wire.gas_filter_result([], np.zeros(1, np.uint64), table)
-        req, mask, ncont, _ = self._requests(_field(args, "Pod"))
+            info, idx, cand, _ = wire.decode_args(self.name_table, body,
+                                                  _lib.PAS_ARGS_NODE_NAMES)
+            req, mask, ncont, _ = self._requests(body[info.pod_off: info.pod_off + info.pod_len])
+        except _lib.PasError as e:
+            if e.code != _lib.PAS_EDECODE:
+                raise
+            return 404, b""  # errDecode (:499-501, 528-533)
+        if info.n_req == 0:
+            return 404, wire.gas_filter_result([], np.zeros(1, np.uint64), wire.NodeTable([]))
+        names = (wire.decode_request_names(body, _lib.PAS_ARGS_NODE_NAMES) if info.n_unknown
+                 else [self.node_names[i] for i in idx])
         res = self.ctx.gas_fit(self.gen, req, mask, ncont, self.i915)
-        fit = np.zeros(w64(len(names)), np.uint64)
-        for j, name in enumerate(names):
-            i = self.node_index.get(name)
-            if i is not None and int(res[0, i]) >> 31:  # unknown node: FetchNode error
+        fit = np.zeros(w64(info.n_req), np.uint64)
+        for j, i in enumerate(idx):
+            if i >= 0 and int(res[0, i]) >> 31:  # unknown node: FetchNode error
                 fit[j >> 6] |= np.uint64(1 << (j & 63))
-        return 200, wire.gas_filter_result(np.arange(len(names), dtype=np.int32), fit, table)
+        return 200, wire.gas_filter_result(np.arange(info.n_req, dtype=np.int32), fit,
+                                           wire.NodeTable(names))
 
     def bind(self, body: bytes) -> Tuple[int, bytes]:
         """Bind + bindNode (:385-445, 546-566): fit on the current usage, commit, annotate."""
@@ -239,7 +236,7 @@ class GASExtender:
             return 404, self._error(f'pod "{key[1]}" not found')
         node_name = _field(args, "Node") or ""
         node = self.node_index.get(node_name)
-        req, mask, ncont, per_container = self._requests(pod)
+        req, mask, ncont, per_container = self._requests(json.dumps(pod).encode())
         if node is None:  # runSchedulingLogic -> FetchNode error (:282-288)
             return 404, self._error(f'node "{node_name}" not found')
         res, st, cards, nsel = self.ctx.gas_bind(self.gen, self.gen + 1, [0], [node], req, mask,
