@@ -617,7 +617,7 @@ int env_int(const char* name, int dflt) {
 // sweeps (scripts/emit_sweep.sh); the ablations are diagnostic timing builds whose outputs
 // are wrong.
 struct TasTuning {
-  int32_t waves = 4;         // waves per eval workgroup (4 or 8)
+  int32_t waves = 4;         // waves per eval workgroup (2, 4 or 8)
   int32_t seg_per_wave = 1;  // adjacent order segments per wave per round (1 or 2)
   int32_t no_group = 0;      // diagnostic: pods in index order (no XCD locality)
   int32_t ablate = 0;
@@ -628,7 +628,8 @@ struct TasTuning {
 const TasTuning& tas_tuning() {
   static const TasTuning t = [] {
     TasTuning x;
-    x.waves = env_int("PAS_EVAL_WAVES", x.waves) == 8 ? 8 : 4;
+    const int w = env_int("PAS_EVAL_WAVES", x.waves);
+    x.waves = w == 8 ? 8 : w == 2 ? 2 : 4;
     x.seg_per_wave = env_int("PAS_EVAL_SEGS", x.seg_per_wave) == 2 ? 2 : 1;
     x.no_group = env_int("PAS_EVAL_NOGROUP", 0);
     x.ablate = env_int("PAS_EVAL_ABLATE", 0);
@@ -720,6 +721,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
 #define PAS_EVAL_CASE(W, S, A) \
   if (tune.waves == W && tune.seg_per_wave == S && tune.ablate == A) fn = &tas_eval_kernel<W, S, A>;
   PAS_EVAL_CASE(4, 2, 0) PAS_EVAL_CASE(8, 1, 0) PAS_EVAL_CASE(8, 2, 0)
+  PAS_EVAL_CASE(2, 1, 0) PAS_EVAL_CASE(2, 2, 0) PAS_EVAL_CASE(2, 1, 2)
   PAS_EVAL_CASE(4, 1, 1) PAS_EVAL_CASE(4, 1, 2) PAS_EVAL_CASE(4, 1, 4) PAS_EVAL_CASE(4, 1, 8)
   PAS_EVAL_CASE(4, 1, 7) PAS_EVAL_CASE(4, 2, 1) PAS_EVAL_CASE(4, 2, 2)
 #undef PAS_EVAL_CASE
