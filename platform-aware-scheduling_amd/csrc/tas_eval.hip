@@ -574,36 +574,325 @@ constexpr int kTpb = 256;
 constexpr int kWaves = kTpb / 64;
 
 
-// One wave per 64-node word, strategies x rules in the wave loop: deschedule.Strategy.
-// Violated (deschedule/strategy.go:31-50) per registered strategy, as
-// nodeStatusForStrategy does (deschedule/enforce.go:154-164).
+// 32 bits of x spread to the even bits of a 64-bit word (Morton order).
+__device__ __forceinline__ uint64_t spread_even(uint32_t x) {
+  uint64_t v = x;
+  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+  v = (v | (v << 2)) & 0x3333333333333333ull;
+  v = (v | (v << 1)) & 0x5555555555555555ull;
+  return v;
+}
+
+// deschedule.Strategy.Violated (deschedule/strategy.go:31-50) per registered strategy, as
+// nodeStatusForStrategy does (deschedule/enforce.go:154-164).  A wave owns 2 * kPair
+// consecutive 64-node words; each lane reads two adjacent nodes with one 16-byte load per
+// word pair, so a rule's column is read as contiguous 1-KB runs.  The lane's presence bits
+// are folded into its compares, the even / odd nodes' hits are ballotted separately and
+// accumulated per strategy, and only the finished words are interleaved back into node
+// order.  The strategies' rules are walked as one flat list, kU at a time, every value load
+// of the batch issued before the first compare; a strategy's words are written when the list
+// passes its end (strategies without rules write 0).
+template <int kPair, int kU, bool kVec>
 __global__ __launch_bounds__(kTpb) void tas_violations_kernel(
     int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
     const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
     const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out) {
-  const int32_t gw = blockIdx.x * kWaves + (threadIdx.x >> 6);
-  if (gw >= W64) return;
+  constexpr int kWd = 2 * kPair;
+  const int32_t gw0 = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * kWd;
+  if (gw0 >= W64) return;
   const int lane = threadIdx.x & 63;
-  const int32_t n = gw * 64 + lane;
-  const bool valid = n < N;
-  for (int32_t s = 0; s < n_strat; ++s) {
-    uint64_t acc = 0;
-    const int32_t r1 = rule_off[s + 1];
-    for (int32_t r = rule_off[s]; r < r1; ++r) {
-      const pas_rule rule = rules[r];
+  const int32_t half = lane >> 5;          // word of its pair the lane's nodes fall in
+  const uint32_t sh = (uint32_t)(lane & 31) * 2;  // bit of its even node in that word
+  int32_t pos[kPair];   // the lane's even node
+  bool ok0[kPair], ok1[kPair];
+#pragma unroll
+  for (int k = 0; k < kPair; ++k) {
+    const int32_t n = (gw0 + 2 * k) * 64 + 2 * lane;
+    ok0[k] = n < N;
+    ok1[k] = n + 1 < N;
+    pos[k] = n;
+  }
+  const int32_t r_end = rule_off[n_strat];
+  int32_t s = 0;
+  int32_t s_end = n_strat > 0 ? rule_off[1] : 0;
+  uint64_t acc_e[kPair] = {}, acc_o[kPair] = {};
+  auto flush = [&]() {
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < kPair; ++k) {
+        const int32_t w = gw0 + 2 * k;
+        const uint64_t lo = spread_even((uint32_t)acc_e[k]) | (spread_even((uint32_t)acc_o[k]) << 1);
+        const uint64_t hi = spread_even((uint32_t)(acc_e[k] >> 32)) |
+                            (spread_even((uint32_t)(acc_o[k] >> 32)) << 1);
+        if (w < W64) viol_out[(int64_t)s * W64 + w] = lo;
+        if (w + 1 < W64) viol_out[(int64_t)s * W64 + w + 1] = hi;
+      }
+#pragma unroll
+    for (int k = 0; k < kPair; ++k) acc_e[k] = acc_o[k] = 0;
+  };
+  for (int32_t r0 = rule_off[0]; r0 < r_end; r0 += kU) {
+    pas_rule ru[kU];
+    int64_t v[kU][kPair][2];
+    uint64_t pr[kU][kPair][2];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) ru[u] = rules[min(r0 + u, r_end - 1)];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int32_t m = (ru[u].metric >= 0 && ru[u].metric < M) ? ru[u].metric : 0;
+      const int64_t* col = vals + (int64_t)m * N;
+      const uint64_t* pw = present + (int64_t)m * W64 + gw0;  // with the values, not after
+#pragma unroll
+      for (int k = 0; k < kPair; ++k) {
+        pr[u][k][0] = pw[2 * k];
+        pr[u][k][1] = gw0 + 2 * k + 1 < W64 ? pw[2 * k + 1] : 0ull;
+      }
+#pragma unroll
+      for (int k = 0; k < kPair; ++k) {
+        if (kVec) {  // N even: rows 16-byte aligned, a pair in bounds or wholly past N
+          const longlong2 x =
+              *reinterpret_cast<const longlong2*>(col + (ok0[k] ? pos[k] : N - 2));
+          v[u][k][0] = x.x;
+          v[u][k][1] = x.y;
+        } else {
+          v[u][k][0] = col[min(pos[k], N - 1)];
+          v[u][k][1] = col[min(pos[k] + 1, N - 1)];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int32_t r = r0 + u;
+      if (r >= r_end) break;
+      while (r >= s_end) {  // the list has passed strategy s: its words are complete
+        flush();
+        ++s;
+        s_end = rule_off[s + 1];
+      }
+      const pas_rule rule = ru[u];
       if (rule.metric < 0 || rule.metric >= M || rule.op < 0 || rule.op > 2) continue;
-      const uint64_t pres = present[(int64_t)rule.metric * W64 + gw];
-      const int64_t v = valid ? vals[(int64_t)rule.metric * N + n] : 0;
       int64_t tm = 0;
       const int sat = target_milli(rule.target, &tm);
-      bool hit;
-      if (rule.op == PAS_OP_LESS_THAN) hit = sat > 0 || (sat == 0 && v < tm);
-      else if (rule.op == PAS_OP_GREATER_THAN) hit = sat < 0 || (sat == 0 && v > tm);
-      else hit = sat == 0 && v == tm;
-      acc |= __ballot(hit && valid) & pres;
+#pragma unroll
+      for (int k = 0; k < kPair; ++k) {
+        const uint64_t pl = (half ? pr[u][k][1] : pr[u][k][0]) >> sh;  // the lane's two bits
+        bool hit[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int64_t x = v[u][k][e];
+          bool h;
+          if (rule.op == PAS_OP_LESS_THAN) h = sat > 0 || (sat == 0 && x < tm);
+          else if (rule.op == PAS_OP_GREATER_THAN) h = sat < 0 || (sat == 0 && x > tm);
+          else h = sat == 0 && x == tm;
+          hit[e] = h && ((pl >> e) & 1);
+        }
+        acc_e[k] |= __ballot(hit[0] && ok0[k]);
+        acc_o[k] |= __ballot(hit[1] && ok1[k]);
+      }
     }
-    if (lane == 0) viol_out[(int64_t)s * W64 + gw] = acc;
   }
+  for (; s < n_strat; ++s) flush();  // the last strategy with rules, then those without
+}
+
+// The sweep with column reuse (n_strat <= 64): the workgroup sorts the flat rule list by
+// metric in LDS (chunks of kDedupRules), so each wave reads every referenced column of its
+// two words once and evaluates all rules on it (C4's 64 rules reference ~41 of the 64
+// columns).  Accumulators are lane-packed: lane s holds strategy s's even / odd hit masks;
+// at the end each lane interleaves its own masks and stores its strategy's two words.
+constexpr int kDedupRules = 256;
+
+struct DedupRule {
+  int64_t tm;      // target * 1000 (when sat == 0)
+  int32_t metric;  // M: skipped (not in the cache / invalid operator)
+  int32_t op;
+  int32_t sat;
+  int32_t strat;
+};
+
+template <bool kVec>
+__global__ __launch_bounds__(kTpb) void tas_violations_dedup_kernel(
+    int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
+    const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
+    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out) {
+  __shared__ DedupRule srt[kDedupRules];
+  __shared__ int32_t key[kDedupRules];
+  __shared__ int32_t off[65];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int32_t gw0 = (blockIdx.x * kWaves + (tid >> 6)) * 2;  // the wave's word pair
+  const bool active = gw0 < W64;  // (no early exit: the workgroup sorts together)
+  const int32_t n = gw0 * 64 + 2 * lane;
+  const bool ok0 = n < N, ok1 = n + 1 < N;
+  const int32_t half = lane >> 5;
+  const uint32_t sh = (uint32_t)(lane & 31) * 2;
+  if (tid <= n_strat) off[tid] = rule_off[tid];
+  __syncthreads();
+  const int32_t r_begin = off[0], r_end = off[n_strat];
+  uint32_t ae_lo = 0, ae_hi = 0, ao_lo = 0, ao_hi = 0;  // lane s: strategy s
+  for (int32_t c0 = r_begin; c0 < r_end; c0 += kDedupRules) {
+    const int32_t nr = min(kDedupRules, r_end - c0);
+    // sort the chunk by metric (stable): rank = rules with a smaller key, or an equal key
+    // and a smaller index
+    __syncthreads();  // the previous chunk's table is no longer read
+    int32_t my_key = 0;
+    DedupRule d{};
+    if (tid < nr) {
+      const int32_t r = c0 + tid;
+      const pas_rule ru = rules[r];
+      int32_t st = 0;  // the strategy: largest s with off[s] <= r
+      for (int32_t b = 64; b > 0; b >>= 1)
+        if (st + b <= n_strat && off[st + b] <= r) st += b;
+      while (st < n_strat - 1 && off[st + 1] <= r) ++st;  // empty strategies at r
+      const bool valid = ru.metric >= 0 && ru.metric < M && ru.op >= 0 && ru.op <= 2;
+      d.metric = valid ? ru.metric : M;
+      d.op = ru.op;
+      d.sat = target_milli(ru.target, &d.tm);
+      d.strat = st;
+      my_key = d.metric;
+      key[tid] = my_key;
+    }
+    __syncthreads();
+    if (tid < nr) {
+      int32_t rank = 0;
+      for (int32_t q = 0; q < nr; ++q) {
+        const int32_t kq = key[q];
+        rank += (kq < my_key || (kq == my_key && q < tid)) ? 1 : 0;
+      }
+      srt[rank] = d;
+    }
+    __syncthreads();
+    if (!active) continue;
+    // walk the sorted rules metric by metric, the next column's loads in flight
+    auto load = [&](int32_t m, int64_t* v, uint64_t* p) {
+      const int64_t* col = vals + (int64_t)min(m, M - 1) * N;
+      if (kVec) {
+        const longlong2 x = *reinterpret_cast<const longlong2*>(col + (ok0 ? n : N - 2));
+        v[0] = x.x;
+        v[1] = x.y;
+      } else {
+        v[0] = col[min(n, N - 1)];
+        v[1] = col[min(n + 1, N - 1)];
+      }
+      const uint64_t* pw = present + (int64_t)min(m, M - 1) * W64 + gw0;
+      p[0] = pw[0];
+      p[1] = gw0 + 1 < W64 ? pw[1] : 0ull;
+    };
+    int32_t i = 0;
+    int32_t m_cur = __builtin_amdgcn_readfirstlane(srt[0].metric);
+    int64_t v[2];
+    uint64_t p[2];
+    load(m_cur, v, p);
+    while (i < nr && m_cur < M) {
+      int32_t j = i + 1;
+      while (j < nr && srt[j].metric == m_cur) ++j;
+      const int32_t m_next = j < nr ? __builtin_amdgcn_readfirstlane(srt[j].metric) : M;
+      int64_t nv[2];
+      uint64_t np[2];
+      load(m_next < M ? m_next : m_cur, nv, np);
+      const uint64_t pl = (half ? p[1] : p[0]) >> sh;  // the lane's two presence bits
+      for (int32_t k = i; k < j; ++k) {
+        const int32_t op = __builtin_amdgcn_readfirstlane(srt[k].op);
+        const int32_t sat = __builtin_amdgcn_readfirstlane(srt[k].sat);
+        const int32_t st = __builtin_amdgcn_readfirstlane(srt[k].strat);
+        const int64_t tm = srt[k].tm;
+        bool hit[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          bool h;
+          if (op == PAS_OP_LESS_THAN) h = sat > 0 || (sat == 0 && v[e] < tm);
+          else if (op == PAS_OP_GREATER_THAN) h = sat < 0 || (sat == 0 && v[e] > tm);
+          else h = sat == 0 && v[e] == tm;
+          hit[e] = h && ((pl >> e) & 1);
+        }
+        const uint64_t be = __ballot(hit[0] && ok0), bo = __ballot(hit[1] && ok1);
+        const bool me = lane == st;
+        ae_lo |= me ? (uint32_t)be : 0u;
+        ae_hi |= me ? (uint32_t)(be >> 32) : 0u;
+        ao_lo |= me ? (uint32_t)bo : 0u;
+        ao_hi |= me ? (uint32_t)(bo >> 32) : 0u;
+      }
+      v[0] = nv[0];
+      v[1] = nv[1];
+      p[0] = np[0];
+      p[1] = np[1];
+      m_cur = m_next;
+      i = j;
+    }
+  }
+  if (active && lane < n_strat) {
+    const uint64_t lo = spread_even(ae_lo) | (spread_even(ao_lo) << 1);
+    const uint64_t hi = spread_even(ae_hi) | (spread_even(ao_hi) << 1);
+    viol_out[(int64_t)lane * W64 + gw0] = lo;
+    if (gw0 + 1 < W64) viol_out[(int64_t)lane * W64 + gw0 + 1] = hi;
+  }
+}
+
+// The sweep by column runs: a wave owns kRun consecutive 64-node words and walks the flat
+// rule list one rule at a time, reading that rule's column over its words as one
+// contiguous kRun * 512-byte run (every DRAM page it opens is read whole) while the next
+// rule's run is already in flight.  Lane k keeps word k's violation mask of the open
+// strategy (its presence word is lane k's own load); at a strategy's end lanes 0..kRun-1
+// store its words with one coalesced store.
+template <int kRun>
+__global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
+    int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
+    const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
+    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out) {
+  static_assert(kRun <= 64, "one word per lane");
+  const int32_t gw0 = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * kRun;
+  if (gw0 >= W64) return;
+  const int lane = threadIdx.x & 63;
+  const int32_t pw_lane = min(gw0 + lane, W64 - 1);
+  const int32_t r_begin = rule_off[0], r_end = rule_off[n_strat];
+  int32_t s = 0;
+  int32_t s_end = rule_off[1];
+  uint64_t acc = 0;  // lane k: word gw0 + k
+  auto flush = [&]() {
+    if (lane < kRun && gw0 + lane < W64) viol_out[(int64_t)s * W64 + gw0 + lane] = acc;
+    acc = 0;
+  };
+  auto load = [&](int32_t r, pas_rule* ru, int64_t (&v)[kRun], uint64_t* pr) {
+    *ru = rules[min(r, r_end - 1)];
+    const int32_t m = (ru->metric >= 0 && ru->metric < M) ? ru->metric : 0;
+    const int64_t* col = vals + (int64_t)m * N;
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) v[k] = col[min((gw0 + k) * 64 + lane, N - 1)];
+    *pr = present[(int64_t)m * W64 + pw_lane];
+  };
+  pas_rule ru;
+  int64_t v[kRun];
+  uint64_t pr = 0;
+  if (r_begin < r_end) load(r_begin, &ru, v, &pr);
+  for (int32_t r = r_begin; r < r_end; ++r) {
+    while (r >= s_end) {  // the list has passed strategy s: its words are complete
+      flush();
+      ++s;
+      s_end = rule_off[s + 1];
+    }
+    pas_rule nru;
+    int64_t nv[kRun];
+    uint64_t npr;
+    load(r + 1, &nru, nv, &npr);  // the next run in flight during this rule's compares
+    if (ru.metric >= 0 && ru.metric < M && ru.op >= 0 && ru.op <= 2) {
+      int64_t tm = 0;
+      const int sat = target_milli(ru.target, &tm);
+#pragma unroll
+      for (int k = 0; k < kRun; ++k) {
+        const bool valid = (gw0 + k) * 64 + lane < N;
+        bool hit;
+        if (ru.op == PAS_OP_LESS_THAN) hit = sat > 0 || (sat == 0 && v[k] < tm);
+        else if (ru.op == PAS_OP_GREATER_THAN) hit = sat < 0 || (sat == 0 && v[k] > tm);
+        else hit = sat == 0 && v[k] == tm;
+        const uint64_t mask = __ballot(hit && valid);
+        acc = lane == k ? (acc | (mask & pr)) : acc;
+      }
+    }
+    ru = nru;
+    pr = npr;
+#pragma unroll
+    for (int k = 0; k < kRun; ++k) v[k] = nv[k];
+  }
+  for (; s < n_strat; ++s) flush();  // the last strategy with rules, then those without
 }
 
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -748,8 +1037,47 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   if (W64 == 0) return PAS_OK;
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_VIOLATIONS, &tl);
-  tas_violations_kernel<<<(W64 + kWaves - 1) / kWaves, kTpb, 0, s>>>(
-      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
+  // word pairs per wave / rules per batch of loads (tuning: PAS_VIOL_PAIRS, PAS_VIOL_U)
+  static const int pairs = env_int("PAS_VIOL_PAIRS", 1), u = env_int("PAS_VIOL_U", 2);
+  using ViolFn = void (*)(int32_t, int32_t, int32_t, int32_t, const int32_t*, const pas_rule*,
+                          const int64_t*, const uint64_t*, uint64_t*);
+  const bool vec = t.n_nodes >= 2 && (t.n_nodes & 1) == 0;
+  ViolFn fn = vec ? &tas_violations_kernel<1, 2, true> : &tas_violations_kernel<1, 2, false>;
+  int per_wave = 2;
+#define PAS_VIOL_CASE(PR, U)                                                            \
+  if (pairs == PR && u == U) {                                                          \
+    fn = vec ? &tas_violations_kernel<PR, U, true> : &tas_violations_kernel<PR, U, false>; \
+    per_wave = 2 * PR;                                                                  \
+  }
+  PAS_VIOL_CASE(1, 1) PAS_VIOL_CASE(1, 4) PAS_VIOL_CASE(2, 1) PAS_VIOL_CASE(2, 2)
+#undef PAS_VIOL_CASE
+  static const int run = env_int("PAS_VIOL_RUN", 8);
+  if (run > 0 && !env_int("PAS_VIOL_FLAT", 0) && !env_int("PAS_VIOL_DEDUP", 0)) {
+    auto rfn = run == 2    ? &tas_violations_run_kernel<2>
+               : run == 4  ? &tas_violations_run_kernel<4>
+               : run == 16 ? &tas_violations_run_kernel<16>
+                           : &tas_violations_run_kernel<8>;
+    const int32_t per = (run == 2 || run == 4 || run == 16) ? run : 8;
+    const int32_t rwaves = (W64 + per - 1) / per;
+    rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
+        t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
+    timing_end(ctx, s, &tl);
+    PAS_HIP(ctx, hipGetLastError());
+    return PAS_OK;
+  }
+  if (n_strat <= 64 && env_int("PAS_VIOL_DEDUP", 0)) {
+    auto dfn = vec ? &tas_violations_dedup_kernel<true> : &tas_violations_dedup_kernel<false>;
+    const int32_t pairs_total = (W64 + 1) / 2;
+    dfn<<<(pairs_total + kWaves - 1) / kWaves, kTpb, 0, s>>>(
+        t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
+    timing_end(ctx, s, &tl);
+    PAS_HIP(ctx, hipGetLastError());
+    return PAS_OK;
+  }
+  const int32_t waves = (W64 + per_wave - 1) / per_wave;
+  fn<<<(waves + kWaves - 1) / kWaves, kTpb, 0, s>>>(t.n_nodes, t.n_metrics, W64, n_strat,
+                                                    d_rule_off, d_rules, t.vals, t.present,
+                                                    d_viol);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;

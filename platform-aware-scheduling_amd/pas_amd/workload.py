@@ -129,7 +129,12 @@ def make_deschedule_rules(snap: TasSnapshotData, n_strategies: int, rules_per_st
     rng = np.random.default_rng(seed)
     m_total = snap.v_milli.shape[0]
     nr = n_strategies * rules_per_strategy
-    metric = rng.integers(0, m_total, size=nr).astype(np.int32)
+    # every column referenced once while there are columns left (C4: 64 rules over the 64
+    # metrics, so a sweep reads 8 * M * N bytes of values)
+    if nr <= m_total:
+        metric = rng.permutation(m_total)[:nr].astype(np.int32)
+    else:
+        metric = rng.integers(0, m_total, size=nr).astype(np.int32)
     op = rng.integers(0, 3, size=nr).astype(np.int32)
     rules = np.zeros(nr, RULE_DTYPE)
     rules["metric"] = metric

@@ -321,6 +321,26 @@ def test_deschedule_parity(ctx, oracle):
                                       oracle.tas_violations(v, pres, rules, off))
 
 
+def test_deschedule_empty_strategies_and_skipped_rules(ctx, oracle):
+    # strategies without rules (first, middle, last), rules on metrics not in the cache
+    # (skipped, strategy.go:37-40), more rules than one batch of the sweep's loads
+    rng = np.random.default_rng(11)
+    n, m = 3000, 6
+    v, pres, _, _, _, _ = random_case(rng, n, m, 1, 1)
+    counts = [0, 3, 0, 0, 21, 1, 15, 0]
+    off = np.concatenate([[0], np.cumsum(counts)]).astype(np.int32)
+    rules = np.zeros(int(off[-1]), pas_amd.RULE_DTYPE)
+    rules["metric"] = rng.integers(0, m, size=len(rules))
+    rules["op"] = rng.integers(0, 3, size=len(rules))
+    rules["target"] = rng.integers(-5_000, 5_000, size=len(rules))
+    rules["metric"][::5] = -1
+    rules["metric"][2::7] = m + 3
+    gen = upload(ctx, v, pres)
+    got = ctx.tas_violations(gen, rules, off)
+    np.testing.assert_array_equal(got, oracle.tas_violations(v, pres, rules, off))
+    assert not got[[0, 2, 3, 7]].any()
+
+
 @pytest.mark.slow
 def test_c4_deschedule_sweep_1m(ctx, oracle):
     # configs[3] per-GPU work at full node count: 1M nodes x 64 metrics, 16 strategies x 4 rules
