@@ -845,34 +845,39 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
   const int32_t pw_lane = min(gw0 + lane, W64 - 1);
   const int32_t r_begin = rule_off[0], r_end = rule_off[n_strat];
   int32_t s = 0;
-  int32_t s_end = rule_off[1];
+  int32_t s_end = n_strat > 0 ? rule_off[1] : 0;
   uint64_t acc = 0;  // lane k: word gw0 + k
   auto flush = [&]() {
     if (lane < kRun && gw0 + lane < W64) viol_out[(int64_t)s * W64 + gw0 + lane] = acc;
     acc = 0;
   };
-  auto load = [&](int32_t r, pas_rule* ru, int64_t (&v)[kRun], uint64_t* pr) {
-    *ru = rules[min(r, r_end - 1)];
-    const int32_t m = (ru->metric >= 0 && ru->metric < M) ? ru->metric : 0;
+  // rule records arrive two rules ahead (scalar loads), so the column loads of the next rule
+  // never wait for its record
+  auto load = [&](const pas_rule& ru, int64_t (&v)[kRun], uint64_t* pr) {
+    const int32_t m = (ru.metric >= 0 && ru.metric < M) ? ru.metric : 0;
     const int64_t* col = vals + (int64_t)m * N;
 #pragma unroll
     for (int k = 0; k < kRun; ++k) v[k] = col[min((gw0 + k) * 64 + lane, N - 1)];
     *pr = present[(int64_t)m * W64 + pw_lane];
   };
-  pas_rule ru;
+  pas_rule ru{}, ru1{};
   int64_t v[kRun];
   uint64_t pr = 0;
-  if (r_begin < r_end) load(r_begin, &ru, v, &pr);
+  if (r_begin < r_end) {  // (no rule records to read otherwise)
+    ru = rules[r_begin];
+    ru1 = rules[min(r_begin + 1, r_end - 1)];
+    load(ru, v, &pr);
+  }
   for (int32_t r = r_begin; r < r_end; ++r) {
     while (r >= s_end) {  // the list has passed strategy s: its words are complete
       flush();
       ++s;
       s_end = rule_off[s + 1];
     }
-    pas_rule nru;
+    const pas_rule ru2 = rules[min(r + 2, r_end - 1)];
     int64_t nv[kRun];
     uint64_t npr;
-    load(r + 1, &nru, nv, &npr);  // the next run in flight during this rule's compares
+    load(ru1, nv, &npr);  // the next run in flight during this rule's compares
     if (ru.metric >= 0 && ru.metric < M && ru.op >= 0 && ru.op <= 2) {
       int64_t tm = 0;
       const int sat = target_milli(ru.target, &tm);
@@ -887,7 +892,8 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
         acc = lane == k ? (acc | (mask & pr)) : acc;
       }
     }
-    ru = nru;
+    ru = ru1;
+    ru1 = ru2;
     pr = npr;
 #pragma unroll
     for (int k = 0; k < kRun; ++k) v[k] = nv[k];
