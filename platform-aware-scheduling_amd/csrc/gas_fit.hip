@@ -637,7 +637,7 @@ __device__ __forceinline__ uint32_t fit_mask(const int64_t (&need)[C],
   return bm;
 }
 
-constexpr int kMB = 8;  // multi-selection pods staged in LDS per round and wave
+constexpr int kMB = 4;  // multi-selection pods staged in LDS per round and wave
 constexpr int kRowChunks = kPacked * (int)sizeof(GasSel) / 16;  // 16-B chunks per row
 
 // Fit mask of the compared kinds (all but SKIP) of a threshold row: bit k = card k's snapshot
@@ -752,6 +752,89 @@ __device__ __forceinline__ uint32_t multi_closed(const int64_t (&free)[kMaxCards
   return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
 }
 
+// Lane-private copy of the node's free values of the compared kinds (all but SKIP) in LDS,
+// [card][lane][kind], so that a lane can read its chosen card's values back with one LDS read
+// (registers cannot be indexed per lane).
+template <int kC>
+struct FreeTab {
+  int64_t* base;  // this wave's table: kMaxCards * 64 * kC
+  __device__ __forceinline__ int64_t* at(uint32_t card, int lane) const {
+    return base + ((int64_t)card * 64 + lane) * kC;
+  }
+};
+
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ void fill_tab(const int64_t (&free)[kMaxCards][Q], const FreeTab<kC>& tab,
+                                         int lane) {
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != SKIP) tab.at(k, lane)[j++] = free[k][q];
+}
+
+// threshold row th (all Q kinds, SKIP dropped) against a gathered card's free values
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ bool th_fits(const int64_t* th, const int64_t (&g)[kC]) {
+  bool ok = true;
+#pragma unroll
+  for (int q = 0, j = 0; q < Q; ++q)
+    if (q != SKIP) ok &= th[q] <= g[j++];
+  return ok;
+}
+
+// multi_closed with the rows that only matter at an already chosen card (2, 4, 5, 6) checked
+// at that card alone, on its free values read back from the lane's LDS copy: S = 2 computes
+// two fit masks instead of three, S = 3 three instead of seven.
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCards][Q],
+                                                   const GasThresholds& t, int32_t S,
+                                                   uint64_t live, uint32_t node_ok,
+                                                   const FreeTab<kC>& tab, int lane) {
+  const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
+  int64_t th[7][Q];
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) th[j][q] = j < 3 || S == 3 ? t.th[j][q] : 0;
+  uint32_t m0, m1, m3 = 0u;
+  th_mask2<Q, SKIP>(free, th[0], th[1], live, &m0, &m1);
+  if (S == 3) m3 = th_mask<Q, SKIP>(free, th[3], live);
+  if (over & 1) m0 = 0u;  // an overflowing threshold passes no card
+  if (over & 2) m1 = 0u;
+  if (over & 8) m3 = 0u;
+  const uint32_t c0 = lowest(m0);
+  int64_t g0[kC];
+  {
+    const int64_t* p = tab.at(min(c0, 7u), lane);
+#pragma unroll
+    for (int j = 0; j < kC; ++j) g0[j] = p[j];
+  }
+  const bool b2 = !(over & 4) && th_fits<Q, SKIP, kC>(th[2], g0);
+  const uint32_t c1 = min(lowest(m1 & ~(1u << c0)), (c0 < 8u && b2) ? c0 : 8u);
+  uint32_t word = c0 | (c1 << 3);
+  bool fits = c0 < 8u && c1 < 8u;
+  if (S == 3) {
+    int64_t g1[kC];
+    const int64_t* p = tab.at(min(c1, 7u), lane);
+#pragma unroll
+    for (int j = 0; j < kC; ++j) g1[j] = p[j];
+    uint32_t touched;
+    if (c0 == c1) {
+      touched = (!(over & 64) && th_fits<Q, SKIP, kC>(th[6], g0)) ? c0 : 8u;
+    } else {
+      const uint32_t t4 = (!(over & 16) && th_fits<Q, SKIP, kC>(th[4], g0)) ? c0 : 8u;
+      const uint32_t t5 = (!(over & 32) && th_fits<Q, SKIP, kC>(th[5], g1)) ? c1 : 8u;
+      touched = min(t4, t5);
+    }
+    const uint32_t untouched = lowest(m3 & ~(1u << c0) & ~(1u << c1));
+    const uint32_t c2 = min(untouched, touched);
+    fits = fits && c2 < 8u;
+    word |= c2 << 6;
+  }
+  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
 // A pod with 4 to 8 selections: the selections in order on a working copy of the free values
 // (registers), each a fit mask on the copy; the chosen card's copy drops by the take, updated
 // under the lanes that chose it (one branch per card some lane chose).
@@ -794,8 +877,9 @@ __device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards]
 // waiting for its copy does not hold up the other waves of the block.
 template <int Q, int SKIP, bool kBits>
 __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                           int32_t* stage_w, uint32_t node_ok, int32_t N,
-                                           int32_t n, bool valid, const int32_t* __restrict__ list,
+                                           int32_t* stage_w, int64_t* tab_base, uint32_t node_ok,
+                                           int32_t N, int32_t n, bool valid,
+                                           const int32_t* __restrict__ list,
                                            const GasSel* __restrict__ sels,
                                            const int32_t* __restrict__ count, const BlockTile& bt,
                                            uint32_t* __restrict__ res,
@@ -804,18 +888,29 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
   const uint64_t live = __ballot(valid && node_ok != 0u);
   int32_t i0, i1;
   list_share(count, bt, &i0, &i1);
-  for (int32_t b0 = i0; b0 < i1; b0 += kMB) {
-    const int32_t nb = min(kMB, i1 - b0);
-    // every load of the batch in flight before the LDS writes (rows past nb: not read)
+  // lists with a skipped kind read chosen cards back from the lane's LDS copy (kC = Q - 1)
+  constexpr bool kGather = Q > 1 && SKIP >= 0;
+  constexpr int kC = Q > 1 ? Q - 1 : 1;
+  const FreeTab<kC> tab{tab_base};
+  if (kGather && i0 < i1) fill_tab<Q, SKIP, kC>(free, tab, lane);
+  // a batch's rows are loaded one batch ahead: every load of the next batch is in flight
+  // while this batch's pods are evaluated (rows past the batch: zeros, not read)
+  constexpr int kIters = kMB * kRowChunks / 64;
+  int4 v[kIters];
+  int32_t wd = 0;
+  auto load_batch = [&](int32_t b0) {
+    const int32_t nb = max(0, min(kMB, i1 - b0));
     const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
-    constexpr int kIters = kMB * kRowChunks / 64;
-    int4 v[kIters];
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
       const int32_t c = lane + it * 64;
       v[it] = c < nb * kRowChunks ? src[c] : int4{0, 0, 0, 0};
     }
-    const int32_t wd = lane < nb ? list[b0 + lane] : 0;
+    wd = lane < nb ? list[b0 + lane] : 0;
+  };
+  if (i0 < i1) load_batch(i0);
+  for (int32_t b0 = i0; b0 < i1; b0 += kMB) {
+    const int32_t nb = min(kMB, i1 - b0);
     __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
 #pragma unroll
     for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
@@ -823,6 +918,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    load_batch(b0 + kMB);
     for (int32_t j = 0; j < nb; ++j) {
       const int32_t pw = __builtin_amdgcn_readfirstlane(stage_w[j]);
       const int32_t pod = pw & 0xFFFFFF;
@@ -830,7 +926,10 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
       const GasSel* rec = stage + j * kPacked;
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
-        if (S <= 3)
+        if (S <= 3 && kGather)
+          out = multi_closed_g<Q, SKIP, kC>(free, *reinterpret_cast<const GasThresholds*>(rec), S,
+                                            live, node_ok, tab, lane);
+        else if (S <= 3)
           out = multi_closed<Q, SKIP>(free, *reinterpret_cast<const GasThresholds*>(rec), S, live,
                                       node_ok);
         else if (S <= kPacked)
@@ -843,18 +942,19 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
 
 template <int Q, bool kBits, int L = 0>
 __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                            int32_t* stage_w, uint32_t node_ok, int32_t N,
+                                            int32_t* stage_w, int64_t* tab, uint32_t node_ok,
+                                            int32_t N,
                                             int32_t n, bool valid, int32_t P,
                                             const int32_t* __restrict__ multi,
                                             const GasSel* __restrict__ sels,
                                             const int32_t* __restrict__ counts,
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
-  multi_list<Q, L - 1, kBits>(free, stage, stage_w, node_ok, N, n, valid, multi + (int64_t)L * P,
+  multi_list<Q, L - 1, kBits>(free, stage, stage_w, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
                               sels + (int64_t)L * P * kPacked, counts + L, bt,
                               res, fit);
   if constexpr (L < Q)
-    multi_lists<Q, kBits, L + 1>(free, stage, stage_w, node_ok, N, n, valid, P, multi, sels,
+    multi_lists<Q, kBits, L + 1>(free, stage, stage_w, tab, node_ok, N, n, valid, P, multi, sels,
                                  counts, bt, res, fit);
 }
 
@@ -867,6 +967,8 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     uint64_t* __restrict__ fit) {
   __shared__ GasSel stage[kTpb / 64][kPacked * kMB];  // a slice per wave
   __shared__ int32_t stage_w[kTpb / 64][kMB];
+  constexpr int kC = Q > 1 ? Q - 1 : 1;
+  __shared__ int64_t tab[kTpb / 64][kMaxCards * 64 * kC];  // FreeTab per wave
   const BlockTile bt = block_tile(chunks);
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
@@ -876,8 +978,8 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  multi_lists<Q, kBits>(free, stage[wave], stage_w[wave], node_ok, N, n, valid, P, multi, sels,
-                        counts, bt, res, fit);
+  multi_lists<Q, kBits>(free, stage[wave], stage_w[wave], tab[wave], node_ok, N, n, valid, P,
+                        multi, sels, counts, bt, res, fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
