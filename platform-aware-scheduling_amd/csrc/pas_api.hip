@@ -189,6 +189,7 @@ void pas_destroy(pas_ctx* ctx) {
   if (ctx->aux) (void)hipFree(ctx->aux);
   if (ctx->label_part) (void)hipFree(ctx->label_part);
   if (ctx->gas_limit) (void)hipFree(ctx->gas_limit);
+  if (ctx->tas_gpass) (void)hipFree(ctx->tas_gpass);
   if (ctx->gas_limit_ev) (void)hipEventDestroy(ctx->gas_limit_ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;

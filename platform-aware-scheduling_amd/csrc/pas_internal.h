@@ -97,6 +97,8 @@ struct pas_ctx {
   void* aux = nullptr;  // per-call device table: TAS rule ranges / GAS container steps
   size_t aux_bytes = 0;
   int64_t* label_part = nullptr;  // per-workgroup partial counts of the label plan
+  void* tas_gpass = nullptr;  // pass bitmaps of clusters past the LDS bitmap (tas_eval)
+  size_t tas_gpass_bytes = 0;
   int64_t* gas_limit = nullptr;     // pods of the last GAS fit past PAS_GAS_MAX_SELECTIONS
   hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
   // timing

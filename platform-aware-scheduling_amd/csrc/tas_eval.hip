@@ -363,6 +363,8 @@ struct EvalParams {
   int32_t* order_len;    // [P]
   int32_t topk;          // 0: whole HostPriorityList; else its first topk entries
   int32_t out_stride;    // N, or topk
+  int32_t pos_base;      // first bucketed position of this launch
+  uint32_t* gpass;       // kGP: [grid][W32p] pass bitmaps in global scratch
 };
 
 // One workgroup of kW waves per pod, XCD-aware over the bucketed pod list (blocks b and b+8
@@ -384,7 +386,10 @@ struct EvalParams {
 // kS: adjacent segments per wave per round.  kAblate (diagnostic timing builds only,
 // PAS_EVAL_ABLATE; outputs wrong): 1 = no stores, 2 = no count exchange, 4 = no pass-bit
 // lookups, 8 = no rule loop.
-template <int kW, int kS, int kAblate, int kAux = kNtAux>
+// kGP (clusters past the LDS pass bitmap, ~1.1M nodes): the pod's pass bitmap lives in a
+// global scratch row instead (P.gpass, one row per workgroup of the launch; lookups are
+// workgroup-coherent loads, clears are L2 atomics) — the same algorithm, slower lookups.
+template <int kW, int kS, int kAblate, int kAux = kNtAux, bool kGP = false>
 __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
   constexpr int T = kW * 64;
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -392,17 +397,19 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
   int32_t* s_base = s_pref + kRuleChunk;              // [kRuleChunk] perm index of range start
   int32_t* s_total = s_base + kRuleChunk;             // [1]
   int32_t* s_cnt = s_total + 16;                      // [2][kW] kept counts per round
-  uint32_t* pass = lds + kMiscWords;                  // [W32p]
+  const int32_t nb = gridDim.x, b = blockIdx.x;
+  const int32_t xcd = b & 7, per_xcd = nb >> 3, rem = nb & 7;
+  const int32_t slot = xcd * per_xcd + min(xcd, rem) + (b >> 3);
+  const int32_t pos = P.pos_base + slot;
+  uint32_t* pass = kGP ? P.gpass + (int64_t)slot * P.W32p : lds + kMiscWords;  // [W32p]
   uint64_t* pass64 = reinterpret_cast<uint64_t*>(pass);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // uniform, in an SGPR
   const int lane = threadIdx.x & 63, tid = threadIdx.x;
-  int32_t* stage = reinterpret_cast<int32_t*>(pass + P.W32p) + wave * kStageWords;
-  const uint32_t pass_off = (uint32_t)(size_t)(lds_u32*)pass;    // LDS byte offsets
+  int32_t* stage =
+      reinterpret_cast<int32_t*>(kGP ? lds + kMiscWords : pass + P.W32p) + wave * kStageWords;
+  const uint32_t pass_off = kGP ? 0u : (uint32_t)(size_t)(lds_u32*)pass;  // LDS byte offsets
   const uint32_t stage_off = (uint32_t)(size_t)(lds_u32*)stage;
 
-  const int32_t nb = gridDim.x, b = blockIdx.x;
-  const int32_t xcd = b & 7, per_xcd = nb >> 3, rem = nb & 7;
-  const int32_t pos = xcd * per_xcd + min(xcd, rem) + (b >> 3);
   const int4 d0 = P.desc[2 * pos], d1 = P.desc[2 * pos + 1];
   // block-uniform, kept in SGPRs (the output descriptors built from them must be scalar)
   const int32_t pod = __builtin_amdgcn_readfirstlane(d0.x);
@@ -512,7 +519,10 @@ __global__ __launch_bounds__(kW * 64) void tas_eval_kernel(EvalParams P) {
         for (int j = 0; j < kSegWords; ++j) {  // all 16 reads in flight
           uint32_t word;  // node >> 5 (bfe: the compiler's shift/mask/add form is longer)
           asm("v_bfe_u32 %0, %1, 5, 27" : "=v"(word) : "v"(node[i][j]));
-          w[j] = (kAblate & 4) ? ~0u : *(lds_u32*)(size_t)(pass_off + word * 4u);
+          if constexpr (kGP)
+            w[j] = __hip_atomic_load(pass + word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          else
+            w[j] = (kAblate & 4) ? ~0u : *(lds_u32*)(size_t)(pass_off + word * 4u);
         }
         cnt[i] = 0;
 #pragma unroll
@@ -954,12 +964,28 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   ep.R = t.row;
   ep.W64 = W64;
   ep.W32p = (2 * W64 + 1 + 3) & ~3;  // + the sentinel's zero word, 16-byte multiple
-  const size_t eval_lds =
+  size_t eval_lds =
       sizeof(uint32_t) * ((size_t)kMiscWords + ep.W32p + (size_t)tune.waves * kStageWords);
   // (kS segments of a wave share its stage: compact_store finishes with the stage first)
-  if (eval_lds > 160 * 1024)
-    return set_error(ctx, PAS_ECAPACITY,
-                     "pas_tas_eval: n_nodes too large for the LDS pass bitmap (max ~1M nodes)");
+  // past ~1.1M nodes the pass bitmaps move to global scratch, launched in chunks of pods
+  const bool global_pass = eval_lds > 160 * 1024 || env_int("PAS_EVAL_GLOBAL_PASS", 0);
+  int32_t chunk = n_pods;
+  if (global_pass) {
+    eval_lds = sizeof(uint32_t) * ((size_t)kMiscWords + 4 * (size_t)kStageWords);
+    const size_t row = sizeof(uint32_t) * (size_t)ep.W32p;
+    chunk = (int32_t)std::max<size_t>(1, std::min<size_t>(n_pods, (256u << 20) / row));
+    const size_t need = row * (size_t)chunk;
+    if (need > ctx->tas_gpass_bytes) {
+      if (ctx->tas_gpass) {
+        PAS_HIP(ctx, hipStreamSynchronize(s));
+        PAS_HIP(ctx, hipFree(ctx->tas_gpass));
+        ctx->tas_gpass = nullptr;
+        ctx->tas_gpass_bytes = 0;
+      }
+      PAS_HIP(ctx, hipMalloc(&ctx->tas_gpass, need));
+      ctx->tas_gpass_bytes = need;
+    }
+  }
   if (n_pods == 0) return PAS_OK;
 
   // scratch: ranges | desc | keys
@@ -1011,6 +1037,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   ep.order_len = d_len;
   ep.topk = topk;
   ep.out_stride = topk ? topk : N;
+  ep.pos_base = 0;
+  ep.gpass = static_cast<uint32_t*>(ctx->tas_gpass);
   using EvalFn = void (*)(EvalParams);
   EvalFn fn = &tas_eval_kernel<4, 1, 0>;
 #define PAS_EVAL_CASE(W, S, A) \
@@ -1025,11 +1053,16 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   if (tune.store_aux == 16) fn = &tas_eval_kernel<4, 1, 0, 16>;
   if (tune.store_aux == 18) fn = &tas_eval_kernel<4, 1, 0, 18>;
   if (tune.store_aux == 19) fn = &tas_eval_kernel<4, 1, 0, 19>;
+  if (global_pass) fn = &tas_eval_kernel<4, 1, 0, kNtAux, true>;
+  const int32_t waves = global_pass ? 4 : tune.waves;
   if (eval_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)eval_lds));
   timing_begin(ctx, s, PAS_K_TAS_EVAL, &tl);
-  fn<<<(unsigned)n_pods, (unsigned)(tune.waves * 64), eval_lds, s>>>(ep);
+  for (int32_t p0 = 0; p0 < n_pods; p0 += chunk) {
+    ep.pos_base = p0;
+    fn<<<(unsigned)std::min(chunk, n_pods - p0), (unsigned)(waves * 64), eval_lds, s>>>(ep);
+  }
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   timing_end(ctx, s, &span);

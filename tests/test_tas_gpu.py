@@ -312,6 +312,28 @@ def test_c2_full_size_properties(ctx, oracle):
             assert bool(ok.all()), f"pod {q} not in documented order"
 
 
+@pytest.mark.parametrize("flags", [1, 2, 3])
+def test_global_pass_bitmap_path(ctx, oracle, monkeypatch, flags):
+    # the path for clusters past the LDS pass bitmap, forced at small sizes: the same
+    # results with the bitmaps in global scratch (PAS_EVAL_GLOBAL_PASS)
+    monkeypatch.setenv("PAS_EVAL_GLOBAL_PASS", "1")
+    rng = np.random.default_rng(70 + flags)
+    for n in (1, 65, 1025, 5000):
+        for cand_frac in (None, 0.6):
+            v, pres, rules, off, prio, cand = random_case(rng, n, 4, 7, 5, cand_frac=cand_frac)
+            assert_same(ctx, oracle, v, pres, rules, off, prio, cand, flags)
+
+
+@pytest.mark.slow
+def test_cluster_past_lds_bitmap(ctx, oracle):
+    # 1.3M nodes: the pass bitmap no longer fits a workgroup's LDS (~1.1M nodes), so the
+    # kernel keeps it in global scratch; full ordered lists, filter rows and lengths vs the
+    # oracle
+    rng = np.random.default_rng(13)
+    v, pres, rules, off, prio, cand = random_case(rng, 1_300_000, 3, 6, 4, cand_frac=0.5)
+    assert_same(ctx, oracle, v, pres, rules, off, prio, cand, 3)
+
+
 def test_deschedule_parity(ctx, oracle):
     rng = np.random.default_rng(4)
     for n in (1, 64, 65, 5000):
