@@ -637,7 +637,7 @@ __device__ __forceinline__ uint32_t fit_mask(const int64_t (&need)[C],
   return bm;
 }
 
-constexpr int kMB = 4;  // multi-selection pods staged in LDS per round and wave
+constexpr int kMB = 2;  // multi-selection pods staged in LDS per round and wave (LDS: 4 workgroups per CU)
 constexpr int kRowChunks = kPacked * (int)sizeof(GasSel) / 16;  // 16-B chunks per row
 
 // Fit mask of the compared kinds (all but SKIP) of a threshold row: bit k = card k's snapshot
