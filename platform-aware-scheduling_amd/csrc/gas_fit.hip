@@ -263,6 +263,17 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
         t.th[j][q] = v;
       }
     }
+    // full-mask rows (0, 1, 3: a selection's own need) that repeat an earlier one (the
+    // selections of one container are identical): bit 8 row 1 == row 0, bit 9 row 3 == row 0,
+    // bit 10 row 3 == row 1 — the kernel copies the mask instead of computing it
+    auto same = [&](int a, int b) {
+      bool eq = ((t.over >> a) & 1) == ((t.over >> b) & 1);
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) eq = eq && t.th[a][q] == t.th[b][q];
+      return eq;
+    };
+    if (same(1, 0)) t.over |= 1 << 8;
+    if (steps == 3 && same(3, 0)) t.over |= 1 << 9;
+    if (steps == 3 && same(3, 1)) t.over |= 1 << 10;
     *reinterpret_cast<GasThresholds*>(out) = t;
   }
   multi[(int64_t)l * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
@@ -798,8 +809,17 @@ __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCar
 #pragma unroll
     for (int q = 0; q < Q; ++q) th[j][q] = j < 3 || S == 3 ? t.th[j][q] : 0;
   uint32_t m0, m1, m3 = 0u;
-  th_mask2<Q, SKIP>(free, th[0], th[1], live, &m0, &m1);
-  if (S == 3) m3 = th_mask<Q, SKIP>(free, th[3], live);
+  if (over & (1 << 8)) {  // the first two selections ask the same: one mask
+    m0 = th_mask<Q, SKIP>(free, th[0], live);
+    m1 = m0;
+  } else {
+    th_mask2<Q, SKIP>(free, th[0], th[1], live, &m0, &m1);
+  }
+  if (S == 3) {
+    if (over & (1 << 9)) m3 = m0;
+    else if (over & (1 << 10)) m3 = m1;
+    else m3 = th_mask<Q, SKIP>(free, th[3], live);
+  }
   if (over & 1) m0 = 0u;  // an overflowing threshold passes no card
   if (over & 2) m1 = 0u;
   if (over & 8) m3 = 0u;
