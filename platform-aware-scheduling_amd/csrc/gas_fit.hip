@@ -225,15 +225,26 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   // the pod's row sits at its list position, so a batch of a list is one contiguous copy
   GasSel* out = sels + ((int64_t)l * n_pods + slot) * kPacked;
   int32_t k = 0, bad = 0;
-  int64_t cmp3[3][PAS_GAS_MAX_RES], take3[3][PAS_GAS_MAX_RES];  // first 3 selections
+  // the first three selections in named registers (a runtime-indexed array would live in
+  // scratch memory)
+  int64_t cmp0[PAS_GAS_MAX_RES], cmp1[PAS_GAS_MAX_RES], cmp2[PAS_GAS_MAX_RES];
+  int64_t take0[PAS_GAS_MAX_RES], take1[PAS_GAS_MAX_RES];
+#pragma unroll
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q) cmp0[q] = cmp1[q] = cmp2[q] = take0[q] = take1[q] = 0;
   for (int32_t c = 0; c < nc; ++c) {
     const GasStep g = container_step(row + c, n_res, i915, req, mask);
     bad |= g.num_i915 > 0 ? g.bad : 0;
     for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
-      if (k < 3) {
-        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
-          cmp3[k][q] = g.cmp[q];
-          take3[k][q] = g.take[q];
+#pragma unroll
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+        if (k == 0) {
+          cmp0[q] = g.cmp[q];
+          take0[q] = g.take[q];
+        } else if (k == 1) {
+          cmp1[q] = g.cmp[q];
+          take1[q] = g.take[q];
+        } else if (k == 2) {
+          cmp2[q] = g.cmp[q];
         }
       }
       if (steps <= 3) continue;
@@ -249,25 +260,42 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   if (steps <= 3) {
     // thresholds: need plus the takes of a subset of the earlier selections (cards taken
     // from by exactly those selections); unrequested kinds stay INT64_MIN
+    //   row 0: c0   1: c1   2: c1 + t0   3: c2   4: c2 + t0   5: c2 + t1   6: c2 + t0 + t1
     GasThresholds t = {};
-    const int32_t subs[7][3] = {{0, 0, 0}, {1, 0, 0}, {1, 1, 0}, {2, 0, 0},
-                                {2, 1, 0}, {2, 0, 1}, {2, 1, 1}};  // {selection, +t0, +t1}
-    for (int j = 0; j < (steps == 2 ? 3 : 7); ++j) {
-      const int32_t sel = subs[j][0];
-      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
-        int64_t v = cmp3[sel][q];
-        if (v != INT64_MIN) {
-          for (int e = 0; e < 2; ++e)
-            if (subs[j][1 + e] && __builtin_add_overflow(v, take3[e][q], &v)) t.over |= 1 << j;
-        }
-        t.th[j][q] = v;
+    auto add = [](int64_t v, int64_t d, bool* o) {
+      int64_t r;
+      if (__builtin_add_overflow(v, d, &r)) *o = true;
+      return r;
+    };
+#pragma unroll
+    for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+      bool o2 = false, o4 = false, o5 = false, o6 = false;
+      t.th[0][q] = cmp0[q];
+      t.th[1][q] = cmp1[q];
+      t.th[2][q] = cmp1[q] == INT64_MIN ? cmp1[q] : add(cmp1[q], take0[q], &o2);
+      t.th[3][q] = cmp2[q];
+      t.th[4][q] = cmp2[q] == INT64_MIN ? cmp2[q] : add(cmp2[q], take0[q], &o4);
+      t.th[5][q] = cmp2[q] == INT64_MIN ? cmp2[q] : add(cmp2[q], take1[q], &o5);
+      if (cmp2[q] == INT64_MIN) {
+        t.th[6][q] = cmp2[q];
+      } else {
+        const int64_t v = add(cmp2[q], take0[q], &o6);
+        t.th[6][q] = o6 ? v : add(v, take1[q], &o6);
       }
+      t.over |= (o2 ? 4 : 0) | (o4 ? 16 : 0) | (o5 ? 32 : 0) | (o6 ? 64 : 0);
+    }
+    if (steps == 2) {  // rows 3..6 unused
+#pragma unroll
+      for (int j = 3; j < 7; ++j)
+#pragma unroll
+        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) t.th[j][q] = 0;
+      t.over &= 7;
     }
     // full-mask rows (0, 1, 3: a selection's own need) that repeat an earlier one (the
     // selections of one container are identical): bit 8 row 1 == row 0, bit 9 row 3 == row 0,
     // bit 10 row 3 == row 1 — the kernel copies the mask instead of computing it
     auto same = [&](int a, int b) {
-      bool eq = ((t.over >> a) & 1) == ((t.over >> b) & 1);
+      bool eq = true;
       for (int q = 0; q < PAS_GAS_MAX_RES; ++q) eq = eq && t.th[a][q] == t.th[b][q];
       return eq;
     };
