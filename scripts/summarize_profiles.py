@@ -21,7 +21,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles")
 TAS_PATH = ("tas_prep_kernel", "tas_eval_kernel")
 GAS_PATH = ("gas_minfree_kernel", "gas_prep_kernel", "gas_fit_single_kernel",
-            "gas_fit_multi_kernel")
+            "gas_fit_multi_kernel", "gas_fit_generic_kernel")
 
 
 def short(name):
@@ -91,7 +91,9 @@ def main():
             traffic["gas_fit_kernel"] = round(sum(hbm(k) for k in GAS_PATH))
             traffic["gas_fit_by_kernel"] = {k: round(hbm(k)) for k in GAS_PATH}
         elif w == "deschedule":
-            traffic["tas_violations_kernel"] = round(hbm("tas_violations_kernel"))
+            # the sweep kernel (tas_violations_run_kernel since round 2), under the bench's key
+            traffic["tas_violations_kernel"] = round(hbm("tas_violations_run_kernel") or
+                                                     hbm("tas_violations_kernel"))
             traffic["label_plan_kernel"] = round(hbm("label_plan_kernel"))
         elif w == "c5":
             traffic["c5_by_kernel"] = {k: round(hbm(k)) for k in kernels}
