@@ -221,8 +221,9 @@ def synthetic_args_body(names, seed=7):
 def request_latency(ctx, batch, n_nodes, reps=5):
     """End-to-end latency of one TAS filter request and one prioritize request over the
     resident n_nodes snapshot: pas_decode_args of a full-NodeList body
-    (every node a candidate) -> pas_tas_eval (host API: candidate bitmap up, pass row and
-    ordered list down) -> pas_encode_tas_filter_result / pas_encode_host_priority_list.  The
+    (every node a candidate) -> pas_tas_eval (filter: candidate bitmap up, pass row down) /
+    pas_tas_prioritize_request (request node ids up, ordered request positions down) ->
+    pas_encode_tas_filter_result / pas_encode_host_priority_list.  The
     name table and the snapshot-name array are per snapshot (built once, untimed); node JSON
     for the FilterResult points into the request body.  Median of reps."""
     import ctypes
@@ -268,10 +269,11 @@ def request_latency(ctx, batch, n_nodes, reps=5):
         assert rc == 0
         filter_bytes = out_len.value
         t3 = time.perf_counter()
-        _, order, plen = ctx.tas_eval(1, rules[:0], np.array([0, 0], np.int32), prio, cand,
-                                      _lib.PAS_TAS_PRIORITIZE)
+        pos = ctx.tas_prioritize_request(1, prio[0], req)
         t4 = time.perf_counter()
-        rc = lib.pas_encode_host_priority_list(int(plen[0]), order.ctypes.data_as(vp), name_arr,
+        # request positions index the request's own names; this body lists the snapshot's
+        # nodes in snapshot order, so those are name_arr
+        rc = lib.pas_encode_host_priority_list(len(pos), pos.ctypes.data_as(vp), name_arr,
                                                out, cap, ctypes.byref(out_len))
         assert rc == 0
         t5 = time.perf_counter()

@@ -174,6 +174,30 @@ int pas_tas_eval_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
                         uint64_t* d_pass_out, int32_t* d_order_out, int32_t* d_order_len,
                         void* hip_stream);
 
+/* Prioritize of ONE extender request in the request's own terms.  Replaces
+ * prioritizeNodesForRule (telemetryscheduler.go:128-149) + core.OrderedList
+ * (operator.go:30-42) for args.Nodes.Items given as
+ *   req_node [n_req]  snapshot node index of Items[j] (pas_decode_args' req_node; -1 or any
+ *                     index outside [0, n_nodes) = a node the snapshot does not hold)
+ *   prio              the pod's scheduleonmetric Rules[0] (host struct); metric < 0 = no
+ *                     rule / metric not cached -> empty list
+ * Outputs
+ *   pos_out  [n_req]  request positions j of the listed nodes, best first (-1 past len);
+ *                     HostPriority i is {Items[pos_out[i]].Name, 10 - i}
+ *   len_out           entries: the distinct request nodes that have the metric
+ * Order: GreaterThan value descending, LessThan ascending, ties by ascending position of
+ * the node's first occurrence in the request; any other operator: first occurrences in
+ * request order.  (pas_tas_eval breaks ties by snapshot node index instead; the two agree
+ * when the request lists nodes in snapshot order.)  A repeated name is listed once
+ * (filteredNodeData is a map, :135-139).  The _device form takes device req_node /
+ * pos_out / len_out and is asynchronous on hip_stream. */
+int pas_tas_prioritize_request(pas_ctx* ctx, uint64_t gen, const pas_rule* prio, int32_t n_req,
+                               const int32_t* req_node, int32_t* pos_out, int32_t* len_out);
+int pas_tas_prioritize_request_device(pas_ctx* ctx, uint64_t gen, const pas_rule* prio,
+                                      int32_t n_req, const int32_t* d_req_node,
+                                      int32_t* d_pos_out, int32_t* d_len_out,
+                                      void* hip_stream);
+
 /* Deschedule sweep: for each registered deschedule strategy s (rules
  * rules[rule_off[s] .. rule_off[s+1])), the node set of deschedule.Strategy.Violated
  * (deschedule/strategy.go:31-50), as the bitmap viol_out[s][W64].  The per-node
@@ -503,8 +527,10 @@ int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
 #define PAS_K_TAS_PREP 5       /* rule ranges + pods bucketed by prioritize order */
 #define PAS_K_TAS_LABELS 6     /* deschedule label plan */
 #define PAS_K_TAS_SPAN 7       /* whole pas_tas_eval path: first launch start to last launch end */
-#define PAS_K_COUNT 8
-#define PAS_TIMING_SPAN 1    /* whole paths: PAS_K_TAS_SPAN, the GAS fit and deschedule launches */
+#define PAS_K_PRIO_REQUEST 8   /* whole pas_tas_prioritize_request path (keys, sort, positions) */
+#define PAS_K_COUNT 9
+#define PAS_TIMING_SPAN 1    /* whole paths: PAS_K_TAS_SPAN, PAS_K_PRIO_REQUEST, the GAS fit and
+                                deschedule launches */
 #define PAS_TIMING_KERNELS 2 /* every launch (events between launches add small gaps) */
 int pas_set_timing(pas_ctx* ctx, int level); /* 0 = off */
 /* Sum of elapsed ms and number of launches recorded for a kernel since the last reset. */

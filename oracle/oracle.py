@@ -44,6 +44,7 @@ def load():
         "or_evaluate_rule": (c_int, [c_int64, c_int32, c_int64]),
         "or_violated": (c_int, [c_int32, c_int32, P, P, P, c_int32, P]),
         "or_ordered_list": (c_int32, [c_int32, c_int32, P, P, P, P, P]),
+        "or_ordered_list_request": (c_int32, [c_int32, c_int32, P, P, P, c_int32, P, P]),
         "or_tas_eval": (c_int, [c_int32, c_int32, P, P, c_int32, P, P, P, P, c_uint32, P, P, P]),
         "or_tas_violations": (c_int, [c_int32, c_int32, P, P, c_int32, P, P, P]),
         "or_rm_add": (c_int, [POINTER(OrRm), c_int32, c_int64]),
@@ -106,6 +107,18 @@ def tas_eval(v_milli, present, rules, rule_off, prio, cand=None, flags=3):
     if rc != 0:
         raise ValueError("oracle: invalid operator (the reference panics)")
     return pass_out, order, lens
+
+
+def prioritize_request(v_milli, present, prio, req_node):
+    """Request positions best-first for one request (SURVEY.md A.3 tie order)."""
+    v = np.ascontiguousarray(v_milli, np.int64)
+    m, n = v.shape
+    p = np.ascontiguousarray(present, np.uint64)
+    rule = np.ascontiguousarray(np.asarray(prio, RULE_DTYPE).reshape(1))
+    req = np.ascontiguousarray(req_node, np.int32)
+    out = np.zeros(max(len(req), 1), np.int32)
+    k = load().or_ordered_list_request(n, m, _p(v), _p(p), _p(rule), len(req), _p(req), _p(out))
+    return out[:k]
 
 
 def tas_violations(v_milli, present, rules, rule_off):

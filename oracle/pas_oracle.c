@@ -132,6 +132,35 @@ int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_mil
   return cnt;
 }
 
+int32_t or_ordered_list_request(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                                const uint64_t* present, const or_rule* rule, int32_t n_req,
+                                const int32_t* req_node, int32_t* out_pos) {
+  if (rule->metric < 0 || !metric_in_cache(n_nodes, n_metrics, present, rule->metric)) return 0;
+  const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
+  const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
+  const size_t cap = (size_t)(n_req > 0 ? n_req : 1);
+  sortable* items = (sortable*)malloc(sizeof(sortable) * cap);
+  sortable* tmp = (sortable*)malloc(sizeof(sortable) * cap);
+  uint8_t* seen = (uint8_t*)calloc((size_t)(n_nodes > 0 ? n_nodes : 1), 1);
+  int32_t cnt = 0;
+  for (int32_t j = 0; j < n_req; ++j) {       /* for _, node := range nodes.Items */
+    const int32_t n = req_node[j];
+    if (n < 0 || n >= n_nodes || seen[n]) continue;  /* not cached / map key already set */
+    seen[n] = 1;
+    if (!has_bit(pres, n)) continue;          /* if v, ok := nodeData[node.Name]; ok */
+    items[cnt].node = j;
+    items[cnt].value = col[n];
+    ++cnt;
+  }
+  if (rule->op == 1) merge_sort(items, tmp, cnt, 1);
+  else if (rule->op == 0) merge_sort(items, tmp, cnt, 0);
+  for (int32_t i = 0; i < cnt; ++i) out_pos[i] = items[i].node;
+  free(items);
+  free(tmp);
+  free(seen);
+  return cnt;
+}
+
 int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
                 const uint64_t* present, int32_t n_pods, const or_rule* rules,
                 const int32_t* rule_off, const or_rule* prio, const uint64_t* cand,

@@ -50,6 +50,16 @@ int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_mil
                         const uint64_t* present, const or_rule* rule, const uint8_t* cand,
                         int32_t* out);
 
+/* The same for one extender request in the request's own terms:
+ * req_node[j] = snapshot node of args.Nodes.Items[j] (-1 / out of range = not in the
+ * snapshot).  filteredNodeData (telemetryscheduler.go:135-139) keeps one entry per name;
+ * the entries are taken in order of first occurrence and stably sorted by value, so ties
+ * (and every entry for other operators) keep ascending first-occurrence position.  Writes
+ * request positions best-first to out_pos and returns the count. */
+int32_t or_ordered_list_request(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                                const uint64_t* present, const or_rule* rule, int32_t n_req,
+                                const int32_t* req_node, int32_t* out_pos);
+
 /* Batched equivalent of pas_tas_eval (include/pas.h): per pod, filterNodes
  * (telemetryscheduler.go:184-225) and/or prioritizeNodesForRule.  Same argument
  * layout as the C-ABI host entry point.  Returns 0 or -1 (invalid operator). */

@@ -61,7 +61,7 @@ void timing_begin(pas_ctx* ctx, hipStream_t s, int kernel, TimedLaunch* tl) {
   // span-level timing brackets whole paths only: events between the launches of a path
   // would add gaps to the span they measure
   if (!ctx->timing || (ctx->timing == PAS_TIMING_SPAN && kernel != PAS_K_TAS_SPAN &&
-                       kernel != PAS_K_GAS_FIT && kernel != PAS_K_TAS_VIOLATIONS &&
+                       kernel != PAS_K_PRIO_REQUEST && kernel != PAS_K_GAS_FIT && kernel != PAS_K_TAS_VIOLATIONS &&
                        kernel != PAS_K_TAS_LABELS))
     return;
   tl->start = take_event(ctx);
@@ -435,6 +435,56 @@ int pas_tas_eval_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
   if ((rc = activate(ctx))) return rc;
   return tas_eval_launch(ctx, n_pods, n_rules, d_rules, d_rule_off, d_prio, d_cand, flags,
                          d_pass_out, d_order_out, d_order_len, 0, pick_stream(ctx, hip_stream));
+}
+
+static int check_prio_request(pas_ctx* ctx, const pas_rule* prio, int32_t n_req,
+                              const void* req, const void* pos, const void* len) {
+  if (!prio || n_req < 0 || !len || (n_req > 0 && (!req || !pos)))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_prioritize_request: bad argument");
+  if (prio->metric >= ctx->tas.n_metrics)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_prioritize_request: metric out of range");
+  return PAS_OK;
+}
+
+int pas_tas_prioritize_request(pas_ctx* ctx, uint64_t gen, const pas_rule* prio, int32_t n_req,
+                               const int32_t* req_node, int32_t* pos_out, int32_t* len_out) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if ((rc = check_prio_request(ctx, prio, n_req, req_node, pos_out, len_out))) return rc;
+  if ((rc = activate(ctx))) return rc;
+  const size_t ws = prio_request_workspace(ctx, n_req);
+  if (!ws) return set_error(ctx, PAS_EDEVICE, "pas_tas_prioritize_request: sort sizing failed");
+  const size_t b_req = sizeof(int32_t) * (size_t)std::max(n_req, 1);
+  if ((rc = ensure_scratch(ctx, carve_size({b_req, b_req, sizeof(int32_t), ws})))) return rc;
+  Carve cv{static_cast<char*>(ctx->scratch)};
+  int32_t* d_req = cv.take<int32_t>(std::max(n_req, 1));
+  int32_t* d_pos = cv.take<int32_t>(std::max(n_req, 1));
+  int32_t* d_len = cv.take<int32_t>(1);
+  void* d_ws = cv.take<char>(ws);
+  hipStream_t s = ctx->stream;
+  if (n_req) PAS_HIP(ctx, hipMemcpyAsync(d_req, req_node, b_req, hipMemcpyHostToDevice, s));
+  if ((rc = prio_request_launch(ctx, *prio, n_req, d_req, d_pos, d_len, d_ws, ws, s))) return rc;
+  PAS_HIP(ctx, hipMemcpyAsync(len_out, d_len, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+  if (n_req) PAS_HIP(ctx, hipMemcpyAsync(pos_out, d_pos, b_req, hipMemcpyDeviceToHost, s));
+  PAS_HIP(ctx, hipStreamSynchronize(s));
+  return PAS_OK;
+}
+
+int pas_tas_prioritize_request_device(pas_ctx* ctx, uint64_t gen, const pas_rule* prio,
+                                      int32_t n_req, const int32_t* d_req_node,
+                                      int32_t* d_pos_out, int32_t* d_len_out,
+                                      void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if ((rc = check_prio_request(ctx, prio, n_req, d_req_node, d_pos_out, d_len_out))) return rc;
+  if ((rc = activate(ctx))) return rc;
+  const size_t ws = prio_request_workspace(ctx, n_req);
+  if (!ws) return set_error(ctx, PAS_EDEVICE, "pas_tas_prioritize_request: sort sizing failed");
+  if ((rc = ensure_scratch(ctx, ws))) return rc;
+  return prio_request_launch(ctx, *prio, n_req, d_req_node, d_pos_out, d_len_out, ctx->scratch,
+                             ws, pick_stream(ctx, hip_stream));
 }
 
 int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const pas_rule* rules,

@@ -141,6 +141,12 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
                     uint32_t flags, uint64_t* d_pass, int32_t* d_order, int32_t* d_len,
                     int32_t topk, hipStream_t s);
+// Single-request prioritize (tas_request.hip): workspace bytes for n_req positions, and the
+// launch (rule is host-side; ws = that many device bytes).
+size_t prio_request_workspace(pas_ctx* ctx, int32_t n_req);
+int prio_request_launch(pas_ctx* ctx, const pas_rule& rule, int32_t n_req, const int32_t* d_req,
+                        int32_t* d_pos, int32_t* d_len, void* ws, size_t ws_bytes,
+                        hipStream_t s);
 int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
                           const int32_t* d_rule_off, uint64_t* d_viol, hipStream_t s);
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,

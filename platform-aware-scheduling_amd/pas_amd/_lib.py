@@ -64,6 +64,7 @@ PAS_K_GAS_FIT = 4
 PAS_K_TAS_PREP = 5
 PAS_K_TAS_LABELS = 6
 PAS_K_TAS_SPAN = 7
+PAS_K_PRIO_REQUEST = 8
 KERNEL_NAMES = {
     PAS_K_TAS_LABELS: "label_plan_kernel",
     PAS_K_TAS_EVAL: "tas_eval_kernel",
@@ -72,6 +73,7 @@ KERNEL_NAMES = {
     PAS_K_GAS_FIT: "gas_fit_kernel",
     PAS_K_TAS_PREP: "tas_prep_kernel",
     PAS_K_TAS_SPAN: "tas_eval_span",
+    PAS_K_PRIO_REQUEST: "prio_request_span",
 }
 
 
@@ -119,6 +121,8 @@ SIGNATURES = {
         c_int, [_P, c_uint64, c_uint64, c_int32, _P, _P, _P, _P]),
     "pas_tas_snapshot_info":(c_int, [_P, POINTER(c_uint64), POINTER(c_int32), POINTER(c_int32)]),
     "pas_tas_eval": (c_int, [_P, c_uint64, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P]),
+    "pas_tas_prioritize_request": (c_int, [_P, c_uint64, _P, c_int32, _P, _P, _P]),
+    "pas_tas_prioritize_request_device": (c_int, [_P, c_uint64, _P, c_int32, _P, _P, _P, _P]),
     "pas_tas_eval_device": (
         c_int,
         [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P, _P],

@@ -229,6 +229,26 @@ class Context:
                                          _stream(stream))
         self._check(rc, "pas_tas_eval_device")
 
+    def tas_prioritize_request(self, gen: int, prio, req_node) -> np.ndarray:
+        """Request positions best-first for one extender request (pas_tas_prioritize_request,
+        SURVEY.md A.3 tie order); req_node[j] = snapshot node of Items[j] or -1."""
+        rule = np.ascontiguousarray(np.asarray(prio, dtype=RULE_DTYPE).reshape(1))
+        req = np.ascontiguousarray(req_node, dtype=np.int32)
+        pos = np.zeros(max(len(req), 1), np.int32)
+        n = ctypes.c_int32(0)
+        rc = self._l.pas_tas_prioritize_request(self._h, gen, _ptr(rule), len(req), _ptr(req),
+                                                _ptr(pos), ctypes.byref(n))
+        self._check(rc, "pas_tas_prioritize_request")
+        return pos[: n.value]
+
+    def tas_prioritize_request_device(self, gen: int, prio, n_req: int, req_t, pos_t, len_t,
+                                      stream=None):
+        rule = np.ascontiguousarray(np.asarray(prio, dtype=RULE_DTYPE).reshape(1))
+        rc = self._l.pas_tas_prioritize_request_device(self._h, gen, _ptr(rule), n_req,
+                                                       _dptr(req_t), _dptr(pos_t), _dptr(len_t),
+                                                       _stream(stream))
+        self._check(rc, "pas_tas_prioritize_request_device")
+
     def tas_violations(self, gen: int, rules: np.ndarray, rule_off: np.ndarray) -> np.ndarray:
         rule_off = np.ascontiguousarray(rule_off, dtype=np.int32)
         s = rule_off.shape[0] - 1

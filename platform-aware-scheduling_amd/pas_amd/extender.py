@@ -156,15 +156,14 @@ class MetricsExtender:
         if prio[0][0] not in self.metric_index:  # ReadMetric error -> [] (:130-133)
             return status, b"[]\n"
         # nodes without metrics in the snapshot are left out, as filteredNodeData keeps only
-        # nodes with a metric (telemetryscheduler.go:128-149): the candidate bitmap has no
-        # bit for them
+        # nodes with a metric (telemetryscheduler.go:128-149); ties keep request order
+        # (SURVEY.md A.3): pas_tas_prioritize_request lists request positions
         code = parse_operator(prio[0][1])
         p = make_rules([self.metric_index[prio[0][0]]], [code if code >= 0 else 3],
                        [int(prio[0][2])])
-        _, order, lens = self.ctx.tas_eval(self.gen, make_rules([], [], []),
-                                           np.zeros(2, np.int32), p, cand[None, :],
-                                           _lib.PAS_TAS_PRIORITIZE)
-        return status, wire.host_priority_list(order[0, : lens[0]], self.table)
+        pos = self.ctx.tas_prioritize_request(self.gen, p[0], idx)
+        table = wire.NodeTable(self._names(body, info, idx))
+        return status, wire.host_priority_list(pos, table)
 
     def bind(self, body: bytes) -> Tuple[int, bytes]:
         return 404, b""  # not implemented by TAS (:178-181)

@@ -54,6 +54,18 @@ def test_prioritize_golden_g5(ctx):
         assert body.endswith(b"\n")
 
 
+def test_prioritize_ties_keep_request_order(ctx):
+    # equal values: the HostPriorityList follows args.Nodes.Items, whatever
+    # the snapshot's node numbering; a repeated name is listed once
+    m = tas(ctx, {"node A": 50, "node B": 50}, TEST_POLICY1, 8103)
+    for names in (["node B", "node A"], ["node A", "node B"], ["node B", "node B", "node A"]):
+        status, body = m.prioritize(args(TWO_NODES["pod_labels"], names))
+        assert status == 200
+        want = list(dict.fromkeys(names))
+        assert [[h["Host"], h["Score"]] for h in json.loads(body)] == [
+            [n, 10 - i] for i, n in enumerate(want)]
+
+
 def test_prioritize_errors_g6(ctx):
     # policy not found -> [] (scheduler_test.go:175-183)
     m = tas(ctx, {"node A": 90, "node B": 100}, TEST_POLICY2, 8101)
