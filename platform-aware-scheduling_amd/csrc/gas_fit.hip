@@ -71,7 +71,10 @@ struct alignas(16) GasThresholds {
   int32_t over;
   int32_t pad[7];
 };
-static_assert(sizeof(GasThresholds) <= sizeof(GasSel) * kPacked, "row");
+// A multi-selection pod's row: its selections as GasSel (rows 0 .. S-1); a pod with 2 or 3
+// selections also has its thresholds from row kThRow on.
+constexpr int kThRow = 4;
+static_assert(sizeof(GasThresholds) <= sizeof(GasSel) * (kPacked - kThRow), "row");
 constexpr int32_t kBadPod = 1 << 30;  // multi-list word flag: a selection has a negative need
 
 // Pod with at most one card selection: its selecting step (compare form), and
@@ -247,7 +250,6 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
           cmp2[q] = g.cmp[q];
         }
       }
-      if (steps <= 3) continue;
       GasSel e = {};
 #pragma unroll
       for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
@@ -302,7 +304,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
     if (same(1, 0)) t.over |= 1 << 8;
     if (steps == 3 && same(3, 0)) t.over |= 1 << 9;
     if (steps == 3 && same(3, 1)) t.over |= 1 << 10;
-    *reinterpret_cast<GasThresholds*>(out) = t;
+    *reinterpret_cast<GasThresholds*>(out + kThRow) = t;
   }
   multi[(int64_t)l * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
 }
@@ -825,11 +827,11 @@ __device__ __forceinline__ bool th_fits(const int64_t* th, const int64_t (&g)[kC
 // multi_closed with the rows that only matter at an already chosen card (2, 4, 5, 6) checked
 // at that card alone, on its free values read back from the lane's LDS copy: S = 2 computes
 // two fit masks instead of three, S = 3 three instead of seven.
-template <int Q, int SKIP, int kC>
+template <int Q, int SKIP, int kC, int S>
 __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCards][Q],
-                                                   const GasThresholds& t, int32_t S,
-                                                   uint64_t live, uint32_t node_ok,
-                                                   const FreeTab<kC>& tab, int lane) {
+                                                   const GasThresholds& t, uint64_t live,
+                                                   uint32_t node_ok, const FreeTab<kC>& tab,
+                                                   int lane) {
   const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
   int64_t th[7][Q];
 #pragma unroll
@@ -919,6 +921,97 @@ __device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards]
   return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
 }
 
+// A pod with several selections, in order: selection t takes the first card (lexicographic)
+// whose current free covers its need (getCardsForContainerGPURequest, scheduler.go:200-257;
+// addRM after each take).  A card no earlier selection of the pod took from still has its
+// snapshot free, so the candidates are the fit mask of the need on the snapshot (free only
+// falls: a card outside the mask cannot pass); among them a card an earlier selection s took
+// from passes only if its current free cur[s] covers the need.  So
+//   c_t = lowest(mask(need_t) without {c_s : s < t, need_t > cur[s]})
+// and the take lowers cur of every s with c_s = c_t (a card first taken reads its snapshot
+// free from the lane's LDS copy).  Registers only, unrolled over t; a selection whose need
+// equals the previous one's reuses its mask (the selections of one container are identical).
+#ifndef PAS_GAS_SEQ_FROM
+#define PAS_GAS_SEQ_FROM 4  // pods with at least this many selections take this path
+#endif
+constexpr int kSeqFrom = PAS_GAS_SEQ_FROM;
+
+__device__ __forceinline__ bool uniform_eq(int64_t a, int64_t b) {
+  const uint64_t x = (uint64_t)a ^ (uint64_t)b;
+  return (__builtin_amdgcn_readfirstlane((uint32_t)x) |
+          __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32))) == 0u;
+}
+
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q],
+                                              const GasSel* rec, int32_t S, uint64_t live,
+                                              uint32_t node_ok, const FreeTab<kC>& tab,
+                                              int lane) {
+  typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+  int64_t fr[kMaxCards][kC];
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != SKIP) fr[k][j++] = free[k][q];
+  int64_t cur[kPacked][kC];
+  uint32_t cs[kPacked];
+  uint32_t word = 0u, m = 0u;
+  bool fits = true;
+  int64_t prev[kC];
+#pragma unroll
+  for (int t = 0; t < kPacked; ++t) {
+    if (t >= S) break;
+    int64_t need[kC], neg[kC];
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != SKIP) {
+        const v2i64 ct = *reinterpret_cast<const v2i64*>(rec[t].ct[q]);
+        need[j] = ct.x;
+        neg[j++] = ct.y;
+      }
+    bool same = t > 0;
+#pragma unroll
+    for (int j = 0; j < kC; ++j) same = same && uniform_eq(need[j], prev[j]);
+    if (!same) m = fit_mask<kC>(need, fr, live);
+    uint32_t bad = 0u;
+#pragma unroll
+    for (int s2 = 0; s2 < t; ++s2) {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[s2][j];
+      bad |= ok ? 0u : (1u << cs[s2]);
+    }
+    const uint32_t c = lowest(m & ~bad);
+    fits = fits && c < 8u;
+    if (!__ballot(fits)) break;
+    int64_t g[kC];
+    {
+      const int64_t* p = tab.at(min(c, 7u), lane);
+#pragma unroll
+      for (int j = 0; j < kC; ++j) g[j] = p[j];
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < t; ++s2)
+#pragma unroll
+      for (int j = 0; j < kC; ++j) g[j] = cs[s2] == c ? cur[s2][j] : g[j];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) g[j] += neg[j];
+#pragma unroll
+    for (int s2 = 0; s2 < t; ++s2)
+#pragma unroll
+      for (int j = 0; j < kC; ++j) cur[s2][j] = cs[s2] == c ? g[j] : cur[s2][j];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      cur[t][j] = g[j];
+      prev[j] = need[j];
+    }
+    cs[t] = c;
+    word |= (c & 7u) << (3 * t);
+  }
+  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
 // Pods with several selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
 // the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
 // reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
@@ -974,12 +1067,14 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
       const GasSel* rec = stage + j * kPacked;
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
-        if (S <= 3 && kGather)
-          out = multi_closed_g<Q, SKIP, kC>(free, *reinterpret_cast<const GasThresholds*>(rec), S,
-                                            live, node_ok, tab, lane);
-        else if (S <= 3)
-          out = multi_closed<Q, SKIP>(free, *reinterpret_cast<const GasThresholds*>(rec), S, live,
-                                      node_ok);
+        const GasThresholds& th = *reinterpret_cast<const GasThresholds*>(rec + kThRow);
+        if (S <= (kSeqFrom <= 3 ? kSeqFrom - 1 : 3) && kGather)
+          out = S == 2 ? multi_closed_g<Q, SKIP, kC, 2>(free, th, live, node_ok, tab, lane)
+                       : multi_closed_g<Q, SKIP, kC, 3>(free, th, live, node_ok, tab, lane);
+        else if (S <= 3 && !kGather)
+          out = multi_closed<Q, SKIP>(free, th, S, live, node_ok);
+        else if (S <= kPacked && kGather && S >= kSeqFrom)
+          out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane);
         else if (S <= kPacked)
           out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
       }
