@@ -121,14 +121,14 @@ def bench_tas(args, world, rank):
         ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pass_t, order_t,
                             len_t, stream)
 
+    settle_steps = distrib.settle(step, args.settle)
     for _ in range(args.warmup):
         step()
-    # timed steps: span events only (HIP events on the launch stream around the path)
-    ctx.reset_timing()
-    ctx.set_timing(1)
-    elapsed = timed_steps(step, args.steps, 0, world)
-    span_ms, span_n = ctx.kernel_time(_lib.PAS_K_TAS_SPAN)
-    span_ms /= max(span_n, 1)
+    # timed steps: two HIP events on the launch stream around all of them (events between
+    # the steps would add ~10 us each to the wall)
+    gpu = {}
+    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu)
+    span_ms = gpu["ms_per_step"]
     # per-kernel breakdown from extra, untimed steps (events around every launch)
     ctx.reset_timing()
     ctx.set_timing(2)
@@ -163,7 +163,7 @@ def bench_tas(args, world, rank):
         "vs_baseline": None,
         "dtype": "int64",
         "data": "synthetic (seeded cluster snapshot + pod batch, SURVEY.md §8(d) distributions)",
-        "config": {
+        "config": {"settle_steps": settle_steps, 
             "workload": "tas_filter_prioritize (BASELINE configs[1])",
             "pods_per_gpu": P, "nodes": N, "metrics": M, "rules_per_pod": R + 1,
             "parallelism": f"pod-sharded x{world} (independent batches, replicated snapshot)",
@@ -174,8 +174,9 @@ def bench_tas(args, world, rank):
         },
         "roofline": {
             "bound": "hbm",
-            "kernel": "tas path span: tas_prep (rule ranges + pod grouping) and tas_eval "
-                      "(filter + ordered lists) on one stream (HIP events around both launches)",
+            "kernel": "tas path: tas_prep (rule ranges + pod grouping) and tas_eval "
+                      "(filter + ordered lists) on one stream (two HIP events on the launch "
+                      "stream around the timed steps)",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
@@ -359,15 +360,20 @@ def bench_gas(args, world, rank):
     def step():
         ctx.gas_fit_device(1, P, C, wl.I915, req_t, mask_t, nc_t, res_t, stream)
 
+    settle_steps = distrib.settle(step, args.settle)
     for _ in range(args.warmup):
         step()
+    gpu = {}
+    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu)
+    # the fit launches alone, from extra, untimed steps (span events around them)
     ctx.reset_timing()
     ctx.set_timing(1)
-    elapsed = timed_steps(step, args.steps, 0, world)
+    for _ in range(min(args.steps, 5)):
+        step()
     ctx.set_timing(0)
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
     alg_bytes = N * (8 * Q + 8 * K * Q + 4) + P * (8 * C * Q + 4 * C + 4) + 4 * P * N
-    kernel_s = (k_ms / max(k_n, 1)) / 1e3
+    kernel_s = gpu["ms_per_step"] / 1e3
     achieved = alg_bytes / kernel_s / 1e9
     out = {
         "metric": "GAS per-card fit evals/sec (pod-node fits), 10k pods×50k nodes×8 cards",
@@ -375,12 +381,14 @@ def bench_gas(args, world, rank):
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C3)",
-        "config": {"workload": "gas_fit (BASELINE configs[2])", "pods_per_gpu": P, "nodes": N,
+        "config": {"settle_steps": settle_steps, "workload": "gas_fit (BASELINE configs[2])", "pods_per_gpu": P, "nodes": N,
                    "cards": K, "resources": Q,
                    "fit_fraction": float((res_t.cpu().numpy().view(np.uint32) >> 31).mean())},
         "roofline": {"bound": "hbm",
-                     "kernel": "gas fit span: gas_fit_single_kernel, gas_fit_multi_kernel and "
-                               "gas_fit_generic_kernel (HIP events around the three launches)",
+                     "kernel": "gas fit path: gas_prep_kernel, gas_fit_single_kernel, "
+                               "gas_fit_multi_kernel and gas_fit_generic_kernel (two HIP events "
+                               "on the launch stream around the timed steps)",
+                     "fit_launches_ms": k_ms / max(k_n, 1),
                      "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic("gas_fit_kernel"), "algorithmic_bytes": alg_bytes,
@@ -454,6 +462,7 @@ def bench_deschedule(args, world, rank):
         ctx.tas_label_plan_device(n_local, S, viol_t, labels_t, add_t, rem_t, total_t, stream)
         gathered["v"] = shard.gather_violations(viol_t, world, N)
 
+    settle_steps = distrib.settle(step, args.settle)
     for _ in range(args.warmup):
         step()
     ctx.reset_timing()
@@ -474,7 +483,7 @@ def bench_deschedule(args, world, rank):
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int64",
         "data": "synthetic (SURVEY.md §8(d) C4)",
-        "config": {"workload": "tas_deschedule_sweep (BASELINE configs[3])", "nodes": N,
+        "config": {"settle_steps": settle_steps, "workload": "tas_deschedule_sweep (BASELINE configs[3])", "nodes": N,
                    "nodes_per_gpu": n_local, "metrics": M, "strategies": S, "rules": len(rules),
                    "step": "sweep + label plan (add/remove masks per node) + all-gather",
                    "snapshot_build_ms": snapshot_ms, "snapshot_refresh_ms": refresh,
@@ -527,6 +536,7 @@ def bench_c5(args, world, rank):
         result["nodes"], result["len"] = topk.run(1, P, len(tbatch.rules), rules_t, off_t,
                                                   prio_t, fit_t, stream)
 
+    settle_steps = distrib.settle(step, args.settle)
     for _ in range(args.warmup):
         step()
     elapsed = timed_steps(step, args.steps, 0, world)
@@ -538,7 +548,7 @@ def bench_c5(args, world, rank):
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int64",
         "data": "synthetic (SURVEY.md §8(d) C5)",
-        "config": {"workload": "tas_gas_topk_node_sharded (BASELINE configs[4])", "pods": P,
+        "config": {"settle_steps": settle_steps, "workload": "tas_gas_topk_node_sharded (BASELINE configs[4])", "pods": P,
                    "nodes": N, "nodes_per_gpu": n_local, "metrics": M, "rules_per_pod": R + 1,
                    "topk": K, "parallelism": f"node-sharded x{world}, top-k records "
                                              "all-gathered and merged",
@@ -576,6 +586,8 @@ def main():
     ap.add_argument("--rules", type=int, default=16)
     ap.add_argument("--topk", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--settle", type=float, default=0.3,
+                    help="seconds of untimed steps before the warmup steps (clocks settle)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-request-latency", action="store_true",
                     help="skip the f2 request-latency leg of the TAS workload")
@@ -600,6 +612,9 @@ def main():
     else:
         _load_package()
         world, rank, _ = distrib.setup()
+        # a stream of our own (not the null stream): libpas launches on it, and the timing
+        # events of distrib.timed_steps are recorded on it
+        torch.cuda.set_stream(torch.cuda.Stream())
         fn = {"tas": bench_tas, "gas": bench_gas, "deschedule": bench_deschedule,
               "c5": bench_c5}[args.workload]
         out = fn(args, world, rank)

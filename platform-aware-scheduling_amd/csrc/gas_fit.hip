@@ -40,6 +40,7 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+constexpr int kPrepTpb = 64;  // pods per prep block: small blocks spread the pods over the CUs
 constexpr int kMaxCards = PAS_GAS_PACKED;  // cards of a fast-path node, in registers
 constexpr int kPacked = PAS_GAS_PACKED;    // selections of a fast-path pod
 
@@ -173,7 +174,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
                                 GasSel* __restrict__ sels, int32_t* __restrict__ counts,
                                 int32_t* __restrict__ big_pods, int32_t* __restrict__ n_big_pods,
                                 int32_t* __restrict__ pod_steps) {
-  const int32_t p = blockIdx.x * kTpb + threadIdx.x;
+  const int32_t p = blockIdx.x * kPrepTpb + threadIdx.x;
   if (p >= n_pods) return;
   const int32_t nc = min(max(n_containers[p], 0), max_containers);
   const int64_t row = (int64_t)p * max_containers;
@@ -1284,9 +1285,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     return PAS_OK;
   }
   // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][P] | their
-  // selection rows [Q+1][P][8] | the generic path's pods [P], nodes [N] and per-pod
-  // selection counts [P] | the flipped kind minima [4], list counts [2(Q+1)] and the generic
-  // list counts [2] (zeroed together)
+  // selection rows [Q+1][P][8] | the generic path's pods [P] and per-pod selection counts
+  // [P] | list counts [2(Q+1)] and the generic pod count (zeroed together).  The flipped
+  // kind minima and the generic path's nodes depend on the snapshot alone: they sit in
+  // g.derived and are recomputed only after the snapshot changed.
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   const int32_t NL = Q + 1;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
@@ -1294,10 +1296,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_multi = al(sizeof(int32_t) * (size_t)NL * n_pods);
   const size_t b_sels = al(sizeof(GasSel) * kPacked * (size_t)NL * n_pods);
   const size_t b_pods = al(sizeof(int32_t) * (size_t)n_pods);
-  const size_t b_nodes = al(sizeof(int32_t) * (size_t)N);
-  constexpr size_t b_tail = PAS_GAS_MAX_RES * sizeof(unsigned long long) +
-                            (2 * (PAS_GAS_MAX_RES + 1) + 2) * sizeof(int32_t);
-  const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_nodes + b_tail;
+  constexpr size_t b_tail = (2 * (PAS_GAS_MAX_RES + 1) + 1) * sizeof(int32_t);
+  const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_tail;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -1319,19 +1319,23 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   base += b_pods;
   int32_t* pod_steps = reinterpret_cast<int32_t*>(base);
   base += b_pods;
-  int32_t* big_nodes = reinterpret_cast<int32_t*>(base);
-  base += b_nodes;
-  unsigned long long* gflip = reinterpret_cast<unsigned long long*>(base);
-  int32_t* counts = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
-  int32_t* n_big = counts + 2 * (PAS_GAS_MAX_RES + 1);  // {pods, nodes}
+  int32_t* counts = reinterpret_cast<int32_t*>(base);
+  int32_t* n_big_pods = counts + 2 * (PAS_GAS_MAX_RES + 1);
+  unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
+  int32_t* n_big_nodes = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
+  int32_t* big_nodes = reinterpret_cast<int32_t*>(static_cast<char*>(g.derived) + 64);
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
-  PAS_HIP(ctx, hipMemsetAsync(gflip, 0, b_tail, s));
-  gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
-                                                           gflip, big_nodes, n_big + 1);
-  gas_prep_kernel<<<(n_pods + kTpb - 1) / kTpb, kTpb, 0, s>>>(
+  PAS_HIP(ctx, hipMemsetAsync(counts, 0, b_tail, s));
+  if (ctx->gas.derived_epoch != ctx->gas.epoch) {
+    PAS_HIP(ctx, hipMemsetAsync(gflip, 0, 64, s));
+    gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
+                                                             gflip, big_nodes, n_big_nodes);
+    ctx->gas.derived_epoch = ctx->gas.epoch;
+  }
+  gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
-      multi, sels, counts, big_pods, n_big, pod_steps);
+      multi, sels, counts, big_pods, n_big_pods, pod_steps);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   // grids: (node block, pod chunk) pairs, ~4096 blocks; each kernel splits each of its
@@ -1368,9 +1372,9 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   ga.mask = d_req_mask;
   ga.ncont = d_n_containers;
   ga.big_pods = big_pods;
-  ga.n_big_pods = n_big;
+  ga.n_big_pods = n_big_pods;
   ga.big_nodes = big_nodes;
-  ga.n_big_nodes = n_big + 1;
+  ga.n_big_nodes = n_big_nodes;
   ga.pod_steps = pod_steps;
   ga.n_pods = n_pods;
   ga.res = d_res;

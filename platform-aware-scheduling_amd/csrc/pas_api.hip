@@ -122,6 +122,7 @@ void free_gas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(g.n_cards));
   free_ptr(reinterpret_cast<void*&>(g.cap));
   free_ptr(reinterpret_cast<void*&>(g.used));
+  free_ptr(g.derived);
   g = GasSnapshot{};
 }
 
@@ -547,6 +548,7 @@ static int gas_alloc(pas_ctx* ctx, int32_t n_nodes, int32_t max_cards, int32_t n
     PAS_HIP(ctx, hipMalloc(&g.cap, sizeof(int64_t) * nn * (size_t)std::max(n_res, 1)));
     PAS_HIP(ctx, hipMalloc(&g.used, sizeof(int64_t) * nn * (size_t)std::max(max_cards, 1) *
                                         (size_t)std::max(n_res, 1)));
+    PAS_HIP(ctx, hipMalloc(&g.derived, 64 + sizeof(int32_t) * nn));
     g.n_nodes = n_nodes;
     g.max_cards = max_cards;
     g.n_res = n_res;
@@ -589,6 +591,7 @@ int pas_gas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t ma
   }
   PAS_HIP(ctx, hipStreamSynchronize(s));
   g.gen = gen;
+  ++g.epoch;
   g.valid = true;
   return PAS_OK;
 }
@@ -616,6 +619,7 @@ int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
                                 hipMemcpyDeviceToDevice, s));
   }
   g.gen = gen;
+  ++g.epoch;
   g.valid = true;
   return PAS_OK;
 }
@@ -744,6 +748,7 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
   }
   PAS_HIP(ctx, hipStreamSynchronize(s));
   ctx->gas.gen = gen_to;
+  ++ctx->gas.epoch;
   return PAS_OK;
 }
 

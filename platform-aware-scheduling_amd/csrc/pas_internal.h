@@ -73,6 +73,12 @@ struct GasSnapshot {
   int32_t* n_cards = nullptr;
   int64_t* cap = nullptr;
   int64_t* used = nullptr;
+  // per-snapshot values the fit derives (gas_fit.hip: flipped kind minima, nodes past the
+  // fast kernels' card count), recomputed by the first fit after a change: `epoch` counts
+  // changes of n_cards / cap / used, `derived_epoch` is the epoch they were computed at
+  uint64_t epoch = 1;
+  uint64_t derived_epoch = 0;
+  void* derived = nullptr;  // gflip[4] u64 | n_big_nodes i32 (+pad) | big_nodes[N] i32
 };
 
 struct TimedLaunch {

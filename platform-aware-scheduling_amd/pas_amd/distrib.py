@@ -68,9 +68,26 @@ def gather_objects(obj, world):
     return out
 
 
-def timed_steps(step, steps, warmup, world, sync=None):
+def settle(step, seconds, sync=None):
+    """Untimed steps for `seconds` of wall time before the warmup: the first ~20 steps of a
+    fresh process run a few % slower (clocks, page tables), which a handful of warmup steps
+    does not cover.  Returns the number of steps run."""
+    if sync is None:
+        sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(4):
+            step()
+        n += 4
+        sync()
+    return n
+
+
+def timed_steps(step, steps, warmup, world, sync=None, gpu=None):
     """Run `warmup` untimed steps, then time exactly `steps` steps bracketed by
-    sync + barrier on both sides; returns the MAX elapsed seconds over ranks."""
+    sync + barrier on both sides; returns the MAX elapsed seconds over ranks.
+    gpu: a dict that receives "ms_per_step", the GPU time of the timed steps measured by two
+    HIP events on the current stream around them (no events between the steps)."""
     if sync is None:
         sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     for _ in range(warmup):
@@ -78,12 +95,21 @@ def timed_steps(step, steps, warmup, world, sync=None):
     sync()
     barrier(world)
     sync()
+    ev = None
+    if gpu is not None:
+        ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
     t0 = time.perf_counter()
+    if ev:
+        ev[0].record()
     for _ in range(steps):
         step()
+    if ev:
+        ev[1].record()
     sync()
     barrier(world)
     t1 = time.perf_counter()
+    if ev:
+        gpu["ms_per_step"] = ev[0].elapsed_time(ev[1]) / max(steps, 1)
     return max_over_ranks(t1 - t0, world)
 
 
