@@ -843,6 +843,9 @@ __global__ __launch_bounds__(kTpb) void tas_violations_dedup_kernel(
 // rule's run is already in flight.  Lane k keeps word k's violation mask of the open
 // strategy (its presence word is lane k's own load); at a strategy's end lanes 0..kRun-1
 // store its words with one coalesced store.
+#ifndef PAS_VIOL_NT
+#define PAS_VIOL_NT 1  // non-temporal column loads: each column byte is read once per sweep
+#endif
 template <int kRun>
 __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
@@ -867,7 +870,10 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     const int32_t m = (ru.metric >= 0 && ru.metric < M) ? ru.metric : 0;
     const int64_t* col = vals + (int64_t)m * N;
 #pragma unroll
-    for (int k = 0; k < kRun; ++k) v[k] = col[min((gw0 + k) * 64 + lane, N - 1)];
+    for (int k = 0; k < kRun; ++k) {
+      const int64_t* a = col + min((gw0 + k) * 64 + lane, N - 1);
+      v[k] = PAS_VIOL_NT ? __builtin_nontemporal_load(a) : *a;
+    }
     *pr = present[(int64_t)m * W64 + pw_lane];
   };
   pas_rule ru{}, ru1{};
