@@ -42,7 +42,7 @@ constexpr int kMaxGroupMetrics = 4096;    // 3 * M + 1 buckets in LDS for the gr
 constexpr int kMiscWords = 4 * kRuleChunk + 16;
 constexpr int kStageWords = ((kSegPos + 31 + 255) / 256) * 256;  // 5 x 256 (b128 reads)
 constexpr int kDumpSlot = kStageWords - 1;  // compaction target of dropped lanes (> 1055)
-constexpr int kNtAux = 2;                   // buffer store cache policy: nt
+constexpr int kNtAux = 18;  // whole-line store cache policy: sc1 nt (streamed out, not kept in L2)
 static_assert(kSegPos == kOrderPad, "order rows are padded by one segment");
 
 typedef int32_t v4i32 __attribute__((ext_vector_type(4)));
@@ -1057,7 +1057,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   if (tune.store_aux == 0) fn = &tas_eval_kernel<4, 1, 0, 0>;
   if (tune.store_aux == 3) fn = &tas_eval_kernel<4, 1, 0, 3>;
   if (tune.store_aux == 16) fn = &tas_eval_kernel<4, 1, 0, 16>;
-  if (tune.store_aux == 18) fn = &tas_eval_kernel<4, 1, 0, 18>;
+  if (tune.store_aux == 2) fn = &tas_eval_kernel<4, 1, 0, 2>;
   if (tune.store_aux == 19) fn = &tas_eval_kernel<4, 1, 0, 19>;
   if (global_pass) fn = &tas_eval_kernel<4, 1, 0, kNtAux, true>;
   const int32_t waves = global_pass ? 4 : tune.waves;
