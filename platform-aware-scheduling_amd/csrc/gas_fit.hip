@@ -391,6 +391,9 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
 #ifndef PAS_GAS_ABLATE
 #define PAS_GAS_ABLATE 0  // diagnostic timing builds only: 1 = no result stores (outputs wrong)
 #endif
+#ifndef PAS_GAS_STORE_AUX
+#define PAS_GAS_STORE_AUX 2  // result word store cache policy: nt (0: plain global store)
+#endif
 template <bool kBits>
 __device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t* __restrict__ fit,
                                            int64_t p, int32_t N, int32_t n, bool valid,
@@ -402,6 +405,11 @@ __device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t*
   if (kBits) {
     const uint64_t b = __ballot(valid && (out >> 31));
     if ((threadIdx.x & 63) == 0 && n < N) fit[p * ((N + 63) / 64) + (n >> 6)] = b;
+  } else if (PAS_GAS_STORE_AUX) {
+    // the pod's row as a buffer (lanes past N store nothing), with the store cache policy
+    const __amdgpu_buffer_rsrc_t row =
+        __builtin_amdgcn_make_buffer_rsrc(res + p * N, 0, N * 4, 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(out, row, n * 4, 0, PAS_GAS_STORE_AUX);
   } else if (valid) {
     res[p * N + n] = out;
   }
