@@ -91,19 +91,22 @@ struct alignas(16) GasSingle {
 __device__ GasStep container_step(int64_t i, int32_t n_res, int32_t i915,
                                   const int64_t* __restrict__ req,
                                   const uint32_t* __restrict__ mask) {
+  // every load unconditional (clamped to the row), so the mask and values arrive together
   const uint32_t m = mask[i];
+  int64_t rv[PAS_GAS_MAX_RES];
+#pragma unroll
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q) rv[q] = req[i * n_res + min(q, n_res - 1)];
   int64_t ni = 0;
-  if (i915 >= 0 && ((m >> i915) & 1u)) {
-    const int64_t v = req[i * n_res + i915];
-    if (v > 0) ni = v;
-  }
+#pragma unroll
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q)
+    if (q == i915 && ((m >> q) & 1u) && rv[q] > 0) ni = rv[q];
   GasStep g = {};
   g.num_i915 = m != 0u ? (int32_t)min(ni, (int64_t)PAS_GAS_MAX_SELECTIONS + 1) : 0;
   g.kinds = (int32_t)(m & ((1u << n_res) - 1u));
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
     const bool has = q < n_res && ((m >> q) & 1u);
-    int64_t v = has ? req[i * n_res + q] : 0;
+    int64_t v = has ? rv[q] : 0;
     if (ni > 1) v /= ni;
     if (has && v < 0) g.bad = 1;
     g.take[q] = v;
