@@ -81,6 +81,9 @@ int pas_create(const pas_config* cfg, pas_ctx** out);
 void pas_destroy(pas_ctx* ctx);
 const char* pas_last_error(const pas_ctx* ctx);
 int pas_set_stream(pas_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
+/* A hip_stream argument (here and in every _device entry point) of NULL names the context's
+ * current stream; PAS_STREAM_NULL names the HIP null stream (e.g. torch's default stream). */
+#define PAS_STREAM_NULL ((void*)1)
 int pas_synchronize(pas_ctx* ctx);
 
 /* Operator string -> pas_op ("LessThan", "GreaterThan", "Equals"), else PAS_EINVAL.

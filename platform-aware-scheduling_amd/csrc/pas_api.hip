@@ -28,6 +28,7 @@ int activate(pas_ctx* ctx) {
 }
 
 hipStream_t pick_stream(pas_ctx* ctx, void* s) {
+  if (s == PAS_STREAM_NULL) return nullptr;  // the HIP null stream
   return s ? reinterpret_cast<hipStream_t>(s) : ctx->stream;
 }
 
@@ -200,7 +201,9 @@ const char* pas_last_error(const pas_ctx* ctx) { return ctx ? ctx->err.c_str() :
 
 int pas_set_stream(pas_ctx* ctx, void* hip_stream) {
   if (!ctx) return PAS_EINVAL;
-  ctx->stream = hip_stream ? reinterpret_cast<hipStream_t>(hip_stream) : ctx->own_stream;
+  ctx->stream = hip_stream == PAS_STREAM_NULL ? nullptr
+                : hip_stream                  ? reinterpret_cast<hipStream_t>(hip_stream)
+                                              : ctx->own_stream;
   return PAS_OK;
 }
 

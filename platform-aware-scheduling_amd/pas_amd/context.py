@@ -46,12 +46,16 @@ def _dptr(t):
     return c_void_p(t.data_ptr())
 
 
+PAS_STREAM_NULL = 1  # include/pas.h: the HIP null stream (NULL names the context's stream)
+
+
 def _stream(s):
+    """A hip_stream argument: None = the context's current stream; a torch.cuda.Stream or a raw
+    handle otherwise, torch's default (null) stream as PAS_STREAM_NULL."""
     if s is None:
         return None
-    if isinstance(s, int):
-        return c_void_p(s)
-    return c_void_p(s.cuda_stream)  # torch.cuda.Stream
+    h = s if isinstance(s, int) else s.cuda_stream
+    return c_void_p(h if h != 0 else PAS_STREAM_NULL)
 
 
 def parse_operator(op: str) -> int:

@@ -82,6 +82,8 @@ class ShardedTopK:
         key = self._buf("key", (n_pods, k), torch.int64)
         node = self._buf("node", (n_pods, k), torch.int32)
         ln = self._buf("len", (n_pods,), torch.int32)
+        if on_gpu and stream != cur:
+            stream.wait_stream(cur)  # the caller's inputs (rules, candidates) are written
         self.ctx.tas_topk_device(gen, n_pods, n_rules, rules_t, rule_off_t, prio_t, cand_t, k,
                                  self.node_base, key, node, ln, stream)
         if on_gpu and stream != cur:
@@ -94,6 +96,8 @@ class ShardedTopK:
         out_len = self._buf("out_len", (n_pods,), torch.int32)
         self.ctx.topk_merge_device(n_pods, k, self.world, keys_all, nodes_all, out_node, out_len,
                                    stream)
+        if on_gpu and stream != cur:
+            cur.wait_stream(stream)  # the caller reads the merged lists on its stream
         return out_node, out_len
 
 
