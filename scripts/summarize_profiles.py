@@ -88,8 +88,13 @@ def main():
             traffic["tas_path"] = round(sum(hbm(k) for k in TAS_PATH))
             traffic["tas_path_by_kernel"] = {k: round(hbm(k)) for k in TAS_PATH}
         elif w == "gas":
-            traffic["gas_fit_kernel"] = round(sum(hbm(k) for k in GAS_PATH))
+            # per step: gas_minfree_kernel runs once per snapshot change, not per fit
+            calls = {r["kernel"]: r["calls"] for r in rows}
+            per = max(calls.get("gas_fit_single_kernel", 1), 1)
+            wt = {k: min(calls.get(k, per) / per, 1.0) for k in GAS_PATH}
+            traffic["gas_fit_kernel"] = round(sum(hbm(k) * wt[k] for k in GAS_PATH))
             traffic["gas_fit_by_kernel"] = {k: round(hbm(k)) for k in GAS_PATH}
+            traffic["gas_fit_launches_per_step"] = {k: round(wt[k], 4) for k in GAS_PATH}
         elif w == "deschedule":
             # the sweep kernel (tas_violations_run_kernel since round 2), under the bench's key
             traffic["tas_violations_kernel"] = round(hbm("tas_violations_run_kernel") or
