@@ -839,12 +839,14 @@ __device__ __forceinline__ bool th_fits(const int64_t* th, const int64_t (&g)[kC
 // multi_closed with the rows that only matter at an already chosen card (2, 4, 5, 6) checked
 // at that card alone, on its free values read back from the lane's LDS copy: S = 2 computes
 // two fit masks instead of three, S = 3 three instead of seven.
-template <int Q, int SKIP, int kC, int S>
-__device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCards][Q],
-                                                   const GasThresholds& t, uint64_t live,
-                                                   uint32_t node_ok, const FreeTab<kC>& tab,
-                                                   int lane) {
-  const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
+// kOvf: some threshold of the pod overflows (over bits 0-6).  Such pods are rare, so the
+// common instantiation drops every overflow test.
+template <int Q, int SKIP, int kC, int S, bool kOvf>
+__device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards][Q],
+                                                const GasThresholds& t, int32_t over,
+                                                uint64_t live, uint32_t node_ok,
+                                                const FreeTab<kC>& tab, int lane) {
+  auto ov = [&](int bit) { return kOvf && (over & bit) != 0; };
   int64_t th[7][Q];
 #pragma unroll
   for (int j = 0; j < 7; ++j)
@@ -862,9 +864,9 @@ __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCar
     else if (over & (1 << 10)) m3 = m1;
     else m3 = th_mask<Q, SKIP>(free, th[3], live);
   }
-  if (over & 1) m0 = 0u;  // an overflowing threshold passes no card
-  if (over & 2) m1 = 0u;
-  if (over & 8) m3 = 0u;
+  if (ov(1)) m0 = 0u;  // an overflowing threshold passes no card
+  if (ov(2)) m1 = 0u;
+  if (ov(8)) m3 = 0u;
   const uint32_t c0 = lowest(m0);
   int64_t g0[kC];
   {
@@ -872,7 +874,7 @@ __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCar
 #pragma unroll
     for (int j = 0; j < kC; ++j) g0[j] = p[j];
   }
-  const bool b2 = !(over & 4) && th_fits<Q, SKIP, kC>(th[2], g0);
+  const bool b2 = !ov(4) && th_fits<Q, SKIP, kC>(th[2], g0);
   const uint32_t c1 = min(lowest(m1 & ~(1u << c0)), (c0 < 8u && b2) ? c0 : 8u);
   uint32_t word = c0 | (c1 << 3);
   bool fits = c0 < 8u && c1 < 8u;
@@ -883,10 +885,10 @@ __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCar
     for (int j = 0; j < kC; ++j) g1[j] = p[j];
     uint32_t touched;
     if (c0 == c1) {
-      touched = (!(over & 64) && th_fits<Q, SKIP, kC>(th[6], g0)) ? c0 : 8u;
+      touched = (!ov(64) && th_fits<Q, SKIP, kC>(th[6], g0)) ? c0 : 8u;
     } else {
-      const uint32_t t4 = (!(over & 16) && th_fits<Q, SKIP, kC>(th[4], g0)) ? c0 : 8u;
-      const uint32_t t5 = (!(over & 32) && th_fits<Q, SKIP, kC>(th[5], g1)) ? c1 : 8u;
+      const uint32_t t4 = (!ov(16) && th_fits<Q, SKIP, kC>(th[4], g0)) ? c0 : 8u;
+      const uint32_t t5 = (!ov(32) && th_fits<Q, SKIP, kC>(th[5], g1)) ? c1 : 8u;
       touched = min(t4, t5);
     }
     const uint32_t untouched = lowest(m3 & ~(1u << c0) & ~(1u << c1));
@@ -895,6 +897,17 @@ __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCar
     word |= c2 << 6;
   }
   return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
+template <int Q, int SKIP, int kC, int S>
+__device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCards][Q],
+                                                   const GasThresholds& t, uint64_t live,
+                                                   uint32_t node_ok, const FreeTab<kC>& tab,
+                                                   int lane) {
+  const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
+  if (over & 0x7F)
+    return closed_body<Q, SKIP, kC, S, true>(free, t, over, live, node_ok, tab, lane);
+  return closed_body<Q, SKIP, kC, S, false>(free, t, over, live, node_ok, tab, lane);
 }
 
 // A pod with 4 to 8 selections: the selections in order on a working copy of the free values
