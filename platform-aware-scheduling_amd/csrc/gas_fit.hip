@@ -43,6 +43,9 @@ constexpr int kTpb = 256;
 constexpr int kPrepTpb = 64;  // pods per prep block: small blocks spread the pods over the CUs
 constexpr int kMaxCards = PAS_GAS_PACKED;  // cards of a fast-path node, in registers
 constexpr int kPacked = PAS_GAS_PACKED;    // selections of a fast-path pod
+// Multi-selection pods are listed by class: S = 2, S = 3, S >= 4 (each class has its own
+// loop in the multi kernel, so no per-pod dispatch on S).
+constexpr int kClasses = 3;
 
 // A (pod, container) step, in compare form: cmp[q] = per-GPU need of a requested kind
 // (getPerGPUResourceRequest :180-190), INT64_MIN for the others, so every card passes them
@@ -163,11 +166,11 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
 
 // One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
 // list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
-// [n_res + 1][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list); a multi
-// pod's selections (containers in order, then gpuNum) go to the row sels[list][slot][8] of
-// its list position.  More
+// [n_res + 1][kClasses][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list
+// and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
+// go to the row sels[list][slot][8] of its list position.  More
 // than PAS_GAS_MAX_SELECTIONS selections are beyond the packed result and keep only the
-// count.  counts: [n_res + 1] single lists, then [n_res + 1] multi lists.
+// count.  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
 __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
                                 int32_t i915, const int64_t* __restrict__ req,
                                 const uint32_t* __restrict__ mask,
@@ -218,19 +221,20 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0)
                             : multi_skip_list(n_res, skip_ok, skip_req);
   const int32_t nl = n_res + 1;
-  const int32_t slot = wave_slot(counts, one_sel ? l : nl + l);
+  const int32_t ml = l * kClasses + (steps == 2 ? 0 : steps == 3 ? 1 : 2);  // multi list
+  const int32_t slot = wave_slot(counts, one_sel ? l : nl + ml);
   if (one_sel) {
     one.word = p | (steps << 24) | (one_bad ? kBadPod : 0);
     single[(int64_t)l * n_pods + slot] = one;
     return;
   }
   if (steps > kPacked) {  // gas_fit_generic_kernel; the fast kernel writes 0 first
-    multi[(int64_t)l * n_pods + slot] = p | ((kPacked + 1) << 24);
+    multi[(int64_t)ml * n_pods + slot] = p | ((kPacked + 1) << 24);
     big_pods[atomicAdd(n_big_pods, 1)] = p;
     return;
   }
   // the pod's row sits at its list position, so a batch of a list is one contiguous copy
-  GasSel* out = sels + ((int64_t)l * n_pods + slot) * kPacked;
+  GasSel* out = sels + ((int64_t)ml * n_pods + slot) * kPacked;
   int32_t k = 0, bad = 0;
   // the first three selections in named registers (a runtime-indexed array would live in
   // scratch memory)
@@ -310,7 +314,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
     if (steps == 3 && same(3, 1)) t.over |= 1 << 10;
     *reinterpret_cast<GasThresholds*>(out + kThRow) = t;
   }
-  multi[(int64_t)l * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
+  multi[(int64_t)ml * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
 }
 
 // gflip[q] = INT64_MAX - gmin[q] (kept flipped so that a zeroed buffer is the identity of the
@@ -956,10 +960,6 @@ __device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards]
 // and the take lowers cur of every s with c_s = c_t (a card first taken reads its snapshot
 // free from the lane's LDS copy).  Registers only, unrolled over t; a selection whose need
 // equals the previous one's reuses its mask (the selections of one container are identical).
-#ifndef PAS_GAS_SEQ_FROM
-#define PAS_GAS_SEQ_FROM 4  // pods with at least this many selections take this path
-#endif
-constexpr int kSeqFrom = PAS_GAS_SEQ_FROM;
 
 __device__ __forceinline__ bool uniform_eq(int64_t a, int64_t b) {
   const uint64_t x = (uint64_t)a ^ (uint64_t)b;
@@ -1041,7 +1041,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
 // the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
 // reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
 // waiting for its copy does not hold up the other waves of the block.
-template <int Q, int SKIP, bool kBits>
+template <int Q, int SKIP, int kCls, bool kBits>
 __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
                                            int32_t* stage_w, int64_t* tab_base, uint32_t node_ok,
                                            int32_t N, int32_t n, bool valid,
@@ -1093,15 +1093,17 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
         const GasThresholds& th = *reinterpret_cast<const GasThresholds*>(rec + kThRow);
-        if (S <= (kSeqFrom <= 3 ? kSeqFrom - 1 : 3) && kGather)
-          out = S == 2 ? multi_closed_g<Q, SKIP, kC, 2>(free, th, live, node_ok, tab, lane)
-                       : multi_closed_g<Q, SKIP, kC, 3>(free, th, live, node_ok, tab, lane);
-        else if (S <= 3 && !kGather)
-          out = multi_closed<Q, SKIP>(free, th, S, live, node_ok);
-        else if (S <= kPacked && kGather && S >= kSeqFrom)
-          out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane);
-        else if (S <= kPacked)
-          out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
+        if constexpr (kCls < 2) {  // S = 2 or 3: closed form
+          if constexpr (kGather)
+            out = multi_closed_g<Q, SKIP, kC, 2 + kCls>(free, th, live, node_ok, tab, lane);
+          else
+            out = multi_closed<Q, SKIP>(free, th, 2 + kCls, live, node_ok);
+        } else if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
+          if constexpr (kGather)
+            out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane);
+          else
+            out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
+        }
       }
       put_result<kBits>(res, fit, pod, N, n, valid, out);
     }
@@ -1118,10 +1120,10 @@ __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q],
                                             const int32_t* __restrict__ counts,
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
-  multi_list<Q, L - 1, kBits>(free, stage, stage_w, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
-                              sels + (int64_t)L * P * kPacked, counts + L, bt,
-                              res, fit);
-  if constexpr (L < Q)
+  multi_list<Q, L / kClasses - 1, L % kClasses, kBits>(
+      free, stage, stage_w, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
+      sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
+  if constexpr (L + 1 < (Q + 1) * kClasses)
     multi_lists<Q, kBits, L + 1>(free, stage, stage_w, tab, node_ok, N, n, valid, P, multi, sels,
                                  counts, bt, res, fit);
 }
@@ -1308,19 +1310,19 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     PAS_HIP(ctx, hipEventRecord(ctx->gas_limit_ev, s));
     return PAS_OK;
   }
-  // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][P] | their
-  // selection rows [Q+1][P][8] | the generic path's pods [P] and per-pod selection counts
-  // [P] | list counts [2(Q+1)] and the generic pod count (zeroed together).  The flipped
+  // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][3][P] |
+  // their selection rows [Q+1][3][P][8] | the generic path's pods [P] and per-pod selection
+  // counts [P] | list counts [Q+1] + [(Q+1)3] and the generic pod count (zeroed together).  The flipped
   // kind minima and the generic path's nodes depend on the snapshot alone: they sit in
   // g.derived and are recomputed only after the snapshot changed.
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   const int32_t NL = Q + 1;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   const size_t b_single = al(sizeof(GasSingle) * (size_t)NL * n_pods);
-  const size_t b_multi = al(sizeof(int32_t) * (size_t)NL * n_pods);
-  const size_t b_sels = al(sizeof(GasSel) * kPacked * (size_t)NL * n_pods);
+  const size_t b_multi = al(sizeof(int32_t) * (size_t)NL * kClasses * n_pods);
+  const size_t b_sels = al(sizeof(GasSel) * kPacked * (size_t)NL * kClasses * n_pods);
   const size_t b_pods = al(sizeof(int32_t) * (size_t)n_pods);
-  constexpr size_t b_tail = (2 * (PAS_GAS_MAX_RES + 1) + 1) * sizeof(int32_t);
+  constexpr size_t b_tail = ((1 + kClasses) * (PAS_GAS_MAX_RES + 1) + 1) * sizeof(int32_t);
   const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_tail;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
@@ -1344,7 +1346,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   int32_t* pod_steps = reinterpret_cast<int32_t*>(base);
   base += b_pods;
   int32_t* counts = reinterpret_cast<int32_t*>(base);
-  int32_t* n_big_pods = counts + 2 * (PAS_GAS_MAX_RES + 1);
+  int32_t* n_big_pods = counts + (1 + kClasses) * (PAS_GAS_MAX_RES + 1);
   unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
   int32_t* n_big_nodes = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
   int32_t* big_nodes = reinterpret_cast<int32_t*>(static_cast<char*>(g.derived) + 64);
