@@ -12,6 +12,6 @@ done
 for i in $(seq "$N"); do
   for T in "${trees[@]}"; do
     timeout -k 10 150 python3 "$T/bench.py" $A --no-cpu-baseline --no-request-latency > /tmp/ab_out.json 2>/tmp/ab_err.log || { cat /tmp/ab_err.log; exit 1; }
-    tail -1 /tmp/ab_out.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$(basename $T)', round(d['ms_per_step'],4), round(d['roofline']['kernel_ms'],4), round(d['roofline']['frac'],4))"
+    tail -1 /tmp/ab_out.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); r=d.get('roofline') or {}; print('$(basename $T)', round(d['ms_per_step'],4), round(r.get('kernel_ms',0),4), round(r.get('frac',0),4), {k: round(v,3) for k,v in (d['config'].get('kernel_ms_per_step') or {}).items()})"
   done
 done
