@@ -392,6 +392,23 @@ __device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
   return chosen;
 }
 
+// Whether any card passes: the fit bit alone (bitmap outputs), no card order needed, so the
+// per-card lane masks are or-ed in SALU instead of selecting a card per lane.
+template <int Q, int SKIP>
+__device__ __forceinline__ bool any_fit(const int64_t (&free)[kMaxCards][Q],
+                                        const int64_t (&cmp)[Q]) {
+  bool any = false;
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k) {
+    bool ok = true;
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (q != SKIP) ok &= cmp[q] <= free[k][q];
+    any |= ok;
+  }
+  return any;
+}
+
 // One (pod, node) result: the packed word, or (kBits) the fit bit in the pod's row of a
 // node bitmap, written per 64-node word by lane 0 of the wave (waves cover aligned
 // 64-node ranges).
@@ -497,8 +514,12 @@ __device__ __forceinline__ void single_list(const int64_t (&free)[kMaxCards][Q],
       const int64_t pod = w & 0xFFFFFF;
       uint32_t out = node_ok;
       if (((w >> 24) & 0xF) == 1) {
-        const int k = (w & kBadPod) ? -1 : first_fit<Q, SKIP>(free, cmp);
-        out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
+        if constexpr (kBits) {
+          out = (!(w & kBadPod) && any_fit<Q, SKIP>(free, cmp)) ? node_ok : 0u;
+        } else {
+          const int k = (w & kBadPod) ? -1 : first_fit<Q, SKIP>(free, cmp);
+          out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
+        }
       }
       put_result<kBits>(res, fit, pod, N, n, valid, out);
 #pragma unroll
