@@ -40,6 +40,12 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+#ifndef PAS_GAS_BLOCKS_SINGLE
+#define PAS_GAS_BLOCKS_SINGLE 8192  // target blocks of a fit grid: (node block, pod chunk) pairs
+#endif
+#ifndef PAS_GAS_BLOCKS_MULTI
+#define PAS_GAS_BLOCKS_MULTI 8192
+#endif
 constexpr int kPrepTpb = 64;  // pods per prep block: small blocks spread the pods over the CUs
 constexpr int kMaxCards = PAS_GAS_PACKED;  // cards of a fast-path node, in registers
 constexpr int kPacked = PAS_GAS_PACKED;    // selections of a fast-path pod
@@ -1388,7 +1394,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   // grids: (node block, pod chunk) pairs, ~4096 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
   const int32_t nb_s = (N + kTpb - 1) / kTpb;
-  const int32_t ch_s = std::max(1, std::min(n_pods, (4096 + nb_s - 1) / nb_s));
+  const int32_t ch_s = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_SINGLE + nb_s - 1) / nb_s));
+  const int32_t ch_m = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_s - 1) / nb_s));
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
   switch (Q * 2 + (bits ? 1 : 0)) {
@@ -1396,8 +1403,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   case QQ * 2 + B:                                                                             \
     gas_fit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                 \
         N, K, n_pods, g.n_cards, g.cap, g.used, single, counts, ch_s, d_res, d_fit);           \
-    gas_fit_multi_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                  \
-        N, K, n_pods, g.n_cards, g.cap, g.used, multi, sels, counts + NL, ch_s, d_res, d_fit); \
+    gas_fit_multi_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                  \
+        N, K, n_pods, g.n_cards, g.cap, g.used, multi, sels, counts + NL, ch_m, d_res, d_fit); \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
