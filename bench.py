@@ -394,6 +394,18 @@ def bench_gas(args, world, rank):
                      "traffic": load_traffic("gas_fit_kernel"), "algorithmic_bytes": alg_bytes,
                      "kernel_ms": kernel_s * 1e3},
     }
+    # The fit kernels are bound by VALU issue, not by HBM: their VALU
+    # wave-instructions per step (SQ_INSTS_VALU, committed PMC pass) over the same GPU time,
+    # against the chip's issue peak: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU
+    # instruction (scripts/diag/issue_rates.hip measures 4.3 for this mix).
+    valu = load_traffic("gas_fit_valu_per_step")
+    if valu:
+        peak = 1024 * 2.4e9 / 4
+        out["issue_roofline"] = {
+            "bound": "valu_issue", "unit": "wave-instructions/s", "achieved": valu / kernel_s,
+            "peak": peak, "frac": valu / kernel_s / peak, "valu_per_step": valu,
+            "salu_per_step": load_traffic("gas_fit_salu_per_step"),
+            "source": "profiles/traffic.json (rocprofv3 --pmc SQ_INSTS_VALU, fit kernels)"}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle

@@ -95,6 +95,14 @@ def main():
             traffic["gas_fit_kernel"] = round(sum(hbm(k) * wt[k] for k in GAS_PATH))
             traffic["gas_fit_by_kernel"] = {k: round(hbm(k)) for k in GAS_PATH}
             traffic["gas_fit_launches_per_step"] = {k: round(wt[k], 4) for k in GAS_PATH}
+            # VALU wave-instructions per step (the fit kernels are issue-bound, not HBM-bound)
+            if any(p.get((k, "SQ_INSTS_VALU")) for k in GAS_PATH):
+                traffic["gas_fit_valu_per_step"] = round(
+                    sum(p.get((k, "SQ_INSTS_VALU"), 0) * wt[k] for k in GAS_PATH))
+                traffic["gas_fit_salu_per_step"] = round(
+                    sum(p.get((k, "SQ_INSTS_SALU"), 0) * wt[k] for k in GAS_PATH))
+                traffic["gas_fit_valu_by_kernel"] = {
+                    k: round(p.get((k, "SQ_INSTS_VALU"), 0)) for k in GAS_PATH}
         elif w == "deschedule":
             # the sweep kernel (tas_violations_run_kernel since round 2), under the bench's key
             traffic["tas_violations_kernel"] = round(hbm("tas_violations_run_kernel") or
@@ -104,7 +112,8 @@ def main():
             traffic["c5_by_kernel"] = {k: round(hbm(k)) for k in kernels}
         print(w, "->", [r["kernel"] + f" {r['avg_us']:.1f}us x{r['calls']}" for r in rows[:8]])
     traffic["_source"] = (f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, round {rnd}; "
-                          "bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB->B)")
+                          "bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KB->B); "
+                          "gas_fit_valu/salu_per_step: SQ_INSTS_VALU / SQ_INSTS_SALU pass")
     with open(tpath, "w") as f:
         json.dump(traffic, f, indent=1)
     print(json.dumps(traffic, indent=1))
