@@ -872,7 +872,9 @@ __device__ __forceinline__ bool th_fits(const int64_t* th, const int64_t (&g)[kC
 // two fit masks instead of three, S = 3 three instead of seven.
 // kOvf: some threshold of the pod overflows (over bits 0-6).  Such pods are rare, so the
 // common instantiation drops every overflow test.
-template <int Q, int SKIP, int kC, int S, bool kOvf>
+// kSame: 1 / 0 = the first two selections ask the same / not (one mask or two), -1 = read it
+// from over bit 8 (the rare overflow instantiation).
+template <int Q, int SKIP, int kC, int S, bool kOvf, int kSame>
 __device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards][Q],
                                                 const GasThresholds& t, int32_t over,
                                                 uint64_t live, uint32_t node_ok,
@@ -884,7 +886,7 @@ __device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards]
 #pragma unroll
     for (int q = 0; q < Q; ++q) th[j][q] = j < 3 || S == 3 ? t.th[j][q] : 0;
   uint32_t m0, m1, m3 = 0u;
-  if (over & (1 << 8)) {  // the first two selections ask the same: one mask
+  if (kSame == 1 || (kSame < 0 && (over & (1 << 8)))) {  // the first two ask the same: one mask
     m0 = th_mask<Q, SKIP>(free, th[0], live);
     m1 = m0;
   } else {
@@ -898,7 +900,9 @@ __device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards]
   if (ov(1)) m0 = 0u;  // an overflowing threshold passes no card
   if (ov(2)) m1 = 0u;
   if (ov(8)) m3 = 0u;
-  const uint32_t c0 = lowest(m0);
+  // card indices with "none" = 8: bit 8 as a sentinel under every 8-card mask, so the
+  // lowest set bit needs no zero test; 8 fails every `< 8` below and clears only bit 8
+  const uint32_t c0 = (uint32_t)__builtin_ctz(m0 | 0x100u);
   int64_t g0[kC];
   {
     const int64_t* p = tab.at(min(c0, 7u), lane);
@@ -906,9 +910,10 @@ __device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards]
     for (int j = 0; j < kC; ++j) g0[j] = p[j];
   }
   const bool b2 = !ov(4) && th_fits<Q, SKIP, kC>(th[2], g0);
-  const uint32_t c1 = min(lowest(m1 & ~(1u << c0)), (c0 < 8u && b2) ? c0 : 8u);
+  const uint32_t u1 = (uint32_t)__builtin_ctz((m1 & ~(1u << c0)) | 0x100u);
+  const uint32_t c1 = b2 ? min(u1, c0) : u1;
   uint32_t word = c0 | (c1 << 3);
-  bool fits = c0 < 8u && c1 < 8u;
+  uint32_t any = c0 | c1;  // >= 8 when a selection found no card
   if (S == 3) {
     int64_t g1[kC];
     const int64_t* p = tab.at(min(c1, 7u), lane);
@@ -922,12 +927,13 @@ __device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards]
       const uint32_t t5 = (!ov(32) && th_fits<Q, SKIP, kC>(th[5], g1)) ? c1 : 8u;
       touched = min(t4, t5);
     }
-    const uint32_t untouched = lowest(m3 & ~(1u << c0) & ~(1u << c1));
+    const uint32_t untouched =
+        (uint32_t)__builtin_ctz((m3 & ~(1u << c0) & ~(1u << c1)) | 0x100u);
     const uint32_t c2 = min(untouched, touched);
-    fits = fits && c2 < 8u;
+    any |= c2;
     word |= c2 << 6;
   }
-  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+  return any < 8u ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
 }
 
 template <int Q, int SKIP, int kC, int S>
@@ -937,8 +943,10 @@ __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCar
                                                    int lane) {
   const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
   if (over & 0x7F)
-    return closed_body<Q, SKIP, kC, S, true>(free, t, over, live, node_ok, tab, lane);
-  return closed_body<Q, SKIP, kC, S, false>(free, t, over, live, node_ok, tab, lane);
+    return closed_body<Q, SKIP, kC, S, true, -1>(free, t, over, live, node_ok, tab, lane);
+  if (over & (1 << 8))
+    return closed_body<Q, SKIP, kC, S, false, 1>(free, t, over, live, node_ok, tab, lane);
+  return closed_body<Q, SKIP, kC, S, false, 0>(free, t, over, live, node_ok, tab, lane);
 }
 
 // A pod with 4 to 8 selections: the selections in order on a working copy of the free values
