@@ -996,17 +996,11 @@ __device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards]
 // free from the lane's LDS copy).  Registers only, unrolled over t; a selection whose need
 // equals the previous one's reuses its mask (the selections of one container are identical).
 
-__device__ __forceinline__ bool uniform_eq(int64_t a, int64_t b) {
-  const uint64_t x = (uint64_t)a ^ (uint64_t)b;
-  return (__builtin_amdgcn_readfirstlane((uint32_t)x) |
-          __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32))) == 0u;
-}
-
 template <int Q, int SKIP, int kC>
 __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q],
                                               const GasSel* rec, int32_t S, uint64_t live,
                                               uint32_t node_ok, const FreeTab<kC>& tab,
-                                              int lane) {
+                                              int lane, uint32_t same_row) {
   typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
   int64_t fr[kMaxCards][kC];
 #pragma unroll
@@ -1030,9 +1024,8 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
         need[j] = ct.x;
         neg[j++] = ct.y;
       }
-    bool same = t > 0;
-#pragma unroll
-    for (int j = 0; j < kC; ++j) same = same && uniform_eq(need[j], prev[j]);
+    // same_row: nibble t all ones = selection t's record equals selection t - 1's
+    const bool same = t > 0 && ((same_row >> (4 * t)) & 0xFu) == 0xFu;
     if (!same) m = fit_mask<kC>(need, fr, live);
     uint32_t bad = 0u;
 #pragma unroll
@@ -1116,6 +1109,16 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
 #pragma unroll
     for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
     if (lane < nb) stage_w[lane] = wd;
+    // for the sequential class: which selections repeat the previous one, for the whole batch
+    // in one ballot (lane l holds 16-B piece l % 4 of selection (l % 32) / 4 of row l / 32)
+    uint64_t same_m = 0;
+    if constexpr (kCls == 2) {
+      static_assert(kIters == 1 && kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "pieces");
+      const int4 u = v[0];
+      const int ux = __shfl_up(u.x, 4, 64), uy = __shfl_up(u.y, 4, 64);
+      const int uz = __shfl_up(u.z, 4, 64), uw = __shfl_up(u.w, 4, 64);
+      same_m = __ballot((lane & 31) >= 4 && u.x == ux && u.y == uy && u.z == uz && u.w == uw);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -1135,7 +1138,8 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
             out = multi_closed<Q, SKIP>(free, th, 2 + kCls, live, node_ok);
         } else if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
           if constexpr (kGather)
-            out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane);
+            out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane,
+                                         (uint32_t)(same_m >> (32 * j)));
           else
             out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
         }
