@@ -723,6 +723,10 @@ __device__ __forceinline__ uint32_t fit_mask(const int64_t (&need)[C],
 
 constexpr int kMB = 2;  // multi-selection pods staged in LDS per round and wave (LDS: 4 workgroups per CU)
 constexpr int kRowChunks = kPacked * (int)sizeof(GasSel) / 16;  // 16-B chunks per row
+// the 16-B piece of a row whose first dword is GasThresholds::over
+constexpr int kOverPiece =
+    (kThRow * (int)sizeof(GasSel) + (int)offsetof(GasThresholds, over)) / 16;
+static_assert((kThRow * sizeof(GasSel) + offsetof(GasThresholds, over)) % 16 == 0, "over");
 
 // Fit mask of the compared kinds (all but SKIP) of a threshold row: bit k = card k's snapshot
 // free passes every compared threshold.
@@ -938,10 +942,9 @@ __device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards]
 
 template <int Q, int SKIP, int kC, int S>
 __device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCards][Q],
-                                                   const GasThresholds& t, uint64_t live,
-                                                   uint32_t node_ok, const FreeTab<kC>& tab,
-                                                   int lane) {
-  const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
+                                                   const GasThresholds& t, int32_t over,
+                                                   uint64_t live, uint32_t node_ok,
+                                                   const FreeTab<kC>& tab, int lane) {
   if (over & 0x7F)
     return closed_body<Q, SKIP, kC, S, true, -1>(free, t, over, live, node_ok, tab, lane);
   if (over & (1 << 8))
@@ -1122,9 +1125,13 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    // the batch's pod words and threshold flags straight from the staging registers (lane j:
+    // pod j's word; the flags word sits in piece kOverPiece of its row), not read back from LDS
+    static_assert(kIters == 1, "one staging register per lane");
+    const int32_t wcur = wd, vcur = v[0].x;
     load_batch(b0 + kMB);
     for (int32_t j = 0; j < nb; ++j) {
-      const int32_t pw = __builtin_amdgcn_readfirstlane(stage_w[j]);
+      const int32_t pw = __builtin_amdgcn_readlane(wcur, j);
       const int32_t pod = pw & 0xFFFFFF;
       const int32_t S = (pw >> 24) & 0xF;
       const GasSel* rec = stage + j * kPacked;
@@ -1133,7 +1140,9 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
         const GasThresholds& th = *reinterpret_cast<const GasThresholds*>(rec + kThRow);
         if constexpr (kCls < 2) {  // S = 2 or 3: closed form
           if constexpr (kGather)
-            out = multi_closed_g<Q, SKIP, kC, 2 + kCls>(free, th, live, node_ok, tab, lane);
+            out = multi_closed_g<Q, SKIP, kC, 2 + kCls>(
+                free, th, __builtin_amdgcn_readlane(vcur, j * kRowChunks + kOverPiece), live,
+                node_ok, tab, lane);
           else
             out = multi_closed<Q, SKIP>(free, th, 2 + kCls, live, node_ok);
         } else if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
