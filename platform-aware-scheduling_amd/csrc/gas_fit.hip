@@ -97,14 +97,25 @@ struct alignas(16) GasSingle {
 
 // getPerGPUResourceRequest: copy the container's map and, when numI915 > 1, divide
 // every entry (the i915 entry included) by numI915, truncating (resource_map.go:129-145).
-__device__ GasStep container_step(int64_t i, int32_t n_res, int32_t i915,
-                                  const int64_t* __restrict__ req,
-                                  const uint32_t* __restrict__ mask) {
-  // every load unconditional (clamped to the row), so the mask and values arrive together
-  const uint32_t m = mask[i];
+// A container's request row: mask and values, every load unconditional (clamped to the row),
+// so they arrive together.
+struct ContainerReq {
+  uint32_t m;
   int64_t rv[PAS_GAS_MAX_RES];
+};
+__device__ __forceinline__ ContainerReq load_container(int64_t i, int32_t n_res,
+                                                       const int64_t* __restrict__ req,
+                                                       const uint32_t* __restrict__ mask) {
+  ContainerReq c;
+  c.m = mask[i];
 #pragma unroll
-  for (int q = 0; q < PAS_GAS_MAX_RES; ++q) rv[q] = req[i * n_res + min(q, n_res - 1)];
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q) c.rv[q] = req[i * n_res + min(q, n_res - 1)];
+  return c;
+}
+
+__device__ GasStep container_step(const ContainerReq& cr, int32_t n_res, int32_t i915) {
+  const uint32_t m = cr.m;
+  const int64_t(&rv)[PAS_GAS_MAX_RES] = cr.rv;
   int64_t ni = 0;
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q)
@@ -190,6 +201,21 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   if (p >= n_pods) return;
   const int32_t nc = min(max(n_containers[p], 0), max_containers);
   const int64_t row = (int64_t)p * max_containers;
+  // the first kPre containers' requests loaded at once (one memory latency, not one per
+  // container and pass); containers past them are loaded when reached
+  constexpr int kPre = 4;
+  ContainerReq pre[kPre] = {};
+  if (nc > 0) {
+#pragma unroll
+    for (int c = 0; c < kPre; ++c) pre[c] = load_container(row + min(c, nc - 1), n_res, req, mask);
+  }
+  auto container = [&](int32_t c) {
+    ContainerReq cr = pre[0];
+#pragma unroll
+    for (int k = 1; k < kPre; ++k) cr = c == k ? pre[k] : cr;
+    if (c >= kPre) cr = load_container(row + c, n_res, req, mask);
+    return container_step(cr, n_res, i915);
+  };
   int32_t steps = 0;
   uint32_t kinds = 0;
   uint32_t skip_ok = (1u << n_res) - 1u, skip_req = 0;  // multi_skip_list
@@ -197,7 +223,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   GasSingle one = {};
   int32_t one_bad = 0;
   for (int32_t c = 0; c < nc; ++c) {
-    const GasStep g = container_step(row + c, n_res, i915, req, mask);
+    const GasStep g = container(c);
     if (g.num_i915 > 0) {
       if (steps == 0) {
 #pragma unroll
@@ -249,7 +275,7 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) cmp0[q] = cmp1[q] = cmp2[q] = take0[q] = take1[q] = 0;
   for (int32_t c = 0; c < nc; ++c) {
-    const GasStep g = container_step(row + c, n_res, i915, req, mask);
+    const GasStep g = container(c);
     bad |= g.num_i915 > 0 ? g.bad : 0;
     for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
 #pragma unroll
