@@ -1041,7 +1041,6 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
   uint32_t cs[kPacked];
   uint32_t word = 0u, m = 0u;
   bool fits = true;
-  int64_t prev[kC];
 #pragma unroll
   for (int t = 0; t < kPacked; ++t) {
     if (t >= S) break;
@@ -1073,20 +1072,19 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
 #pragma unroll
       for (int j = 0; j < kC; ++j) g[j] = p[j];
     }
+    // one valid entry per card: the newest take's; the entry it replaces is marked stale
+    // (card 9, outside every 8-card mask) instead of being rewritten
 #pragma unroll
-    for (int s2 = 0; s2 < t; ++s2)
+    for (int s2 = 0; s2 < t; ++s2) {
+      const bool e = cs[s2] == c;
 #pragma unroll
-      for (int j = 0; j < kC; ++j) g[j] = cs[s2] == c ? cur[s2][j] : g[j];
-#pragma unroll
-    for (int j = 0; j < kC; ++j) g[j] += neg[j];
-#pragma unroll
-    for (int s2 = 0; s2 < t; ++s2)
-#pragma unroll
-      for (int j = 0; j < kC; ++j) cur[s2][j] = cs[s2] == c ? g[j] : cur[s2][j];
+      for (int j = 0; j < kC; ++j) g[j] = e ? cur[s2][j] : g[j];
+      cs[s2] = e ? 9u : cs[s2];
+    }
 #pragma unroll
     for (int j = 0; j < kC; ++j) {
+      g[j] += neg[j];
       cur[t][j] = g[j];
-      prev[j] = need[j];
     }
     cs[t] = c;
     word |= (c & 7u) << (3 * t);
