@@ -1038,7 +1038,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
     for (int q = 0, j = 0; q < Q; ++q)
       if (q != SKIP) fr[k][j++] = free[k][q];
   int64_t cur[kPacked][kC];
-  uint32_t cs[kPacked];
+  uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot (0: stale)
   uint32_t word = 0u, m = 0u;
   bool fits = true;
 #pragma unroll
@@ -1061,7 +1061,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
       bool ok = true;
 #pragma unroll
       for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[s2][j];
-      bad |= ok ? 0u : (1u << cs[s2]);
+      bad |= ok ? 0u : cb[s2];
     }
     const uint32_t c = lowest(m & ~bad);
     fits = fits && c < 8u;
@@ -1073,20 +1073,21 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
       for (int j = 0; j < kC; ++j) g[j] = p[j];
     }
     // one valid entry per card: the newest take's; the entry it replaces is marked stale
-    // (card 9, outside every 8-card mask) instead of being rewritten
+    // (no card bit) instead of being rewritten
+    const uint32_t bc = 1u << c;  // c = 8 (no card): bit 8, outside every 8-card mask
 #pragma unroll
     for (int s2 = 0; s2 < t; ++s2) {
-      const bool e = cs[s2] == c;
+      const bool e = cb[s2] == bc;
 #pragma unroll
       for (int j = 0; j < kC; ++j) g[j] = e ? cur[s2][j] : g[j];
-      cs[s2] = e ? 9u : cs[s2];
+      cb[s2] = e ? 0u : cb[s2];
     }
 #pragma unroll
     for (int j = 0; j < kC; ++j) {
       g[j] += neg[j];
       cur[t][j] = g[j];
     }
-    cs[t] = c;
+    cb[t] = bc;
     word |= (c & 7u) << (3 * t);
   }
   return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
