@@ -1099,7 +1099,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
 // waiting for its copy does not hold up the other waves of the block.
 template <int Q, int SKIP, int kCls, bool kBits>
 __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                           int32_t* stage_w, int64_t* tab_base, uint32_t node_ok,
+                                           int64_t* tab_base, uint32_t node_ok,
                                            int32_t N, int32_t n, bool valid,
                                            const int32_t* __restrict__ list,
                                            const GasSel* __restrict__ sels,
@@ -1136,7 +1136,6 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
     __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
 #pragma unroll
     for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
-    if (lane < nb) stage_w[lane] = wd;
     // for the sequential class: which selections repeat the previous one, for the whole batch
     // in one ballot (lane l holds 16-B piece l % 4 of selection (l % 32) / 4 of row l / 32)
     uint64_t same_m = 0;
@@ -1185,7 +1184,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
 
 template <int Q, bool kBits, int L = 0>
 __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                            int32_t* stage_w, int64_t* tab, uint32_t node_ok,
+                                            int64_t* tab, uint32_t node_ok,
                                             int32_t N,
                                             int32_t n, bool valid, int32_t P,
                                             const int32_t* __restrict__ multi,
@@ -1194,10 +1193,10 @@ __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q],
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
   multi_list<Q, L / kClasses - 1, L % kClasses, kBits>(
-      free, stage, stage_w, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
+      free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
       sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
   if constexpr (L + 1 < (Q + 1) * kClasses)
-    multi_lists<Q, kBits, L + 1>(free, stage, stage_w, tab, node_ok, N, n, valid, P, multi, sels,
+    multi_lists<Q, kBits, L + 1>(free, stage, tab, node_ok, N, n, valid, P, multi, sels,
                                  counts, bt, res, fit);
 }
 
@@ -1209,7 +1208,6 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
     uint64_t* __restrict__ fit) {
   __shared__ GasSel stage[kTpb / 64][kPacked * kMB];  // a slice per wave
-  __shared__ int32_t stage_w[kTpb / 64][kMB];
   constexpr int kC = Q > 1 ? Q - 1 : 1;
   __shared__ int64_t tab[kTpb / 64][kMaxCards * 64 * kC];  // FreeTab per wave
   const BlockTile bt = block_tile(chunks);
@@ -1221,7 +1219,7 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  multi_lists<Q, kBits>(free, stage[wave], stage_w[wave], tab[wave], node_ok, N, n, valid, P,
+  multi_lists<Q, kBits>(free, stage[wave], tab[wave], node_ok, N, n, valid, P,
                         multi, sels, counts, bt, res, fit);
 }
 
