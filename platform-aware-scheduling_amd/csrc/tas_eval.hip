@@ -164,11 +164,15 @@ __device__ void ranges_group(const RangesParams& R, int32_t r) {
       const int64_t* f2 = R.f32 + (int64_t)m * (R.R >> 5);
       const int32_t na = (c + 1023) >> 10, nb = (c + 31) >> 5;
       int32_t n1l = 0, n1u = 0;  // fences (1024 apart) below the target
-      for (int32_t i0 = 0; i0 < na; i0 += 4 * kRuleLanes) {
-        int32_t a, b;
-        count_below<4>(f1 + i0, na - i0, f1 + i0, na - i0, t, gl, gmask, &a, &b);
-        n1l += a;
-        n1u += b;
+      if (na <= 16 * kRuleLanes) {  // up to 131 072 nodes: every fence load in flight at once
+        count_below<16>(f1, na, f1, na, t, gl, gmask, &n1l, &n1u);
+      } else {
+        for (int32_t i0 = 0; i0 < na; i0 += 4 * kRuleLanes) {
+          int32_t a, b;
+          count_below<4>(f1 + i0, na - i0, f1 + i0, na - i0, t, gl, gmask, &a, &b);
+          n1l += a;
+          n1u += b;
+        }
       }
       // 1024-blocks holding each bound (sorted[1024 b1] is below; block 0 if none is)
       const int32_t b1l = max(n1l - 1, 0), b1u = max(n1u - 1, 0);
@@ -215,6 +219,41 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
   const bool prio = (g.flags & PAS_TAS_PRIORITIZE) != 0 && g.M > 0;
   for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
   __syncthreads();
+  const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
+  if (g.P > 0 && g.P <= kGroupTpb * kGU) {
+    // one round: every load of the pods (prioritize rule, rule offsets) in flight together,
+    // the keys kept in registers between the histogram and the scatter
+    pas_rule r[kGU];
+    int32_t c[kGU], r0[kGU], r1[kGU], key[kGU];
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int32_t pc = min(tid + u * kGroupTpb, g.P - 1);
+      r[u] = prio ? g.prio[pc] : pas_rule{-1, 0, 0};
+      r0[u] = filt ? g.rule_off[pc] : 0;
+      r1[u] = filt ? g.rule_off[pc + 1] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) c[u] = prio ? g.cnt[min(max(r[u].metric, 0), g.M - 1)] : 0;
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const bool listed = prio && r[u].metric >= 0 && r[u].metric < g.M && c[u] > 0;
+      key[u] = listed ? order_of(r[u].op) * g.M + r[u].metric : G;
+      c[u] = listed ? c[u] : 0;
+      if (tid + u * kGroupTpb < g.P) atomicAdd(&hist[key[u]], 1);
+    }
+    __syncthreads();
+    block_exclusive_scan(hist, G + 1);
+#pragma unroll
+    for (int u = 0; u < kGU; ++u) {
+      const int32_t p = tid + u * kGroupTpb;
+      if (p >= g.P) continue;
+      int32_t pos = atomicAdd(&hist[key[u]], 1);  // order inside a bucket is free
+      if (g.no_group) pos = p;
+      g.desc[2 * pos] = make_int4(p, key[u] < G ? key[u] : -1, c[u], 0);
+      g.desc[2 * pos + 1] = make_int4(r0[u], r1[u], 0, 0);
+    }
+    return;
+  }
   for (int32_t p0 = tid; p0 < g.P; p0 += kGroupTpb * kGU) {
     pas_rule r[kGU];
     int32_t c[kGU];
@@ -242,7 +281,6 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
   }
   __syncthreads();
   block_exclusive_scan(hist, G + 1);
-  const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
   for (int32_t p0 = tid; p0 < g.P; p0 += kGroupTpb * kGU) {
     int2 kc[kGU];
     int32_t r0[kGU], r1[kGU];
