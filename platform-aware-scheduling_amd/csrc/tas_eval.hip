@@ -218,11 +218,12 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
   const int tid = threadIdx.x;
   const bool prio = (g.flags & PAS_TAS_PRIORITIZE) != 0 && g.M > 0;
   for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
-  __syncthreads();
   const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
-  if (g.P > 0 && g.P <= kGroupTpb * kGU) {
+  if (g.P > 0 && g.P <= kGroupTpb * kGU && g.M <= kGroupTpb) {
     // one round: every load of the pods (prioritize rule, rule offsets) in flight together,
     // the keys kept in registers between the histogram and the scatter
+    // the per-metric node counts staged in LDS (after the histogram) with the same round
+    int32_t* cnt = sh + G + 1;
     pas_rule r[kGU];
     int32_t c[kGU], r0[kGU], r1[kGU], key[kGU];
 #pragma unroll
@@ -232,8 +233,10 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
       r0[u] = filt ? g.rule_off[pc] : 0;
       r1[u] = filt ? g.rule_off[pc + 1] : 0;
     }
+    if (tid < g.M) cnt[tid] = g.cnt[tid];
+    __syncthreads();
 #pragma unroll
-    for (int u = 0; u < kGU; ++u) c[u] = prio ? g.cnt[min(max(r[u].metric, 0), g.M - 1)] : 0;
+    for (int u = 0; u < kGU; ++u) c[u] = prio ? cnt[min(max(r[u].metric, 0), g.M - 1)] : 0;
 #pragma unroll
     for (int u = 0; u < kGU; ++u) {
       const bool listed = prio && r[u].metric >= 0 && r[u].metric < g.M && c[u] > 0;
@@ -254,6 +257,7 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
     }
     return;
   }
+  __syncthreads();
   for (int32_t p0 = tid; p0 < g.P; p0 += kGroupTpb * kGU) {
     pas_rule r[kGU];
     int32_t c[kGU];
@@ -1058,7 +1062,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   const int32_t range_rules = (flags & PAS_TAS_FILTER) ? n_rules : 0;
   RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges};
   GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, tune.no_group};
-  const size_t group_lds = sizeof(int32_t) * ((size_t)G + 1);
+  const size_t group_lds = sizeof(int32_t) * ((size_t)G + 1 + (size_t)M);  // hist | cnt
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_prep_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_lds));
