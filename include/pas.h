@@ -246,6 +246,7 @@ int pas_label_patch_json(int32_t n_strategies, const char* const* names, uint64_
 #define PAS_GAS_MAX_RES 4         /* gpu.intel.com/ resource kinds per batch */
 #define PAS_GAS_MAX_SELECTIONS 64 /* card selections per pod: sum over containers of i915 */
 #define PAS_GAS_PACKED 8          /* selections / card ranks the packed result word holds */
+#define PAS_REQ_UNKNOWN_KIND 0x80000000u /* req_mask: requests a kind the snapshot lacks */
 /* bits 24-27 of a result word besides a count S <= PAS_GAS_PACKED: */
 #define PAS_GAS_SEL_EXTENDED 15   /* the pod fits (bit 31 set) but its card selection does not
                                      pack: more than 8 selections or a card rank >= 8; the
@@ -293,7 +294,12 @@ int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
  *             (containerRequests, utils.go:14-32); res_index i915 identifies
  *             gpu.intel.com/i915 among the n_res kinds (or -1 if absent)
  *   req_mask  [n_pods][max_containers] bit q set = container requests kind q
- *             (the key exists in its resourceMap, even with value 0)
+ *             (the key exists in its resourceMap, even with value 0); bit 31
+ *             (PAS_REQ_UNKNOWN_KIND) = the container also requests a gpu.intel.com/ kind
+ *             outside the snapshot's n_res kinds.  No node's capacity map has that key, so
+ *             every checkResourceCapacity of the container fails (:349-354): with
+ *             numI915 > 0 the pod fits no node; with numI915 == 0 it makes no selection
+ *             and the flag changes nothing (:206-215)
  *   n_containers [n_pods]
  * Output res_out[n_pods][n_nodes], one word per (pod, node):
  *   bit 31     the pod fits (node passes GASExtender.filterNodes, :467-473)
@@ -509,8 +515,8 @@ int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char*
  * requests named gpu.intel.com/... as AsInt64 values (ok ignored), in the pas_gas_fit layout
  * req[max_containers][n_kinds] / req_mask[max_containers] for kinds[0 .. n_kinds), and
  * *n_containers = len(spec.containers).  gpu.intel.com requests of other kinds are counted
- * in *n_unknown (a container with numI915 > 0 requesting one fits no node: capacity lacks the
- * key, scheduler.go:349-354).  A quantity ParseQuantity rejects is PAS_EDECODE
+ * in *n_unknown, and such a container's req_mask carries PAS_REQ_UNKNOWN_KIND (with
+ * numI915 > 0 it fits no node: capacity lacks the key, scheduler.go:349-354).  n_kinds <= 31.  A quantity ParseQuantity rejects is PAS_EDECODE
  * (Quantity.UnmarshalJSON); PAS_ECAPACITY when n_containers > max_containers.  With
  * n_kinds 0 (req may be NULL) it only validates the quantities, as the TAS decode does. */
 int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,

@@ -412,7 +412,7 @@ int or_gas_fit_ex(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32
                   int32_t max_containers, int32_t i915_index, const int64_t* req,
                   const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
                   uint8_t* sel_out, int32_t* nsel_out) {
-  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_RM_MAX_KEYS) return -1;
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
   or_rm node_used[OR_GAS_MAX_CARDS];
   uint8_t sel[OR_GAS_MAX_SEL];
   for (int32_t p = 0; p < n_pods; ++p) {
@@ -456,6 +456,7 @@ int or_gas_fit_ex(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32
         memset(&per_gpu, 0, sizeof per_gpu);
         for (int32_t q = 0; q < n_res; ++q)
           if (mask & (1u << q)) { per_gpu.has[q] = 1; per_gpu.val[q] = req[base * n_res + q]; }
+        if (mask & OR_REQ_UNKNOWN_KIND) per_gpu.has[OR_UNKNOWN_KEY] = 1;  /* no capacity key */
         int64_t num_i915 = 0;                   /* getNumI915 :192-198 */
         if (i915_index >= 0 && per_gpu.has[i915_index] && per_gpu.val[i915_index] > 0)
           num_i915 = per_gpu.val[i915_index];
@@ -523,6 +524,7 @@ static void container_map(int32_t n_res, const int64_t* req, uint32_t mask, or_r
   memset(out, 0, sizeof(or_rm));                    /* containerRequests (utils.go:14-32) */
   for (int32_t q = 0; q < n_res; ++q)
     if (mask & (1u << q)) { out->has[q] = 1; out->val[q] = req[q]; }
+  if (mask & OR_REQ_UNKNOWN_KIND) out->has[OR_UNKNOWN_KEY] = 1;  /* a kind no map holds */
 }
 
 int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
@@ -531,7 +533,7 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out, int32_t* status,
                 uint8_t* cards_out, int32_t* nsel_out) {
-  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_RM_MAX_KEYS) return -1;
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
   for (int32_t b = 0; b < n_binds; ++b) {
     const int32_t p = bind_pod[b], n = bind_node[b];
     if (n < 0 || n >= n_nodes) return -1;
@@ -585,7 +587,7 @@ int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int3
                    const uint32_t* req_mask, const int32_t* n_containers,
                    const int32_t* cards_per_container, const int32_t* cards, int32_t cards_stride,
                    int32_t* status) {
-  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_RM_MAX_KEYS) return -1;
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
   for (int32_t r = 0; r < n_rel; ++r) {
     const int32_t p = rel_pod[r], n = rel_node[r];
     if (n < 0 || n >= n_nodes) return -1;

@@ -111,6 +111,12 @@ int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const o
 #define OR_GAS_MAX_SEL 64
 #define OR_GAS_SEL_EXTENDED 15
 #define OR_GAS_SEL_LIMIT 14
+/* req_mask bit 31: the container requests a gpu.intel.com/ kind outside the packed kinds
+ * (include/pas.h PAS_REQ_UNKNOWN_KIND); restated as the key OR_UNKNOWN_KEY of its request
+ * map, which no capacity or usage map holds (containerRequests keeps every gpu.intel.com/
+ * key, utils.go:14-32; checkResourceCapacity then fails on it, scheduler.go:349-354). */
+#define OR_REQ_UNKNOWN_KIND 0x80000000u
+#define OR_UNKNOWN_KEY (OR_RM_MAX_KEYS - 1)
 
 /* GAS filter over every (pod, node) of a packed snapshot, one runSchedulingLogic
  * (scheduler.go:280-338) each; same layouts and result encoding as pas_gas_fit (words of

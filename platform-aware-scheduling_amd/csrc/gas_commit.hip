@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
       for (int64_t g = 0; g < num; ++g) {
         int chosen = -1;
         for (int k = 0; k < ncard && chosen < 0; ++k) {
-          bool ok = true;
+          bool ok = !(m & PAS_REQ_UNKNOWN_KIND);  // a key no capacity map has (:349-354)
           for (int q = 0; q < Q; ++q)
             if ((m >> q) & 1u) ok = ok && kind_fits(r[q], cap[q], w[k][q]);
           if (ok) chosen = k;
@@ -160,6 +160,8 @@ __global__ __launch_bounds__(kTpb) void gas_release_kernel(int32_t n_seg, BindAr
       const uint32_t m = a.mask[b];
       int64_t r[kMaxRes];
       for (int q = 0; q < Q; ++q) r[q] = a.req[b * Q + q] / kc;  // divide(numCards)
+      // subtractRM of a key no card map has (a kind outside the snapshot) -> errInput
+      if (m & PAS_REQ_UNKNOWN_KIND) ok = false;
       for (int32_t j = 0; ok && j < kc; ++j) {
         const int32_t k = a.cards[(int64_t)op * a.cards_stride + off + j];
         const bool known = k >= 0 && k < ncard;

@@ -123,6 +123,7 @@ __device__ GasStep container_step(const ContainerReq& cr, int32_t n_res, int32_t
   GasStep g = {};
   g.num_i915 = m != 0u ? (int32_t)min(ni, (int64_t)PAS_GAS_MAX_SELECTIONS + 1) : 0;
   g.kinds = (int32_t)(m & ((1u << n_res) - 1u));
+  g.bad = (m & PAS_REQ_UNKNOWN_KIND) ? 1 : 0;  // a key no capacity map has (:349-354)
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
     const bool has = q < n_res && ((m >> q) & 1u);
@@ -1291,7 +1292,7 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
       for (int64_t g = 0; g < num; ++g) {
         int chosen = -1;
         for (int k = 0; k < ncard && chosen < 0; ++k) {
-          bool ok = true;
+          bool ok = !(m & PAS_REQ_UNKNOWN_KIND);  // a key no capacity map has (:349-354)
           for (int q = 0; q < Q; ++q)
             if ((m >> q) & 1u) ok = ok && kind_fits(r[q], cap[q], w[k][q]);
           if (ok) chosen = k;

@@ -457,8 +457,8 @@ int pas_tas_prioritize_request(pas_ctx* ctx, uint64_t gen, const pas_rule* prio,
   if (rc) return rc;
   if ((rc = check_prio_request(ctx, prio, n_req, req_node, pos_out, len_out))) return rc;
   if ((rc = activate(ctx))) return rc;
-  const size_t ws = prio_request_workspace(ctx, n_req);
-  if (!ws) return set_error(ctx, PAS_EDEVICE, "pas_tas_prioritize_request: sort sizing failed");
+  size_t ws = 0;
+  if ((rc = prio_request_workspace(ctx, n_req, &ws))) return rc;
   const size_t b_req = sizeof(int32_t) * (size_t)std::max(n_req, 1);
   if ((rc = ensure_scratch(ctx, carve_size({b_req, b_req, sizeof(int32_t), ws})))) return rc;
   Carve cv{static_cast<char*>(ctx->scratch)};
@@ -484,8 +484,8 @@ int pas_tas_prioritize_request_device(pas_ctx* ctx, uint64_t gen, const pas_rule
   if (rc) return rc;
   if ((rc = check_prio_request(ctx, prio, n_req, d_req_node, d_pos_out, d_len_out))) return rc;
   if ((rc = activate(ctx))) return rc;
-  const size_t ws = prio_request_workspace(ctx, n_req);
-  if (!ws) return set_error(ctx, PAS_EDEVICE, "pas_tas_prioritize_request: sort sizing failed");
+  size_t ws = 0;
+  if ((rc = prio_request_workspace(ctx, n_req, &ws))) return rc;
   if ((rc = ensure_scratch(ctx, ws))) return rc;
   return prio_request_launch(ctx, *prio, n_req, d_req_node, d_pos_out, d_len_out, ctx->scratch,
                              ws, pick_stream(ctx, hip_stream));
@@ -666,7 +666,7 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
     int64_t sel = 0;
     for (int32_t c = 0; c < n_containers[p]; ++c) {
       const int64_t b = (int64_t)p * max_containers + c;
-      if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
+      if ((req_mask[b] & ~PAS_REQ_UNKNOWN_KIND) >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
       int64_t v = 0;
       if (release) {
         v = cpc[(int64_t)i * max_containers + c];
@@ -840,7 +840,7 @@ static int gas_fit_host(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_
     int64_t sel = 0;
     for (int32_t c = 0; c < n_containers[p]; ++c) {
       const int64_t b = (int64_t)p * max_containers + c;
-      if (req_mask[b] >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
+      if ((req_mask[b] & ~PAS_REQ_UNKNOWN_KIND) >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
       if (i915_index >= 0 && (req_mask[b] >> i915_index & 1u)) {
         const int64_t v = std::max<int64_t>(req[b * Q + i915_index], 0);
         sel = std::min<int64_t>(sel + std::min<int64_t>(v, PAS_GAS_MAX_SELECTIONS + 1),

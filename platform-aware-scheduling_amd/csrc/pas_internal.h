@@ -149,7 +149,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
                     int32_t topk, hipStream_t s);
 // Single-request prioritize (tas_request.hip): workspace bytes for n_req positions, and the
 // launch (rule is host-side; ws = that many device bytes).
-size_t prio_request_workspace(pas_ctx* ctx, int32_t n_req);
+int prio_request_workspace(pas_ctx* ctx, int32_t n_req, size_t* bytes);  // status
 int prio_request_launch(pas_ctx* ctx, const pas_rule& rule, int32_t n_req, const int32_t* d_req,
                         int32_t* d_pos, int32_t* d_len, void* ws, size_t ws_bytes,
                         hipStream_t s);

@@ -308,14 +308,18 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
   }
 }
 
-__global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, RangesParams R,
-                                                             int ablate) {
+// PAS_PREP_ABLATE (compile time, diagnostic timing builds only; outputs wrong): 1 = no
+// ranges, 2 = no grouping.  The product library is built with 0.
+#ifndef PAS_PREP_ABLATE
+#define PAS_PREP_ABLATE 0
+#endif
+__global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, RangesParams R) {
   extern __shared__ __attribute__((aligned(16))) int32_t sh[];
   if (blockIdx.x == 0) {
-    if (!(ablate & 2)) group_body(g, sh);
+    if (!(PAS_PREP_ABLATE & 2)) group_body(g, sh);
     return;
   }
-  if (ablate & 1) return;
+  if (PAS_PREP_ABLATE & 1) return;
   const int32_t r =
       (int32_t)(blockIdx.x - 1) * (kGroupTpb / kRuleLanes) + (int32_t)(threadIdx.x / kRuleLanes);
   if (r < R.n_rules) ranges_group(R, r);
@@ -425,9 +429,9 @@ struct EvalParams {
 //      the exchange, and the exchange orders LDS only, so loads and stores stay in flight
 //      across rounds;
 //   C. FilterResult row -> HBM, HostPriorityList length.
-// kS: adjacent segments per wave per round.  kAblate (diagnostic timing builds only,
-// PAS_EVAL_ABLATE; outputs wrong): 1 = no stores, 2 = no count exchange, 4 = no pass-bit
-// lookups, 8 = no rule loop.
+// kS: adjacent segments per wave per round.  kAblate (diagnostic timing builds only: the
+// compile-time PAS_EVAL_ABLATE, 0 in the product library; outputs wrong): 1 = no stores,
+// 2 = no count exchange, 4 = no pass-bit lookups, 8 = no rule loop.
 // kGP (clusters past the LDS pass bitmap, ~1.1M nodes): the pod's pass bitmap lives in a
 // global scratch row instead (P.gpass, one row per workgroup of the launch; lookups are
 // workgroup-coherent loads, clears are L2 atomics) — the same algorithm, slower lookups.
@@ -626,259 +630,6 @@ constexpr int kTpb = 256;
 constexpr int kWaves = kTpb / 64;
 
 
-// 32 bits of x spread to the even bits of a 64-bit word (Morton order).
-__device__ __forceinline__ uint64_t spread_even(uint32_t x) {
-  uint64_t v = x;
-  v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
-  v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
-  v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
-  v = (v | (v << 2)) & 0x3333333333333333ull;
-  v = (v | (v << 1)) & 0x5555555555555555ull;
-  return v;
-}
-
-// deschedule.Strategy.Violated (deschedule/strategy.go:31-50) per registered strategy, as
-// nodeStatusForStrategy does (deschedule/enforce.go:154-164).  A wave owns 2 * kPair
-// consecutive 64-node words; each lane reads two adjacent nodes with one 16-byte load per
-// word pair, so a rule's column is read as contiguous 1-KB runs.  The lane's presence bits
-// are folded into its compares, the even / odd nodes' hits are ballotted separately and
-// accumulated per strategy, and only the finished words are interleaved back into node
-// order.  The strategies' rules are walked as one flat list, kU at a time, every value load
-// of the batch issued before the first compare; a strategy's words are written when the list
-// passes its end (strategies without rules write 0).
-template <int kPair, int kU, bool kVec>
-__global__ __launch_bounds__(kTpb) void tas_violations_kernel(
-    int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
-    const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
-    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out) {
-  constexpr int kWd = 2 * kPair;
-  const int32_t gw0 = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * kWd;
-  if (gw0 >= W64) return;
-  const int lane = threadIdx.x & 63;
-  const int32_t half = lane >> 5;          // word of its pair the lane's nodes fall in
-  const uint32_t sh = (uint32_t)(lane & 31) * 2;  // bit of its even node in that word
-  int32_t pos[kPair];   // the lane's even node
-  bool ok0[kPair], ok1[kPair];
-#pragma unroll
-  for (int k = 0; k < kPair; ++k) {
-    const int32_t n = (gw0 + 2 * k) * 64 + 2 * lane;
-    ok0[k] = n < N;
-    ok1[k] = n + 1 < N;
-    pos[k] = n;
-  }
-  const int32_t r_end = rule_off[n_strat];
-  int32_t s = 0;
-  int32_t s_end = n_strat > 0 ? rule_off[1] : 0;
-  uint64_t acc_e[kPair] = {}, acc_o[kPair] = {};
-  auto flush = [&]() {
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < kPair; ++k) {
-        const int32_t w = gw0 + 2 * k;
-        const uint64_t lo = spread_even((uint32_t)acc_e[k]) | (spread_even((uint32_t)acc_o[k]) << 1);
-        const uint64_t hi = spread_even((uint32_t)(acc_e[k] >> 32)) |
-                            (spread_even((uint32_t)(acc_o[k] >> 32)) << 1);
-        if (w < W64) viol_out[(int64_t)s * W64 + w] = lo;
-        if (w + 1 < W64) viol_out[(int64_t)s * W64 + w + 1] = hi;
-      }
-#pragma unroll
-    for (int k = 0; k < kPair; ++k) acc_e[k] = acc_o[k] = 0;
-  };
-  for (int32_t r0 = rule_off[0]; r0 < r_end; r0 += kU) {
-    pas_rule ru[kU];
-    int64_t v[kU][kPair][2];
-    uint64_t pr[kU][kPair][2];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) ru[u] = rules[min(r0 + u, r_end - 1)];
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int32_t m = (ru[u].metric >= 0 && ru[u].metric < M) ? ru[u].metric : 0;
-      const int64_t* col = vals + (int64_t)m * N;
-      const uint64_t* pw = present + (int64_t)m * W64 + gw0;  // with the values, not after
-#pragma unroll
-      for (int k = 0; k < kPair; ++k) {
-        pr[u][k][0] = pw[2 * k];
-        pr[u][k][1] = gw0 + 2 * k + 1 < W64 ? pw[2 * k + 1] : 0ull;
-      }
-#pragma unroll
-      for (int k = 0; k < kPair; ++k) {
-        if (kVec) {  // N even: rows 16-byte aligned, a pair in bounds or wholly past N
-          const longlong2 x =
-              *reinterpret_cast<const longlong2*>(col + (ok0[k] ? pos[k] : N - 2));
-          v[u][k][0] = x.x;
-          v[u][k][1] = x.y;
-        } else {
-          v[u][k][0] = col[min(pos[k], N - 1)];
-          v[u][k][1] = col[min(pos[k] + 1, N - 1)];
-        }
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int32_t r = r0 + u;
-      if (r >= r_end) break;
-      while (r >= s_end) {  // the list has passed strategy s: its words are complete
-        flush();
-        ++s;
-        s_end = rule_off[s + 1];
-      }
-      const pas_rule rule = ru[u];
-      if (rule.metric < 0 || rule.metric >= M || rule.op < 0 || rule.op > 2) continue;
-      int64_t tm = 0;
-      const int sat = target_milli(rule.target, &tm);
-#pragma unroll
-      for (int k = 0; k < kPair; ++k) {
-        const uint64_t pl = (half ? pr[u][k][1] : pr[u][k][0]) >> sh;  // the lane's two bits
-        bool hit[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int64_t x = v[u][k][e];
-          bool h;
-          if (rule.op == PAS_OP_LESS_THAN) h = sat > 0 || (sat == 0 && x < tm);
-          else if (rule.op == PAS_OP_GREATER_THAN) h = sat < 0 || (sat == 0 && x > tm);
-          else h = sat == 0 && x == tm;
-          hit[e] = h && ((pl >> e) & 1);
-        }
-        acc_e[k] |= __ballot(hit[0] && ok0[k]);
-        acc_o[k] |= __ballot(hit[1] && ok1[k]);
-      }
-    }
-  }
-  for (; s < n_strat; ++s) flush();  // the last strategy with rules, then those without
-}
-
-// The sweep with column reuse (n_strat <= 64): the workgroup sorts the flat rule list by
-// metric in LDS (chunks of kDedupRules), so each wave reads every referenced column of its
-// two words once and evaluates all rules on it (C4's 64 rules reference ~41 of the 64
-// columns).  Accumulators are lane-packed: lane s holds strategy s's even / odd hit masks;
-// at the end each lane interleaves its own masks and stores its strategy's two words.
-constexpr int kDedupRules = 256;
-
-struct DedupRule {
-  int64_t tm;      // target * 1000 (when sat == 0)
-  int32_t metric;  // M: skipped (not in the cache / invalid operator)
-  int32_t op;
-  int32_t sat;
-  int32_t strat;
-};
-
-template <bool kVec>
-__global__ __launch_bounds__(kTpb) void tas_violations_dedup_kernel(
-    int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
-    const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
-    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out) {
-  __shared__ DedupRule srt[kDedupRules];
-  __shared__ int32_t key[kDedupRules];
-  __shared__ int32_t off[65];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int32_t gw0 = (blockIdx.x * kWaves + (tid >> 6)) * 2;  // the wave's word pair
-  const bool active = gw0 < W64;  // (no early exit: the workgroup sorts together)
-  const int32_t n = gw0 * 64 + 2 * lane;
-  const bool ok0 = n < N, ok1 = n + 1 < N;
-  const int32_t half = lane >> 5;
-  const uint32_t sh = (uint32_t)(lane & 31) * 2;
-  if (tid <= n_strat) off[tid] = rule_off[tid];
-  __syncthreads();
-  const int32_t r_begin = off[0], r_end = off[n_strat];
-  uint32_t ae_lo = 0, ae_hi = 0, ao_lo = 0, ao_hi = 0;  // lane s: strategy s
-  for (int32_t c0 = r_begin; c0 < r_end; c0 += kDedupRules) {
-    const int32_t nr = min(kDedupRules, r_end - c0);
-    // sort the chunk by metric (stable): rank = rules with a smaller key, or an equal key
-    // and a smaller index
-    __syncthreads();  // the previous chunk's table is no longer read
-    int32_t my_key = 0;
-    DedupRule d{};
-    if (tid < nr) {
-      const int32_t r = c0 + tid;
-      const pas_rule ru = rules[r];
-      int32_t st = 0;  // the strategy: largest s with off[s] <= r
-      for (int32_t b = 64; b > 0; b >>= 1)
-        if (st + b <= n_strat && off[st + b] <= r) st += b;
-      while (st < n_strat - 1 && off[st + 1] <= r) ++st;  // empty strategies at r
-      const bool valid = ru.metric >= 0 && ru.metric < M && ru.op >= 0 && ru.op <= 2;
-      d.metric = valid ? ru.metric : M;
-      d.op = ru.op;
-      d.sat = target_milli(ru.target, &d.tm);
-      d.strat = st;
-      my_key = d.metric;
-      key[tid] = my_key;
-    }
-    __syncthreads();
-    if (tid < nr) {
-      int32_t rank = 0;
-      for (int32_t q = 0; q < nr; ++q) {
-        const int32_t kq = key[q];
-        rank += (kq < my_key || (kq == my_key && q < tid)) ? 1 : 0;
-      }
-      srt[rank] = d;
-    }
-    __syncthreads();
-    if (!active) continue;
-    // walk the sorted rules metric by metric, the next column's loads in flight
-    auto load = [&](int32_t m, int64_t* v, uint64_t* p) {
-      const int64_t* col = vals + (int64_t)min(m, M - 1) * N;
-      if (kVec) {
-        const longlong2 x = *reinterpret_cast<const longlong2*>(col + (ok0 ? n : N - 2));
-        v[0] = x.x;
-        v[1] = x.y;
-      } else {
-        v[0] = col[min(n, N - 1)];
-        v[1] = col[min(n + 1, N - 1)];
-      }
-      const uint64_t* pw = present + (int64_t)min(m, M - 1) * W64 + gw0;
-      p[0] = pw[0];
-      p[1] = gw0 + 1 < W64 ? pw[1] : 0ull;
-    };
-    int32_t i = 0;
-    int32_t m_cur = __builtin_amdgcn_readfirstlane(srt[0].metric);
-    int64_t v[2];
-    uint64_t p[2];
-    load(m_cur, v, p);
-    while (i < nr && m_cur < M) {
-      int32_t j = i + 1;
-      while (j < nr && srt[j].metric == m_cur) ++j;
-      const int32_t m_next = j < nr ? __builtin_amdgcn_readfirstlane(srt[j].metric) : M;
-      int64_t nv[2];
-      uint64_t np[2];
-      load(m_next < M ? m_next : m_cur, nv, np);
-      const uint64_t pl = (half ? p[1] : p[0]) >> sh;  // the lane's two presence bits
-      for (int32_t k = i; k < j; ++k) {
-        const int32_t op = __builtin_amdgcn_readfirstlane(srt[k].op);
-        const int32_t sat = __builtin_amdgcn_readfirstlane(srt[k].sat);
-        const int32_t st = __builtin_amdgcn_readfirstlane(srt[k].strat);
-        const int64_t tm = srt[k].tm;
-        bool hit[2];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          bool h;
-          if (op == PAS_OP_LESS_THAN) h = sat > 0 || (sat == 0 && v[e] < tm);
-          else if (op == PAS_OP_GREATER_THAN) h = sat < 0 || (sat == 0 && v[e] > tm);
-          else h = sat == 0 && v[e] == tm;
-          hit[e] = h && ((pl >> e) & 1);
-        }
-        const uint64_t be = __ballot(hit[0] && ok0), bo = __ballot(hit[1] && ok1);
-        const bool me = lane == st;
-        ae_lo |= me ? (uint32_t)be : 0u;
-        ae_hi |= me ? (uint32_t)(be >> 32) : 0u;
-        ao_lo |= me ? (uint32_t)bo : 0u;
-        ao_hi |= me ? (uint32_t)(bo >> 32) : 0u;
-      }
-      v[0] = nv[0];
-      v[1] = nv[1];
-      p[0] = np[0];
-      p[1] = np[1];
-      m_cur = m_next;
-      i = j;
-    }
-  }
-  if (active && lane < n_strat) {
-    const uint64_t lo = spread_even(ae_lo) | (spread_even(ao_lo) << 1);
-    const uint64_t hi = spread_even(ae_hi) | (spread_even(ao_hi) << 1);
-    viol_out[(int64_t)lane * W64 + gw0] = lo;
-    if (gw0 + 1 < W64) viol_out[(int64_t)lane * W64 + gw0 + 1] = hi;
-  }
-}
-
 // The sweep by column runs: a wave owns kRun consecutive 64-node words and walks the flat
 // rule list one rule at a time, reading that rule's column over its words as one
 // contiguous kRun * 512-byte run (every DRAM page it opens is read whole) while the next
@@ -966,15 +717,18 @@ int env_int(const char* name, int dflt) {
   return e ? std::atoi(e) : dflt;
 }
 
+#ifndef PAS_EVAL_ABLATE
+#define PAS_EVAL_ABLATE 0  // diagnostic timing builds only (outputs wrong); see tas_eval_kernel
+#endif
+
 // Launch shape of the eval kernel.  The PAS_EVAL_* environment overrides exist for tuning
-// sweeps (scripts/emit_sweep.sh); the ablations are diagnostic timing builds whose outputs
-// are wrong.
+// sweeps (scripts/tas_sweep.sh); every one of them leaves the outputs unchanged (launch
+// shape, pod order across workgroups, store cache policy) — tests/test_env_knobs.py checks
+// that.  Output-changing diagnostics (PAS_EVAL_ABLATE, PAS_PREP_ABLATE) are compile-time.
 struct TasTuning {
   int32_t waves = 4;         // waves per eval workgroup (2, 4 or 8)
   int32_t seg_per_wave = 1;  // adjacent order segments per wave per round (1 or 2)
   int32_t no_group = 0;      // diagnostic: pods in index order (no XCD locality)
-  int32_t ablate = 0;
-  int32_t prep_ablate = 0;
   int32_t store_aux = kNtAux;  // cache policy of the whole-line stores
 };
 
@@ -985,8 +739,6 @@ const TasTuning& tas_tuning() {
     x.waves = w == 8 ? 8 : w == 2 ? 2 : 4;
     x.seg_per_wave = env_int("PAS_EVAL_SEGS", x.seg_per_wave) == 2 ? 2 : 1;
     x.no_group = env_int("PAS_EVAL_NOGROUP", 0);
-    x.ablate = env_int("PAS_EVAL_ABLATE", 0);
-    x.prep_ablate = env_int("PAS_PREP_ABLATE", 0);
     x.store_aux = env_int("PAS_EVAL_AUX", x.store_aux);
     return x;
   }();
@@ -1070,7 +822,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   const unsigned prep_blocks =
       1u + (unsigned)((range_rules + kRulesPerBlock - 1) / kRulesPerBlock);
   timing_begin(ctx, s, PAS_K_TAS_PREP, &tl);
-  tas_prep_kernel<<<prep_blocks, kGroupTpb, group_lds, s>>>(gp, rp, tune.prep_ablate);
+  tas_prep_kernel<<<prep_blocks, kGroupTpb, group_lds, s>>>(gp, rp);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
 
@@ -1088,20 +840,19 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   ep.pos_base = 0;
   ep.gpass = static_cast<uint32_t*>(ctx->tas_gpass);
   using EvalFn = void (*)(EvalParams);
-  EvalFn fn = &tas_eval_kernel<4, 1, 0>;
-#define PAS_EVAL_CASE(W, S, A) \
-  if (tune.waves == W && tune.seg_per_wave == S && tune.ablate == A) fn = &tas_eval_kernel<W, S, A>;
-  PAS_EVAL_CASE(4, 2, 0) PAS_EVAL_CASE(8, 1, 0) PAS_EVAL_CASE(8, 2, 0)
-  PAS_EVAL_CASE(2, 1, 0) PAS_EVAL_CASE(2, 2, 0) PAS_EVAL_CASE(2, 1, 2)
-  PAS_EVAL_CASE(4, 1, 1) PAS_EVAL_CASE(4, 1, 2) PAS_EVAL_CASE(4, 1, 4) PAS_EVAL_CASE(4, 1, 8)
-  PAS_EVAL_CASE(4, 1, 7) PAS_EVAL_CASE(4, 2, 1) PAS_EVAL_CASE(4, 2, 2)
+  constexpr int kA = PAS_EVAL_ABLATE;
+  EvalFn fn = &tas_eval_kernel<4, 1, kA>;
+#define PAS_EVAL_CASE(W, S) \
+  if (tune.waves == W && tune.seg_per_wave == S) fn = &tas_eval_kernel<W, S, kA>;
+  PAS_EVAL_CASE(4, 2) PAS_EVAL_CASE(8, 1) PAS_EVAL_CASE(8, 2) PAS_EVAL_CASE(2, 1)
+  PAS_EVAL_CASE(2, 2)
 #undef PAS_EVAL_CASE
-  if (tune.store_aux == 0) fn = &tas_eval_kernel<4, 1, 0, 0>;
-  if (tune.store_aux == 3) fn = &tas_eval_kernel<4, 1, 0, 3>;
-  if (tune.store_aux == 16) fn = &tas_eval_kernel<4, 1, 0, 16>;
-  if (tune.store_aux == 2) fn = &tas_eval_kernel<4, 1, 0, 2>;
-  if (tune.store_aux == 19) fn = &tas_eval_kernel<4, 1, 0, 19>;
-  if (global_pass) fn = &tas_eval_kernel<4, 1, 0, kNtAux, true>;
+  if (tune.store_aux == 0) fn = &tas_eval_kernel<4, 1, kA, 0>;
+  if (tune.store_aux == 3) fn = &tas_eval_kernel<4, 1, kA, 3>;
+  if (tune.store_aux == 16) fn = &tas_eval_kernel<4, 1, kA, 16>;
+  if (tune.store_aux == 2) fn = &tas_eval_kernel<4, 1, kA, 2>;
+  if (tune.store_aux == 19) fn = &tas_eval_kernel<4, 1, kA, 19>;
+  if (global_pass) fn = &tas_eval_kernel<4, 1, kA, kNtAux, true>;
   const int32_t waves = global_pass ? 4 : tune.waves;
   if (eval_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
@@ -1124,47 +875,16 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   if (W64 == 0) return PAS_OK;
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_VIOLATIONS, &tl);
-  // word pairs per wave / rules per batch of loads (tuning: PAS_VIOL_PAIRS, PAS_VIOL_U)
-  static const int pairs = env_int("PAS_VIOL_PAIRS", 1), u = env_int("PAS_VIOL_U", 2);
-  using ViolFn = void (*)(int32_t, int32_t, int32_t, int32_t, const int32_t*, const pas_rule*,
-                          const int64_t*, const uint64_t*, uint64_t*);
-  const bool vec = t.n_nodes >= 2 && (t.n_nodes & 1) == 0;
-  ViolFn fn = vec ? &tas_violations_kernel<1, 2, true> : &tas_violations_kernel<1, 2, false>;
-  int per_wave = 2;
-#define PAS_VIOL_CASE(PR, U)                                                            \
-  if (pairs == PR && u == U) {                                                          \
-    fn = vec ? &tas_violations_kernel<PR, U, true> : &tas_violations_kernel<PR, U, false>; \
-    per_wave = 2 * PR;                                                                  \
-  }
-  PAS_VIOL_CASE(1, 1) PAS_VIOL_CASE(1, 4) PAS_VIOL_CASE(2, 1) PAS_VIOL_CASE(2, 2)
-#undef PAS_VIOL_CASE
+  // words per wave (an output-invariant tuning knob: PAS_VIOL_RUN = 2, 4, 8 or 16)
   static const int run = env_int("PAS_VIOL_RUN", 8);
-  if (run > 0 && !env_int("PAS_VIOL_FLAT", 0) && !env_int("PAS_VIOL_DEDUP", 0)) {
-    auto rfn = run == 2    ? &tas_violations_run_kernel<2>
-               : run == 4  ? &tas_violations_run_kernel<4>
-               : run == 16 ? &tas_violations_run_kernel<16>
-                           : &tas_violations_run_kernel<8>;
-    const int32_t per = (run == 2 || run == 4 || run == 16) ? run : 8;
-    const int32_t rwaves = (W64 + per - 1) / per;
-    rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
-        t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
-    timing_end(ctx, s, &tl);
-    PAS_HIP(ctx, hipGetLastError());
-    return PAS_OK;
-  }
-  if (n_strat <= 64 && env_int("PAS_VIOL_DEDUP", 0)) {
-    auto dfn = vec ? &tas_violations_dedup_kernel<true> : &tas_violations_dedup_kernel<false>;
-    const int32_t pairs_total = (W64 + 1) / 2;
-    dfn<<<(pairs_total + kWaves - 1) / kWaves, kTpb, 0, s>>>(
-        t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
-    timing_end(ctx, s, &tl);
-    PAS_HIP(ctx, hipGetLastError());
-    return PAS_OK;
-  }
-  const int32_t waves = (W64 + per_wave - 1) / per_wave;
-  fn<<<(waves + kWaves - 1) / kWaves, kTpb, 0, s>>>(t.n_nodes, t.n_metrics, W64, n_strat,
-                                                    d_rule_off, d_rules, t.vals, t.present,
-                                                    d_viol);
+  auto rfn = run == 2    ? &tas_violations_run_kernel<2>
+             : run == 4  ? &tas_violations_run_kernel<4>
+             : run == 16 ? &tas_violations_run_kernel<16>
+                         : &tas_violations_run_kernel<8>;
+  const int32_t per = (run == 2 || run == 4 || run == 16) ? run : 8;
+  const int32_t rwaves = (W64 + per - 1) / per;
+  rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
+      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;

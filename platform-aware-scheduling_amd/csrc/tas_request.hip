@@ -119,16 +119,19 @@ Bits key_bits(int32_t n_nodes, int32_t n_req) {
 
 }  // namespace
 
-size_t prio_request_workspace(pas_ctx* ctx, int32_t n_req) {
+int prio_request_workspace(pas_ctx* ctx, int32_t n_req, size_t* bytes) {
+  *bytes = 0;
+  if (n_req == 0) return PAS_OK;  // the launch returns an empty list before any sort
   const Bits b = key_bits(ctx->tas.n_nodes, n_req);
   size_t tmp = 0;
   uint64_t* none = nullptr;
   if (rocprim::radix_sort_keys(nullptr, tmp, none, none, (size_t)n_req, 0, b.rb + b.pb) !=
       hipSuccess)
-    return 0;
+    return set_error(ctx, PAS_EDEVICE, "pas_tas_prioritize_request: sort sizing failed");
   auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  return up(sizeof(int32_t) * (size_t)ctx->tas.n_nodes) + 2 * up(sizeof(uint64_t) * n_req) +
-         up(tmp);
+  *bytes = up(sizeof(int32_t) * (size_t)ctx->tas.n_nodes) + 2 * up(sizeof(uint64_t) * n_req) +
+           up(tmp);
+  return PAS_OK;
 }
 
 int prio_request_launch(pas_ctx* ctx, const pas_rule& rule, int32_t n_req,

@@ -416,6 +416,22 @@ bool string_field(Scanner& s, std::string* v) {
   return s.string(v);
 }
 
+// A map[string]string field (ObjectMeta labels / annotations): null is a nil map, every
+// value must be a string or null (json.Unmarshal fails on any other value, whichever key it
+// sits under).  on_entry(key, value) sees each string entry in order.
+template <class F>
+bool string_map(Scanner& s, F&& on_entry) {
+  const char c = s.peek();
+  if (c == 'n') return s.literal("null");
+  if (c != '{') return s.mismatch();
+  return s.object([&](std::string_view k) {
+    std::string v;  // a fresh element: null stores ""
+    if (!string_field(s, &v)) return false;
+    on_entry(k, v);
+    return true;
+  });
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- name table
@@ -759,21 +775,15 @@ int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char*
         if (m != '{') return s.mismatch();
         return s.object([&](std::string_view mk) {
           if (fold_match("namespace", mk)) return string_field(s, &ns);
+          if (fold_match("annotations", mk)) return string_map(s, [](std::string_view, auto&) {});
           if (!fold_match("labels", mk)) return s.skip();
-          const char l = s.peek();
-          if (l == 'n') {  // a nil map
-            has_label = false;
-            return s.literal("null");
-          }
-          if (l != '{') return s.mismatch();
-          // a map decodes into the existing map (entries accumulate across repeated keys)
-          return s.object([&](std::string_view lk) {
-            if (lk != want) return s.skip();
-            std::string v;  // a fresh element: null stores ""
-            if (!string_field(s, &v)) return false;
+          if (s.peek() == 'n') has_label = false;  // a nil map
+          // a map decodes into the existing map (entries accumulate across repeated keys);
+          // every entry is type-checked, not only the policy label
+          return string_map(s, [&](std::string_view lk, const std::string& v) {
+            if (lk != want) return;
             has_label = true;
             value = v;
-            return true;
           });
         });
       });
@@ -792,7 +802,7 @@ int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char*
 int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
                             const char* const* kinds, int32_t max_containers, int64_t* req,
                             uint32_t* req_mask, int32_t* n_containers, int32_t* n_unknown) {
-  if (len < 0 || (len > 0 && !pod) || n_kinds < 0 || n_kinds > 32 || (n_kinds > 0 && !kinds) ||
+  if (len < 0 || (len > 0 && !pod) || n_kinds < 0 || n_kinds > 31 || (n_kinds > 0 && !kinds) ||
       max_containers < 0 || (max_containers > 0 && ((n_kinds > 0 && !req) || !req_mask)) ||
       !n_containers ||
       !n_unknown)
@@ -836,6 +846,15 @@ int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
         if (r == 'n') return s.literal("null");
         if (r != '{') return s.mismatch();
         return s.object([&](std::string_view rk) {
+          if (fold_match("limits", rk)) {  // a ResourceList too: every value is parsed
+            const char m = s.peek();
+            if (m == 'n') return s.literal("null");
+            if (m != '{') return s.mismatch();
+            return s.object([&](std::string_view) {
+              int64_t v = 0;
+              return quantity(&v);
+            });
+          }
           if (!fold_match("requests", rk)) return s.skip();
           const char m = s.peek();
           if (m == 'n') {
@@ -867,6 +886,16 @@ int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
       s.type_err = true;
     } else {
       ok = s.object([&](std::string_view k) {
+        if (fold_match("metadata", k)) {  // ObjectMeta maps are type-checked as Go decodes them
+          const char m = s.peek();
+          if (m == 'n') return s.literal("null");
+          if (m != '{') return s.mismatch();
+          return s.object([&](std::string_view mk) {
+            if (fold_match("labels", mk) || fold_match("annotations", mk))
+              return string_map(s, [](std::string_view, auto&) {});
+            return s.skip();
+          });
+        }
         if (!fold_match("spec", k)) return s.skip();
         const char sp = s.peek();
         if (sp == 'n') return s.literal("null");
@@ -904,8 +933,9 @@ int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
       if (name.compare(0, sizeof kPrefix - 1, kPrefix) != 0) continue;
       int32_t q = 0;
       while (q < n_kinds && name != kinds[q]) ++q;
-      if (q == n_kinds) {
+      if (q == n_kinds) {  // no node's capacity has the key: every check fails (:349-354)
         ++*n_unknown;
+        req_mask[c] |= PAS_REQ_UNKNOWN_KIND;
         continue;
       }
       req[(int64_t)c * n_kinds + q] = cont[c].values[i];

@@ -49,6 +49,7 @@ PAS_GAS_MAX_CARDS = 64
 PAS_GAS_MAX_RES = 4
 PAS_GAS_MAX_SELECTIONS = 64
 PAS_GAS_PACKED = 8
+PAS_REQ_UNKNOWN_KIND = 0x80000000
 PAS_GAS_SEL_EXTENDED = 15
 PAS_GAS_SEL_LIMIT = 14
 

@@ -45,6 +45,17 @@ def _decode(body: bytes):
     return json.loads(body)
 
 
+def _compact(item: bytes) -> bytes:
+    """Compact re-encoding of one node item the library's decoder accepted.  Invalid UTF-8
+    becomes U+FFFD, as Go's decoder maps it; nesting past Python's recursion limit (Go allows
+    10000 levels) keeps the item's own bytes."""
+    try:
+        return json.dumps(json.loads(item.decode("utf-8", "replace")), separators=(",", ":"),
+                          ensure_ascii=False).encode()
+    except RecursionError:
+        return item
+
+
 class MetricsExtender:
     """TAS extender: Filter / Prioritize / Bind (telemetryscheduler.go:36-244).
 
@@ -124,8 +135,7 @@ class MetricsExtender:
                                            make_rules([-1], [0], [0]), cand[None, :],
                                            _lib.PAS_TAS_FILTER)
         # the shim's json.Marshal of each v1.Node (here: the compact re-encoding of the item)
-        blobs = [json.dumps(json.loads(body[o:o + n]), separators=(",", ":")).encode()
-                 for o, n in spans]
+        blobs = [_compact(body[o:o + n]) for o, n in spans]
         table = wire.NodeTable(self._names(body, info, idx), blobs)
         order = np.arange(info.n_req, dtype=np.int32)
         # the pass row re-indexed to the request's own order (duplicates keep their verdict);
@@ -192,9 +202,10 @@ class GASExtender:
         """containerRequests (utils.go:14-32) through pas_decode_pod_requests: gpu.intel.com/
         requests as AsInt64 (ok ignored) in the pas_gas_fit layout, plus each container's
         numI915 (its annotation segment length)."""
-        req, mask, ncont, unknown = wire.decode_pod_requests(pod_json, self.kinds)
-        if unknown:
-            raise KeyError("a gpu.intel.com resource kind not in the snapshot")
+        # a container requesting a gpu.intel.com/ kind no node has carries
+        # PAS_REQ_UNKNOWN_KIND in its mask: with numI915 > 0 it fits no node (capacity lacks
+        # the key, :349-354), with numI915 == 0 it makes no selection (:206-215)
+        req, mask, ncont, _ = wire.decode_pod_requests(pod_json, self.kinds)
         per_container = []
         for ci in range(int(ncont[0])):
             on = self.i915 >= 0 and (int(mask[0, ci]) >> self.i915) & 1

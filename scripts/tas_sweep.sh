@@ -1,6 +1,7 @@
 #!/bin/bash
 # Diagnostic sweep of TAS launch shapes / ablations given as env assignments, e.g.
-#   tas_sweep.sh "PAS_EVAL_WAVES=8" "PAS_EVAL_ABLATE=1".  Runs the TAS GPU tests first.
+#   tas_sweep.sh "PAS_EVAL_WAVES=8" "PAS_EVAL_SEGS=2".  Runs the TAS GPU tests first.
+# (Ablations are compile-time: scripts/diag/build_variant.sh with -DPAS_EVAL_ABLATE=N.)
 set -u
 cd "$(dirname "$0")/.."; mkdir -p gpurun_out/sweep
 timeout -k 10 300 python -u -m pytest tests/test_tas_gpu.py -x -q \

@@ -168,3 +168,25 @@ def test_deschedule_enforce_g4(ctx):
         assert bodies["node-1"].decode() == c["derived"]["patch"]
         after = apply_label_patch(c["labels"], bodies["node-1"])
         assert [n for n in g["nodes"] if after.get(g["policy"]) == "violating"] == c["want"]
+
+
+def test_gas_filter_unknown_kind(ctx):
+    # a request for a gpu.intel.com/ kind no node has (scheduler.go:206-215, 349-354): with
+    # an i915 in the same container every node fails; without one it fits with no cards
+    names, nodes = gas_cluster()
+    kinds = ["gpu.intel.com/i915", "gpu.intel.com/memory.max"]
+    n_cards, cap, used, card_names = sn.gas_snapshot_from_nodes(nodes, kinds)
+    ctx.gas_snapshot_set(8400, n_cards, cap, used)
+    g = ext.GASExtender(ctx, 8400, names, card_names, kinds)
+
+    def filt(requests):
+        pod = {"metadata": {"name": "u", "namespace": "default"},
+               "spec": {"containers": [{"resources": {"requests": r}} for r in requests]}}
+        status, out = g.filter(json.dumps({"Pod": pod, "NodeNames": names}).encode())
+        assert status == 200
+        return json.loads(out)["NodeNames"]
+
+    assert filt([{"gpu.intel.com/i915": "1", "gpu.intel.com/tiles": "1"}]) is None
+    assert filt([{"gpu.intel.com/tiles": "1"}, {"gpu.intel.com/i915": "1"}]) == ["node-1"]
+    assert filt([{"gpu.intel.com/i915": "1", "gpu.intel.com/memory.max": "1G"},
+                 {"gpu.intel.com/i915": "1", "gpu.intel.com/foo": "0"}]) is None

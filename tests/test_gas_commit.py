@@ -200,3 +200,67 @@ def test_bind_errors(ctx):
         ctx.gas_bind(gen, gen + 1, [0], [0], np.array([[[65]]], np.int64), mask, one, 0)
     assert e.value.code == pas_amd._lib.PAS_ECAPACITY
     assert ctx.gas_snapshot_get()[0] == gen
+
+
+@pytest.mark.gpu
+def test_fit_bind_fit_refreshes_kind_minima(ctx, oracle):
+    # The fit caches each kind's minimum free over the snapshot per epoch (kind skipping,
+    # gas_fit.hip).  Fit, then binds that exhaust card0's i915 on node 0 (the minimum drops
+    # from 2 to 0), then fit again on the same context: a stale minimum would skip the i915
+    # compare and pick card0; the reference picks card1.  Release restores it.
+    n_cards = np.full(4, 2, np.int32)
+    cap = np.tile(np.array([[2, 1000]], np.int64), (4, 1))
+    used = np.zeros((4, 2, 2), np.int64)
+    req = np.array([[[1, 10]]], np.int64)
+    mask = np.array([[3]], np.uint32)
+    ncont = np.ones(1, np.int32)
+    gen = _upload(ctx, n_cards, cap, used)
+    before = ctx.gas_fit(gen, req, mask, ncont, 0)
+    assert decode_gas_word(before[0, 0]) == (True, [0])
+    res, st = ctx.gas_bind(gen, gen + 1, [0, 0], [0, 0], req, mask, ncont, 0)
+    assert list(st) == [0, 0]
+    w_used, _, _ = oracle.gas_bind(n_cards, cap, used, req, mask, ncont, 0, [0, 0], [0, 0])
+    after = ctx.gas_fit(gen + 1, req, mask, ncont, 0)
+    want = oracle.gas_fit(n_cards, cap, w_used, req, mask, ncont, 0)
+    assert decode_gas_word(want[0, 0]) == (True, [1])
+    np.testing.assert_array_equal(after, want)
+    cpc = np.ones((2, 1), np.int32)
+    cards = np.zeros((2, 8), np.int32)
+    st2 = ctx.gas_release(gen + 1, gen + 2, [0, 0], [0, 0], req, mask, ncont, cpc, cards)
+    assert list(st2) == [0, 0]
+    again = ctx.gas_fit(gen + 2, req, mask, ncont, 0)
+    np.testing.assert_array_equal(again, before)
+
+
+@pytest.mark.gpu
+def test_unknown_kind_bind_release(ctx, oracle):
+    # a container flagged PAS_REQ_UNKNOWN_KIND (a gpu.intel.com/ kind the snapshot lacks):
+    # with numI915 > 0 the bind does not fit; with numI915 == 0 it binds with no cards; a
+    # release naming cards for such a container is errInput (subtractRM of a missing key)
+    unk = pas_amd._lib.PAS_REQ_UNKNOWN_KIND
+    n_cards = np.full(3, 2, np.int32)
+    cap = np.tile(np.array([[4, 1000]], np.int64), (3, 1))
+    used = np.zeros((3, 2, 2), np.int64)
+    req = np.array([[[1, 10], [0, 0]], [[0, 5], [1, 10]], [[1, 10], [1, 5]]], np.int64)
+    mask = np.array([[3 | unk, 0], [2 | unk, 3], [3, 3]], np.uint32)
+    ncont = np.array([1, 2, 2], np.int32)
+    gen = _upload(ctx, n_cards, cap, used)
+    pods, nodes = [0, 1, 2], [0, 1, 2]
+    res, st = ctx.gas_bind(gen, gen + 1, pods, nodes, req, mask, ncont, 0)
+    w_used, w_res, w_st = oracle.gas_bind(n_cards, cap, used, req, mask, ncont, 0, pods, nodes)
+    assert list(w_st) == [pas_amd._lib.PAS_GAS_WONT_FIT, 0, 0]
+    np.testing.assert_array_equal(res, w_res)
+    np.testing.assert_array_equal(st, w_st)
+    _, after = ctx.gas_snapshot_get()
+    np.testing.assert_array_equal(after, w_used)
+    rel_mask = mask.copy()
+    rel_mask[2, 0] |= unk  # the annotation names a card for a flagged container
+    cpc = np.array([[0, 1], [1, 1]], np.int32)
+    cards = np.zeros((2, 8), np.int32)
+    st2 = ctx.gas_release(gen + 1, gen + 2, [1, 2], [1, 2], req, rel_mask, ncont, cpc, cards)
+    w_back, w_st2 = oracle.gas_release(n_cards, w_used, req, rel_mask, ncont, [1, 2], [1, 2], cpc,
+                                       cards)
+    assert list(w_st2) == [0, pas_amd._lib.PAS_GAS_ERR_INPUT]
+    np.testing.assert_array_equal(st2, w_st2)
+    _, back = ctx.gas_snapshot_get()
+    np.testing.assert_array_equal(back, w_back)

@@ -211,3 +211,26 @@ def test_narrow_kind_boundary(ctx, oracle, cap_max):
     got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
     np.testing.assert_array_equal(got, want)
     assert 0.02 < (want >> 31).mean() < 0.98
+
+
+@pytest.mark.parametrize("k", [3, 8, 12])
+def test_unknown_kind_flag_parity(ctx, oracle, k):
+    # containers flagged PAS_REQ_UNKNOWN_KIND (they also request a gpu.intel.com/ kind the
+    # snapshot lacks): a pod with such a container and numI915 > 0 fits no node; with
+    # numI915 == 0 the flag changes nothing (scheduler.go:206-215, 349-354).  Single,
+    # multi-selection and (k = 12: nodes past 8 cards) generic kernels.
+    rng = np.random.default_rng(900 + k)
+    n_cards, cap, used, req, mask, ncont = random_gas(rng, 500, k, 3, 80, 4, i915=0)
+    flag = rng.random(mask.shape) < 0.15
+    mask = mask | np.where(flag, pas_amd._lib.PAS_REQ_UNKNOWN_KIND, 0).astype(np.uint32)
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
+    np.testing.assert_array_equal(got, want)
+    # pods whose flagged container selects a card never fit; flagged containers with no
+    # selection leave the pod's result as without the flag
+    sel = (req[:, :, 0] > 0) & ((mask & 1) == 1)
+    live = np.arange(mask.shape[1])[None, :] < ncont[:, None]
+    blocked = (flag & sel & live).any(axis=1)
+    assert blocked.any() and not (want[blocked] >> 31).any()
+    clean = oracle.gas_fit(n_cards, cap, used, req, mask & 0x7FFFFFFF, ncont, 0)
+    np.testing.assert_array_equal(want[~blocked], clean[~blocked])

@@ -228,3 +228,18 @@ def test_g11_gas_readme(oracle):
             if fits:
                 assert ",".join(cards[k] for k in sel) == want["annotation"]
                 commit_pod(used[0], req[0], mask[0], [sel])
+
+
+def test_unknown_kind_semantics(oracle):
+    # runSchedulingLogic with a gpu.intel.com/ key no capacity map has (scheduler.go:206-215,
+    # 341-383): numI915 > 0 -> checkResourceCapacity fails on every card -> errWontFit;
+    # numI915 == 0 -> no selection, the pod fits with an empty annotation segment
+    unk = 0x80000000
+    n_cards = np.array([2], np.int32)
+    cap = np.array([[4, 1000]], np.int64)
+    used = np.zeros((1, 2, 2), np.int64)
+    req = np.array([[[1, 10]], [[0, 10]], [[1, 10]]], np.int64)
+    mask = np.array([[3 | unk], [2 | unk], [3]], np.uint32)
+    got = oracle.gas_fit(n_cards, cap, used, req, mask, np.ones(3, np.int32), 0)
+    assert [int(w) >> 31 for w in got[:, 0]] == [0, 1, 1]
+    assert int(got[1, 0]) == 0x80000000  # fits, no cards

@@ -201,3 +201,13 @@ def test_gpu_device_entry_matches_host(ctx, oracle):
     k = int(len_t.item())
     np.testing.assert_array_equal(pos_t[:k].cpu().numpy(), want)
     assert (pos_t[k:] == -1).all()
+
+
+@pytest.mark.gpu
+def test_gpu_empty_snapshot_empty_request(ctx):
+    # N = 0 and n_req = 0: every workspace part is 0 bytes; the call is an empty list, not a
+    # sizing failure
+    gen = upload(ctx, np.zeros((1, 0), np.int64), np.zeros((1, 0), np.uint64))
+    assert len(ctx.tas_prioritize_request(gen, rule(0, 1), np.zeros(0, np.int32))) == 0
+    # unknown nodes only (req -1): nothing listed
+    assert len(ctx.tas_prioritize_request(gen, rule(0, 0), np.full(3, -1, np.int32))) == 0

@@ -260,6 +260,7 @@ def test_pod_requests_unknown_and_repeated():
            b'"gpu.intel.com/tiles":"2","gpu.intel.com/i915":"3"}}}]}}')
     req, mask, nc, unknown = wire.decode_pod_requests(pod, KINDS)
     assert unknown == 1 and req[0, 0, 0] == 3
+    assert mask[0, 0] == 1 | _lib.PAS_REQ_UNKNOWN_KIND  # flagged: no node has that key
     # containers is a slice: a repeated key decodes element-wise into the old containers
     pod = (b'{"spec":{"containers":[{"resources":{"requests":{"gpu.intel.com/i915":"1"}}},{}],'
            b'"containers":[null]}}')
@@ -270,3 +271,54 @@ def test_pod_requests_unknown_and_repeated():
     many = pod_with(*[{"gpu.intel.com/i915": "1"}] * 40).encode()  # grows past 16 containers
     req, mask, nc, _ = wire.decode_pod_requests(many, KINDS)
     assert nc[0] == 40 and (req[0, :, 0] == 1).all()
+
+
+def test_pod_requests_unknown_kind_flag_per_container():
+    # only the container that names a kind outside the list is flagged; a non-gpu.intel.com
+    # resource is not a GAS key at all (resourcePrefix, utils.go:9-12)
+    pod = pod_with({"gpu.intel.com/i915": "1"},
+                   {"gpu.intel.com/tiles": "1", "cpu": "1"},
+                   {"gpu.intel.com/tiles": "0", "gpu.intel.com/i915": "0"},
+                   {"memory": "1Gi"}).encode()
+    req, mask, nc, unknown = wire.decode_pod_requests(pod, KINDS)
+    assert nc[0] == 4 and unknown == 2
+    u = _lib.PAS_REQ_UNKNOWN_KIND
+    assert list(mask[0]) == [1, u, 1 | u, 0]
+
+
+@pytest.mark.parametrize("meta", [
+    b'{"labels":{"app":5}}', b'{"labels":{"telemetry-policy":"p","x":true}}',
+    b'{"annotations":{"a":{}}}', b'{"labels":[]}', b'{"annotations":7}'])
+def test_pod_metadata_maps_type_checked(meta):
+    # ObjectMeta labels / annotations are map[string]string: a non-string value anywhere
+    # fails json.Decode (TAS: empty body; GAS: 404), not only under the policy label
+    pod = b'{"metadata":' + meta + b',"spec":{"containers":[]}}'
+    with pytest.raises(_lib.PasError) as e:
+        wire.decode_pod_policy(pod, "telemetry-policy")
+    assert e.value.code == _lib.PAS_EDECODE
+    with pytest.raises(_lib.PasError) as e:
+        wire.decode_pod_requests(pod, KINDS)
+    assert e.value.code == _lib.PAS_EDECODE
+
+
+def test_pod_metadata_maps_null_values_ok():
+    pod = (b'{"metadata":{"namespace":"ns","labels":{"a":null,"telemetry-policy":"p"},'
+           b'"annotations":null},"spec":{"containers":[]}}')
+    assert wire.decode_pod_policy(pod, "telemetry-policy") == ("ns", "p")
+    assert wire.decode_pod_requests(pod, KINDS)[2][0] == 0
+
+
+@pytest.mark.parametrize("limits,ok", [
+    (b'{"cpu":"2","gpu.intel.com/i915":"1"}', True), (b'null', True),
+    (b'{"cpu":"abc"}', False), (b'{"memory":true}', False), (b'[]', False)])
+def test_container_limits_validated(limits, ok):
+    # ResourceRequirements.limits is a ResourceList too: every Quantity is parsed on decode
+    pod = (b'{"spec":{"containers":[{"resources":{"limits":' + limits +
+           b',"requests":{"gpu.intel.com/i915":"1"}}}]}}')
+    if ok:
+        req, mask, nc, _ = wire.decode_pod_requests(pod, KINDS)
+        assert nc[0] == 1 and mask[0, 0] == 1 and req[0, 0, 0] == 1
+    else:
+        with pytest.raises(_lib.PasError) as e:
+            wire.decode_pod_requests(pod, KINDS)
+        assert e.value.code == _lib.PAS_EDECODE
