@@ -512,62 +512,128 @@ def bench_deschedule(args, world, rank):
 
 # ------------------------------------------------------------------------------- C5
 
-def bench_c5(args, world, rank):
-    """configs[4]: TAS+GAS over a node-sharded cluster: per rank, the GAS fit bitmaps of its
-    nodes become the TAS candidates, the TAS filter + prioritize keeps each pod's first k
-    nodes of the shard, and the records of all ranks are all-gathered (RCCL) and merged into
-    the cluster's first k per pod (strong scaling: the cluster is fixed)."""
-    P, N, M, R, K = args.pods, args.nodes, args.metrics, args.rules - 1, args.topk
+def c5_setup(args, world, rank):
+    """The C5 workload on this rank: its node range of the cluster as resident TAS and GAS
+    snapshots (generations 1 and 2), the pod batch on the device."""
+    P, N, M, R = args.pods, args.nodes, args.metrics, args.rules - 1
     ctx = pas_amd.Context(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
     n0, n1 = shard.node_range(N, world, rank)
-    n_local = n1 - n0
     tsnap = wl.make_tas_snapshot(N, M, seed=0xC5)
     v, pres = shard_tas(tsnap, n0, n1)
-    ctx.tas_snapshot_set_device(1, n_local, M, dev(v), dev(pres.view(np.int64)), stream)
+    ctx.tas_snapshot_set_device(1, n1 - n0, M, dev(v), dev(pres.view(np.int64)), stream)
     tbatch = wl.make_tas_batch(tsnap, P, R, seed=0xC5)
     del tsnap, v, pres
     gsnap = wl.make_gas_snapshot(N, seed=0xC5)
-    ctx.gas_snapshot_set_device(2, n_local, gsnap.used.shape[1], gsnap.used.shape[2],
+    ctx.gas_snapshot_set_device(2, n1 - n0, gsnap.used.shape[1], gsnap.used.shape[2],
                                 dev(gsnap.n_cards[n0:n1]), dev(gsnap.cap[n0:n1]),
                                 dev(gsnap.used[n0:n1]), stream)
     gbatch = wl.make_gas_batch(P, seed=0xC5)
     del gsnap
-    rules_t, off_t = dev(tbatch.rules.view(np.uint8)), dev(tbatch.rule_off)
-    prio_t = dev(tbatch.prio.view(np.uint8))
-    req_t, mask_t = dev(gbatch.req), dev(gbatch.req_mask.view(np.int32))
-    nc_t = dev(gbatch.n_containers)
-    fit_t = torch.empty((P, pas_amd.w64(n_local)), dtype=torch.int64, device="cuda")
-    topk = shard.ShardedTopK(ctx, K, world, rank, n0)
+    t = {"rules": dev(tbatch.rules.view(np.uint8)), "off": dev(tbatch.rule_off),
+         "prio": dev(tbatch.prio.view(np.uint8)), "req": dev(gbatch.req),
+         "mask": dev(gbatch.req_mask.view(np.int32)), "ncont": dev(gbatch.n_containers),
+         "n_rules": len(tbatch.rules), "C": gbatch.req.shape[1]}
+    return ctx, stream, n0, n1, t
+
+
+def c5_step_fn(ctx, stream, topk, P, t):
+    """One C5 step: the rank's combined TAS + GAS records along each pod's order
+    (pas_tas_gas_topk_device), all-gathered and merged into every pod's global first k."""
     result = {}
 
     def step():
-        ctx.gas_fit_bitmap_device(2, P, gbatch.req.shape[1], wl.I915, req_t, mask_t, nc_t, fit_t,
-                                  stream)
-        result["nodes"], result["len"] = topk.run(1, P, len(tbatch.rules), rules_t, off_t,
-                                                  prio_t, fit_t, stream)
+        result["nodes"], result["len"] = topk.run_tas_gas(
+            1, 2, P, t["n_rules"], t["rules"], t["off"], t["prio"], t["C"], wl.I915, t["req"],
+            t["mask"], t["ncont"], stream=stream)
+    return step, result
 
+
+def bench_c5(args, world, rank):
+    """configs[4]: TAS+GAS over a node-sharded cluster: per rank, each pod's first k nodes of
+    the shard that pass its dontschedule filter and fit its GPU request, evaluated along the
+    pod's prioritize order until k are kept (pas_tas_gas_topk_device); the records of all
+    ranks are all-gathered (RCCL) and merged into the cluster's first k per pod (strong
+    scaling: the cluster is fixed).  value = pods whose top-k list is produced per second;
+    the (pod, node) pairs actually evaluated are reported beside it, never counted as the
+    P x N evaluations the composed path would perform."""
+    P, N, M, R, K = args.pods, args.nodes, args.metrics, args.rules - 1, args.topk
+    ctx, stream, n0, n1, t = c5_setup(args, world, rank)
+    topk = shard.ShardedTopK(ctx, K, world, rank, n0)
+    step, result = c5_step_fn(ctx, stream, topk, P, t)
     settle_steps = distrib.settle(step, args.settle)
     for _ in range(args.warmup):
         step()
-    elapsed = timed_steps(step, args.steps, 0, world)
+    gpu = {}
+    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu)
+    # the combined kernel alone, from extra untimed steps (events around the launch)
+    ctx.reset_timing()
+    ctx.set_timing(2)
+    n_detail = min(args.steps, 5)
+    for _ in range(n_detail):
+        step()
+    ctx.set_timing(0)
+    k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_GAS_TOPK)
     out = {
-        "metric": "combined TAS+GAS pod-node evals/sec, node-sharded, per-pod top-k merge",
-        "value": P * N * args.steps / elapsed,
-        "unit": "pod-node evals/s",
+        "metric": "combined TAS+GAS per-pod top-k lists/sec, 64k pods x 1M nodes, node-sharded",
+        "value": P * args.steps / elapsed,
+        "unit": "pods/s (top-k HostPriorityLists)",
         "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "int64",
         "data": "synthetic (SURVEY.md §8(d) C5)",
-        "config": {"settle_steps": settle_steps, "workload": "tas_gas_topk_node_sharded (BASELINE configs[4])", "pods": P,
-                   "nodes": N, "nodes_per_gpu": n_local, "metrics": M, "rules_per_pod": R + 1,
+        "config": {"settle_steps": settle_steps,
+                   "workload": "tas_gas_topk_node_sharded (BASELINE configs[4])", "pods": P,
+                   "nodes": N, "nodes_per_gpu": n1 - n0, "metrics": M, "rules_per_pod": R + 1,
                    "topk": K, "parallelism": f"node-sharded x{world}, top-k records "
                                              "all-gathered and merged",
+                   "step": "pas_tas_gas_topk_device (filter + fit along each pod's order until "
+                           "k kept) + all-gather + pas_topk_merge_device",
+                   "topk_kernel_ms": k_ms / max(k_n, 1),
+                   "gpu_ms_per_step": gpu["ms_per_step"],
                    "mean_list_len": float(result["len"].float().mean().item())},
     }
     ctx.close()
     return out
+
+
+def node_sharded_record(args, world, rank):
+    """The north_star's 1M-node scaling point, run inside a multi-GPU bench.py call: the C5
+    step (64k pods x 1M nodes, node-sharded over the ranks, RCCL all-gather + merge) and the
+    C4 deschedule sweep (1M nodes x 64 rules + all-gather of the violation bitmaps), each
+    timed with the same barrier / max-over-ranks protocol.  The driver's 1/2/4/8 runs of
+    bench.py then carry the node-sharded curve without a --workload flag."""
+    import argparse as _ap
+    import torch.distributed as dist
+    rec = {"nodes": 1_000_000, "world_size": world,
+           "backend": dist.get_backend() if world > 1 else None}
+    a = _ap.Namespace(**vars(args))
+    a.pods, a.nodes, a.steps, a.warmup, a.settle = args.ns_pods, args.ns_nodes, 10, 2, 0.1
+    rec["nodes"] = a.nodes
+    ctx, stream, n0, n1, t = c5_setup(a, world, rank)
+    topk = shard.ShardedTopK(ctx, a.topk, world, rank, n0)
+    step, result = c5_step_fn(ctx, stream, topk, a.pods, t)
+    for _ in range(a.warmup):
+        step()
+    el = timed_steps(step, a.steps, 0, world)
+    # every rank ends the step with the same merged lists (all-gather + identical merge)
+    digest = (int(result["nodes"].to(torch.int64).sum().item()),
+              int(result["len"].to(torch.int64).sum().item()))
+    rec["c5_topk"] = {"pods": a.pods, "nodes_per_gpu": n1 - n0, "topk": a.topk,
+                      "ms_per_step": el / a.steps * 1e3,
+                      "pods_per_s": a.pods * a.steps / el, "scaling": "strong",
+                      "entries": digest[1],
+                      "ranks_agree": len(set(distrib.gather_objects(digest, world))) == 1}
+    ctx.close()
+    del topk, t, result
+    torch.cuda.empty_cache()
+    d = bench_deschedule(a, world, rank)
+    rec["c4_deschedule"] = {"nodes_per_gpu": d["config"]["nodes_per_gpu"],
+                            "ms_per_step": d["ms_per_step"],
+                            "node_rule_evals_per_s": d["value"],
+                            "sweep_kernel_ms": d["roofline"]["kernel_ms"], "scaling": "strong"}
+    return rec
 
 
 def bench_launch_check(args, world, rank):
@@ -601,6 +667,15 @@ def main():
     ap.add_argument("--settle", type=float, default=0.3,
                     help="seconds of untimed steps before the warmup steps (clocks settle)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-node-sharded", action="store_true",
+                    help="with --gpus N > 1: skip the node-sharded 1M-node sub-record")
+    ap.add_argument("--ns-pods", type=int, default=65_536,
+                    help="pods of the node-sharded sub-record's C5 step")
+    ap.add_argument("--ns-nodes", type=int, default=1_000_000,
+                    help="cluster nodes of the node-sharded sub-record")
+    ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
+                    help="collective backend of a multi-rank run (auto: RCCL on GPUs); gloo "
+                         "lets several ranks share one GPU (tests)")
     ap.add_argument("--no-request-latency", action="store_true",
                     help="skip the f2 request-latency leg of the TAS workload")
     args = ap.parse_args()
@@ -623,7 +698,10 @@ def main():
         out = bench_launch_check(args, world, rank)
     else:
         _load_package()
-        world, rank, _ = distrib.setup()
+        world, rank, _ = distrib.setup(None if args.backend == "auto" else args.backend)
+        if args.backend == "gloo" and torch.cuda.is_available():
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0"))
+                                  % torch.cuda.device_count())
         # a stream of our own (not the null stream): libpas launches on it, and the timing
         # events of distrib.timed_steps are recorded on it
         torch.cuda.set_stream(torch.cuda.Stream())
@@ -634,6 +712,10 @@ def main():
             import torch.distributed as dist
             out["config"]["world_size"] = dist.get_world_size()
             out["config"]["backend"] = dist.get_backend()
+            if args.workload == "tas" and not args.no_node_sharded:
+                # the north_star's node-sharded curve at 1M nodes rides on every multi-GPU
+                # run of the headline workload (the N = 1 line is unchanged)
+                out["node_sharded"] = node_sharded_record(args, world, rank)
     if rank == 0:
         print(json.dumps(out), flush=True)
     distrib.teardown(world)

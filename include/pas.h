@@ -418,6 +418,24 @@ int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
                         int32_t node_base, int64_t* d_top_key, int32_t* d_top_node,
                         int32_t* d_top_len, void* hip_stream);
 
+/* The same records for the combined TAS + GAS filter (BASELINE configs[4]): the first k
+ * entries of the shard's HostPriorityList over the nodes that pass the pod's dontschedule
+ * filter (and d_cand when given) AND fit its GPU request (runSchedulingLogic on the
+ * context's resident GAS snapshot of the same nodes, gpuscheduler/scheduler.go:280-338).
+ * Equal to pas_gas_fit_bitmap_device over the shard followed by pas_tas_topk_device with
+ * the fit bitmaps (intersected with d_cand) as candidates, but evaluated along each pod's
+ * order: a node is filtered and fitted only until k nodes are kept, so a pod costs about
+ * k / (pass rate) node evaluations instead of the shard's n_nodes.  The GAS arguments are
+ * those of pas_gas_fit_device; a pod past PAS_GAS_MAX_SELECTIONS fits no node (len 0).  The
+ * two snapshots must hold the same number of nodes (PAS_EINVAL otherwise). */
+int pas_tas_gas_topk_device(pas_ctx* ctx, uint64_t tas_gen, uint64_t gas_gen, int32_t n_pods,
+                            int32_t n_rules, const pas_rule* d_rules, const int32_t* d_rule_off,
+                            const pas_rule* d_prio, const uint64_t* d_cand,
+                            int32_t max_containers, int32_t i915_index, const int64_t* d_req,
+                            const uint32_t* d_req_mask, const int32_t* d_n_containers,
+                            int32_t k, int32_t node_base, int64_t* d_top_key,
+                            int32_t* d_top_node, int32_t* d_top_len, void* hip_stream);
+
 /* Merge of n_shards record sets laid out [n_shards][n_pods][k] (the layout of an
  * all-gather of the per-shard top_key / top_node): out_node[n_pods][k] = the k smallest
  * (key, node) records' nodes in order (-1 past out_len), out_len = min(k, records). */
@@ -537,7 +555,8 @@ int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
 #define PAS_K_TAS_LABELS 6     /* deschedule label plan */
 #define PAS_K_TAS_SPAN 7       /* whole pas_tas_eval path: first launch start to last launch end */
 #define PAS_K_PRIO_REQUEST 8   /* whole pas_tas_prioritize_request path (keys, sort, positions) */
-#define PAS_K_COUNT 9
+#define PAS_K_TAS_GAS_TOPK 9   /* combined TAS + GAS top-k along each pod's order */
+#define PAS_K_COUNT 10
 #define PAS_TIMING_SPAN 1    /* whole paths: PAS_K_TAS_SPAN, PAS_K_PRIO_REQUEST, the GAS fit and
                                 deschedule launches */
 #define PAS_TIMING_KERNELS 2 /* every launch (events between launches add small gaps) */

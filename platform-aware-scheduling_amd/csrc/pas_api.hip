@@ -1066,6 +1066,35 @@ int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
                          pick_stream(ctx, hip_stream));
 }
 
+int pas_tas_gas_topk_device(pas_ctx* ctx, uint64_t tas_gen, uint64_t gas_gen, int32_t n_pods,
+                            int32_t n_rules, const pas_rule* d_rules, const int32_t* d_rule_off,
+                            const pas_rule* d_prio, const uint64_t* d_cand,
+                            int32_t max_containers, int32_t i915_index, const int64_t* d_req,
+                            const uint32_t* d_req_mask, const int32_t* d_n_containers,
+                            int32_t k, int32_t node_base, int64_t* d_top_key,
+                            int32_t* d_top_node, int32_t* d_top_len, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, tas_gen);
+  if (rc) return rc;
+  if ((rc = check_gas_gen(ctx, gas_gen))) return rc;
+  if (ctx->gas.n_nodes != ctx->tas.n_nodes)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_gas_topk_device: TAS and GAS snapshots differ "
+                                      "in node count");
+  if (n_pods < 0 || n_rules < 0 || k < 1 || node_base < 0 || max_containers < 0 ||
+      i915_index >= ctx->gas.n_res || i915_index < -1)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_gas_topk_device: bad shape");
+  if ((int64_t)node_base + ctx->tas.n_nodes > INT32_MAX)
+    return set_error(ctx, PAS_EINVAL, "pas_tas_gas_topk_device: node ids past int32");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_rule_off || !d_prio || (n_rules > 0 && !d_rules) || !d_top_key || !d_top_node ||
+      !d_top_len || !d_n_containers || (max_containers > 0 && (!d_req || !d_req_mask)))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_gas_topk_device: null argument");
+  if ((rc = activate(ctx))) return rc;
+  return tas_gas_topk_launch(ctx, n_pods, d_rules, d_rule_off, d_prio, d_cand, max_containers,
+                             i915_index, d_req, d_req_mask, d_n_containers, k, node_base,
+                             d_top_key, d_top_node, d_top_len, pick_stream(ctx, hip_stream));
+}
+
 int pas_topk_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
                           const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
                           int32_t* d_out_len, void* hip_stream) {

@@ -164,6 +164,12 @@ int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
                     int32_t k, int32_t node_base, int64_t* d_key, int32_t* d_node,
                     int32_t* d_len, hipStream_t s);
+int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
+                        const int32_t* d_rule_off, const pas_rule* d_prio,
+                        const uint64_t* d_cand, int32_t max_containers, int32_t i915_index,
+                        const int64_t* d_req, const uint32_t* d_req_mask,
+                        const int32_t* d_n_containers, int32_t k, int32_t node_base,
+                        int64_t* d_key, int32_t* d_node, int32_t* d_len, hipStream_t s);
 int topk_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
                       const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
                       int32_t* d_out_len, hipStream_t s);

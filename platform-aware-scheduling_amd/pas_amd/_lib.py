@@ -66,6 +66,7 @@ PAS_K_TAS_PREP = 5
 PAS_K_TAS_LABELS = 6
 PAS_K_TAS_SPAN = 7
 PAS_K_PRIO_REQUEST = 8
+PAS_K_TAS_GAS_TOPK = 9
 KERNEL_NAMES = {
     PAS_K_TAS_LABELS: "label_plan_kernel",
     PAS_K_TAS_EVAL: "tas_eval_kernel",
@@ -75,6 +76,7 @@ KERNEL_NAMES = {
     PAS_K_TAS_PREP: "tas_prep_kernel",
     PAS_K_TAS_SPAN: "tas_eval_span",
     PAS_K_PRIO_REQUEST: "prio_request_span",
+    PAS_K_TAS_GAS_TOPK: "tas_gas_topk_kernel",
 }
 
 
@@ -180,6 +182,11 @@ SIGNATURES = {
     "pas_tas_topk_device": (
         c_int,
         [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_int32, c_int32, _P, _P, _P, _P],
+    ),
+    "pas_tas_gas_topk_device": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, c_int32, _P, _P, _P, _P, c_int32, c_int32, _P, _P, _P,
+         c_int32, c_int32, _P, _P, _P, _P],
     ),
     "pas_topk_merge_device": (c_int, [_P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P]),
     "pas_encode_host_priority_list": (

@@ -453,6 +453,19 @@ class Context:
                                          _stream(stream))
         self._check(rc, "pas_tas_topk_device")
 
+    def tas_gas_topk_device(self, tas_gen: int, gas_gen: int, n_pods: int, n_rules: int, rules_t,
+                            rule_off_t, prio_t, cand_t, max_containers: int, i915_index: int,
+                            req_t, mask_t, ncont_t, k: int, node_base: int, key_t, node_t, len_t,
+                            stream=None):
+        """The same records over the nodes that pass TAS and fit the pod's GPU request
+        (pas_tas_gas_topk_device: evaluated along each pod's order until k are kept)."""
+        rc = self._l.pas_tas_gas_topk_device(
+            self._h, tas_gen, gas_gen, n_pods, n_rules, _dptr(rules_t), _dptr(rule_off_t),
+            _dptr(prio_t), _dptr(cand_t), max_containers, i915_index, _dptr(req_t),
+            _dptr(mask_t), _dptr(ncont_t), k, node_base, _dptr(key_t), _dptr(node_t),
+            _dptr(len_t), _stream(stream))
+        self._check(rc, "pas_tas_gas_topk_device")
+
     def topk_merge_device(self, n_pods: int, k: int, n_shards: int, keys_t, nodes_t, out_node_t,
                           out_len_t, stream=None):
         """Merge of [n_shards][P][k] records into the global first-k lists."""

@@ -7,9 +7,9 @@ the prioritize order (core.OrderedList, operator.go:30-42) is global.  So each r
 contiguous node range of the cluster as its resident snapshot and:
 
   * top-k prioritize: evaluates every pod against its shard, keeps the first k entries of
-    the shard's HostPriorityList as (key, global node) records (pas_tas_topk_device), the
-    records of all ranks are all-gathered over RCCL, and every rank merges them into the
-    exact global first k (pas_topk_merge_device);
+    the shard's HostPriorityList as (key, global node) records (pas_tas_topk_device, or
+    pas_tas_gas_topk_device for TAS + GAS), the records of all ranks are all-gathered over
+    RCCL, and every rank merges them into the exact global first k (pas_topk_merge_device);
   * deschedule sweep: sweeps its shard's nodes and all-gathers the violation bitmaps
     (S x W64 words per shard; shard ranges are multiples of 64 nodes so the words of all
     ranks concatenate into the cluster bitmap).
@@ -74,6 +74,25 @@ class ShardedTopK:
         """`stream`: the torch.cuda.Stream the kernels run on (None = torch's current stream).
         The collectives run on torch's current stream, so the two are ordered with
         wait_stream in both directions when they differ."""
+        def records(key, node, ln, s):
+            self.ctx.tas_topk_device(gen, n_pods, n_rules, rules_t, rule_off_t, prio_t, cand_t,
+                                     self.k, self.node_base, key, node, ln, s)
+        return self._run(n_pods, records, stream)
+
+    def run_tas_gas(self, tas_gen: int, gas_gen: int, n_pods: int, n_rules: int, rules_t,
+                    rule_off_t, prio_t, max_containers: int, i915_index: int, req_t, mask_t,
+                    ncont_t, cand_t=None, stream=None):
+        """The combined TAS + GAS top-k (BASELINE configs[4]): the shard's records over the
+        nodes that pass the pod's dontschedule filter and fit its GPU request
+        (pas_tas_gas_topk_device on the rank's resident TAS and GAS snapshots), merged."""
+        def records(key, node, ln, s):
+            self.ctx.tas_gas_topk_device(tas_gen, gas_gen, n_pods, n_rules, rules_t, rule_off_t,
+                                         prio_t, cand_t, max_containers, i915_index, req_t,
+                                         mask_t, ncont_t, self.k, self.node_base, key, node, ln,
+                                         s)
+        return self._run(n_pods, records, stream)
+
+    def _run(self, n_pods, records, stream):
         k = self.k
         on_gpu = torch.cuda.is_available() and str(self.device).startswith("cuda")
         cur = torch.cuda.current_stream() if on_gpu else None
@@ -84,8 +103,7 @@ class ShardedTopK:
         ln = self._buf("len", (n_pods,), torch.int32)
         if on_gpu and stream != cur:
             stream.wait_stream(cur)  # the caller's inputs (rules, candidates) are written
-        self.ctx.tas_topk_device(gen, n_pods, n_rules, rules_t, rule_off_t, prio_t, cand_t, k,
-                                 self.node_base, key, node, ln, stream)
+        records(key, node, ln, stream)
         if on_gpu and stream != cur:
             cur.wait_stream(stream)  # records written before the all-gather reads them
         keys_all = _all_gather(key, self.world)

@@ -59,3 +59,29 @@ def test_failing_rank_fails_the_launch():
     code = "import os, sys, time; r = int(os.environ['RANK']); time.sleep(0.2); sys.exit(3 if r == 1 else 0)"
     assert d.launch_local_ranks(2, [sys.executable, "-c", code]) == 3
     assert d.launch_local_ranks(3, [sys.executable, "-c", "import os; assert os.environ['WORLD_SIZE'] == '3'"]) == 0
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_multi_rank_bench_carries_node_sharded_record():
+    """`bench.py --gpus 2` of the headline workload: rank 0's line carries the node-sharded
+    sub-record (C5 top-k + C4 sweep over a node-sharded cluster, all-gathers across the
+    ranks).  Two ranks share the box's one GPU, so the collectives run over gloo here; the
+    driver's 8-GPU node runs the same code over RCCL."""
+    r = _run(["--gpus", "2", "--backend", "gloo", "--pods", "256", "--nodes", "20000",
+              "--ns-pods", "1024", "--ns-nodes", "60000", "--steps", "3", "--warmup", "1",
+              "--settle", "0", "--no-cpu-baseline", "--no-request-latency"])
+    assert r.returncode == 0, r.stderr[-4000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    out = lines[0]
+    assert out["n_gpus"] == 2 and out["config"]["world_size"] == 2
+    ns = out["node_sharded"]
+    assert ns["world_size"] == 2 and ns["backend"] == "gloo" and ns["nodes"] == 60000
+    c5 = ns["c5_topk"]
+    assert c5["pods"] == 1024 and c5["nodes_per_gpu"] == 30016 and c5["ranks_agree"]
+    assert c5["ms_per_step"] > 0 and 0 < c5["entries"] <= 1024 * 16
+    c4 = ns["c4_deschedule"]
+    assert c4["nodes_per_gpu"] == 30016 and c4["ms_per_step"] > 0

@@ -3,13 +3,16 @@
 * C3 (configs[2]): the whole 10k-pod x 50k-node GAS batch the bench times, every
   (pod, node) word bit-exact against oracle.gas_fit (scheduler.go:280-383), and the fit
   bitmaps of pas_gas_fit_bitmap_device equal to bit 31 of the words.
-* C5 (configs[4]): 64k pods x 1M nodes, TAS + GAS combined as bench.py runs it: the GAS fit
-  bitmaps of a node range become the TAS candidates, each range keeps its pods' first k
-  HostPriorityList entries (pas_tas_topk_device) and the ranges are merged
-  (pas_topk_merge_device).  Checked
+* C5 (configs[4]): 64k pods x 1M nodes, TAS + GAS combined: each node range keeps its
+  pods' first k HostPriorityList entries over the nodes that pass TAS and fit GAS, and the
+  ranges are merged (pas_topk_merge_device).  Two ways to a range's records: the GAS fit
+  bitmaps as TAS candidates of pas_tas_topk_device (every (pod, node) evaluated), and
+  pas_tas_gas_topk_device (bench.py's step: evaluated along each pod's order until k are
+  kept).  Checked
     - for a 128-pod sample, bit-exact against the oracle composition oracle.gas_fit ->
       candidate bitmap -> oracle.tas_eval (telemetryscheduler.go:128-149,184-225) -> first k;
-    - for all 65,536 pods: the 8-range merge equals the whole-cluster (one range) lists, and
+    - for all 65,536 pods: the 8-range merge equals the whole-cluster (one range) lists, the
+      lazy path equals the composed one (1 and 8 ranges), and
       len = min(k, |fit AND pass AND present|), entries unique, every entry fits / passes /
       has the metric, order ascending in (key, node) (the documented tie rule, pas.h).
 The collectives of the multi-rank path are covered over gloo in test_shard.py; here the
@@ -100,9 +103,11 @@ class _C5:
         self.gsnap = wl.make_gas_snapshot(N, seed=0xC5)
         self.gbatch = wl.make_gas_batch(P, seed=0xC5)
 
-    def run_ranges(self, world):
+    def run_ranges(self, world, lazy=False):
         """(nodes [P][k], lens [P], fit bitmaps of the whole cluster [P][W64] or None) over
-        `world` node ranges, each in its own context, merged on the device."""
+        `world` node ranges, each in its own context, merged on the device.  lazy: the
+        combined top-k along each pod's order (pas_tas_gas_topk_device, bench.py's C5 step)
+        instead of fit bitmaps -> pas_tas_topk_device."""
         P, N, k = self.P, self.N, self.k
         t, g = self.tsnap, self.gsnap
         rules_t, off_t = _dev(self.tbatch.rules.view(np.uint8)), _dev(self.tbatch.rule_off)
@@ -122,11 +127,19 @@ class _C5:
                 c.gas_snapshot_set_device(2, nl, g.used.shape[1], g.used.shape[2],
                                           _dev(g.n_cards[n0:n1]), _dev(g.cap[n0:n1]),
                                           _dev(g.used[n0:n1]), s)
-                fit_t = torch.empty((P, pas_amd.w64(nl)), dtype=torch.int64, device="cuda")
-                c.gas_fit_bitmap_device(2, P, C, wl.I915, req_t, mask_t, nc_t, fit_t, s)
                 key = torch.empty((P, k), dtype=torch.int64, device="cuda")
                 node = torch.empty((P, k), dtype=torch.int32, device="cuda")
                 ln = torch.empty(P, dtype=torch.int32, device="cuda")
+                if lazy:
+                    c.tas_gas_topk_device(1, 2, P, len(self.tbatch.rules), rules_t, off_t, prio_t,
+                                          None, C, wl.I915, req_t, mask_t, nc_t, k, n0, key, node,
+                                          ln, s)
+                    torch.cuda.synchronize()
+                    keys.append(key)
+                    nodes.append(node)
+                    continue
+                fit_t = torch.empty((P, pas_amd.w64(nl)), dtype=torch.int64, device="cuda")
+                c.gas_fit_bitmap_device(2, P, C, wl.I915, req_t, mask_t, nc_t, fit_t, s)
                 c.tas_topk_device(1, P, len(self.tbatch.rules), rules_t, off_t, prio_t, fit_t, k,
                                   n0, key, node, ln, s)
                 if world == 1:  # pass bitmaps of the whole cluster for the property checks
@@ -152,8 +165,9 @@ def c5():
 
 
 def test_c5_sample_vs_oracle_composition(c5, oracle):
-    """128 pods of the C5 batch: GPU merged lists (8 ranges) == oracle composition."""
-    nodes8, lens8, _ = c5.run_ranges(8)
+    """128 pods of the C5 batch: GPU merged lists (8 ranges, the lazy combined top-k bench.py
+    times) == oracle composition."""
+    nodes8, lens8, _ = c5.run_ranges(8, lazy=True)
     nodes8, lens8 = nodes8.cpu().numpy(), lens8.cpu().numpy()
     sample = np.arange(0, c5.P, c5.P // 128)
     t, g, tb, gb = c5.tsnap, c5.gsnap, c5.tbatch, c5.gbatch
@@ -188,6 +202,11 @@ def test_c5_full_batch_properties(c5):
     nodes8, lens8, _ = c5.run_ranges(8)
     assert torch.equal(lens1, lens8)
     assert torch.equal(nodes1, nodes8)
+    # the lazy combined top-k (bench.py's C5 step), whole cluster and 8 ranges: every pod
+    for world in (1, 8):
+        lz_nodes, lz_lens, _ = c5.run_ranges(world, lazy=True)
+        assert torch.equal(lz_lens, lens1), world
+        assert torch.equal(lz_nodes, nodes1), world
     # every pass bit is also a fit bit (pass = cand AND NOT violated)
     assert not bool(((pass_t & ~fit_t) != 0).any())
     vals = _dev(c5.tsnap.v_milli)

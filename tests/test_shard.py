@@ -315,3 +315,68 @@ def test_sharded_topk_two_ranks_one_gpu(tmp_path, oracle):
             m = min(12, int(lens[p]))
             assert ln[p] == m
             np.testing.assert_array_equal(nodes[p, :m], order[p, :m])
+
+
+def _lazy_vs_composed(ctx, v, pres, batch, gsnap, gbatch, cand, k, node_base, i915):
+    """pas_tas_gas_topk_device vs pas_gas_fit_bitmap_device -> pas_tas_topk_device on one
+    context (both device paths), records and lengths."""
+    P = len(batch.prio)
+    n = v.shape[1]
+    gen_t, gen_g = 4101, 4102
+    ctx.tas_snapshot_set(gen_t, v, pres)
+    ctx.gas_snapshot_set(gen_g, gsnap.n_cards, gsnap.cap, gsnap.used)
+    rules_t, off_t, prio_t, cand_t = _rule_tensors(batch, cand)
+    req_t, mask_t = _dev(gbatch.req), _dev(gbatch.req_mask.view(np.int32))
+    nc_t = _dev(gbatch.n_containers)
+    C = gbatch.req.shape[1]
+    fit_t = torch.empty((P, (n + 63) // 64), dtype=torch.int64, device="cuda")
+    ctx.gas_fit_bitmap_device(gen_g, P, C, i915, req_t, mask_t, nc_t, fit_t)
+    if cand_t is not None:
+        fit_t &= cand_t
+    out = []
+    for lazy in (False, True):
+        key = torch.empty((P, k), dtype=torch.int64, device="cuda")
+        node = torch.empty((P, k), dtype=torch.int32, device="cuda")
+        ln = torch.empty(P, dtype=torch.int32, device="cuda")
+        if lazy:
+            ctx.tas_gas_topk_device(gen_t, gen_g, P, len(batch.rules), rules_t, off_t, prio_t,
+                                    cand_t, C, i915, req_t, mask_t, nc_t, k, node_base, key,
+                                    node, ln)
+        else:
+            ctx.tas_topk_device(gen_t, P, len(batch.rules), rules_t, off_t, prio_t, fit_t, k,
+                                node_base, key, node, ln)
+        ctx.synchronize()
+        out.append((key.cpu().numpy(), node.cpu().numpy(), ln.cpu().numpy()))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,n,cards,cand_frac", [(16, 5000, 8, None), (1, 3000, 8, 0.7),
+                                                 (70, 4200, 8, 0.9), (300, 2000, 3, None),
+                                                 (16, 3000, 12, 0.8)])
+def test_tas_gas_topk_equals_composition(ctx, k, n, cards, cand_frac):
+    """The lazy combined top-k equals GAS fit bitmaps -> TAS top-k (the composed C5 path):
+    records (key, global node) and lengths, with candidate masks, ties and Equals pods,
+    unknown-kind containers, pods with no fitting node and nodes of 9-16 cards."""
+    from pas_amd import workload as wl
+    from test_gas_gpu import random_gas
+    snap, batch = make_case(0x60 + k + cards, n, 6, 96, 7, cand_frac=cand_frac)
+    rng = np.random.default_rng(k * 7 + n)
+    if cards == 8:
+        gsnap = wl.make_gas_snapshot(n, seed=0x61 + k)
+        gbatch = wl.make_gas_batch(96, seed=0x61 + k)
+        i915 = wl.I915
+    else:
+        nc, cap, used, req, mask, ncont = random_gas(rng, n, cards, 3, 96, 4, i915=0)
+        cap *= 4  # roomy enough that most pods fit somewhere
+        req[0, 0, 0], mask[0, 0], ncont[0] = 70, 1, max(ncont[0], 1)  # past 64 selections
+        gsnap, gbatch = wl.GasSnapshotData(nc, cap, used), wl.GasBatch(req, mask, ncont)
+        i915 = 0
+    flag = rng.random(gbatch.req_mask.shape) < 0.05
+    gbatch.req_mask = gbatch.req_mask | np.where(flag, 0x80000000, 0).astype(np.uint32)
+    batch.prio["metric"][::17] = 99  # no scheduling rule: empty list
+    composed, lazy = _lazy_vs_composed(ctx, snap.v_milli, snap.present, batch, gsnap, gbatch,
+                                       batch.cand, k, 1234, i915)
+    for a, b in zip(composed, lazy):
+        np.testing.assert_array_equal(b, a)
+    assert (composed[2] > 0).mean() > 0.4
