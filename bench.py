@@ -121,7 +121,7 @@ def bench_tas(args, world, rank):
         ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pass_t, order_t,
                             len_t, stream)
 
-    settle_steps = distrib.settle(step, args.settle)
+    settle_steps = distrib.settle(step, args.settle, world=world)
     for _ in range(args.warmup):
         step()
     # timed steps: two HIP events on the launch stream around all of them (events between
@@ -360,7 +360,7 @@ def bench_gas(args, world, rank):
     def step():
         ctx.gas_fit_device(1, P, C, wl.I915, req_t, mask_t, nc_t, res_t, stream)
 
-    settle_steps = distrib.settle(step, args.settle)
+    settle_steps = distrib.settle(step, args.settle, world=world)
     for _ in range(args.warmup):
         step()
     gpu = {}
@@ -474,7 +474,7 @@ def bench_deschedule(args, world, rank):
         ctx.tas_label_plan_device(n_local, S, viol_t, labels_t, add_t, rem_t, total_t, stream)
         gathered["v"] = shard.gather_violations(viol_t, world, N)
 
-    settle_steps = distrib.settle(step, args.settle)
+    settle_steps = distrib.settle(step, args.settle, world=world)
     for _ in range(args.warmup):
         step()
     ctx.reset_timing()
@@ -562,7 +562,7 @@ def bench_c5(args, world, rank):
     ctx, stream, n0, n1, t = c5_setup(args, world, rank)
     topk = shard.ShardedTopK(ctx, K, world, rank, n0)
     step, result = c5_step_fn(ctx, stream, topk, P, t)
-    settle_steps = distrib.settle(step, args.settle)
+    settle_steps = distrib.settle(step, args.settle, world=world)
     for _ in range(args.warmup):
         step()
     gpu = {}

@@ -68,19 +68,25 @@ def gather_objects(obj, world):
     return out
 
 
-def settle(step, seconds, sync=None):
+def settle(step, seconds, sync=None, world=1):
     """Untimed steps for `seconds` of wall time before the warmup: the first ~20 steps of a
     fresh process run a few % slower (clocks, page tables), which a handful of warmup steps
-    does not cover.  Returns the number of steps run."""
+    does not cover.  Returns the number of steps run.  With world > 1 every rank runs the
+    same number of steps (the ranks agree after each round of 4), since a step may hold a
+    collective: ranks stopping at different counts would leave one waiting forever."""
     if sync is None:
         sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while True:
+        go = time.perf_counter() - t0 < seconds
+        if world > 1:
+            go = max_over_ranks(0.0 if go else 1.0, world) == 0.0  # all ranks still in time
+        if not go:
+            return n
         for _ in range(4):
             step()
         n += 4
         sync()
-    return n
 
 
 def timed_steps(step, steps, warmup, world, sync=None, gpu=None):

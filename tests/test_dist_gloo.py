@@ -114,3 +114,31 @@ def test_whole_job_rate():
     sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
     from pas_amd import distrib
     assert distrib.whole_job_rate(4096 * 100_000, 8, 10, 2.0) == 4096 * 100_000 * 8 * 10 / 2.0
+
+
+def _settle_worker(rank, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(WORLD),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
+    import torch
+    import torch.distributed as dist
+    from pas_amd import distrib
+    world, _, _ = distrib.setup("gloo")
+    # a step holding a collective, slower on rank 1: settle must stop both ranks at the same
+    # step count, or the faster one would wait in an all-reduce nobody joins
+    naps = [0.001, 0.004]
+
+    def step():
+        time.sleep(naps[rank])
+        t = torch.ones(1)
+        dist.all_reduce(t)
+    n = distrib.settle(step, 0.15, sync=lambda: None, world=world)
+    elapsed = distrib.timed_steps(step, 3, 1, world, sync=lambda: None)
+    np.save(os.path.join(out_dir, f"settle{rank}.npy"), np.array([n, elapsed]))
+    distrib.teardown(world)
+
+
+def test_settle_agrees_across_ranks(tmp_path):
+    mp.spawn(_settle_worker, args=(_free_port(), str(tmp_path)), nprocs=WORLD, join=True)
+    a, b = (np.load(tmp_path / f"settle{r}.npy") for r in range(WORLD))
+    assert a[0] == b[0] and a[0] >= 4 and a[0] % 4 == 0
