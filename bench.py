@@ -286,6 +286,7 @@ def request_latency(ctx, batch, n_nodes, reps=5):
                                   + res["encode_prioritize_ms"])
     res.update(nodes=n_nodes, body_bytes=len(body), filter_response_bytes=filter_bytes,
                decode_gb_per_s=len(body) / res["decode_ms"] / 1e6,
+               decode_threads=int(lib.pas_decode_threads(len(body))),
                note="host API calls (PCIe transfers of the candidate bitmap, pass row and "
                     "ordered list included); median of %d" % reps)
     table.close()

@@ -529,6 +529,13 @@ int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char*
                           int64_t ns_cap, int64_t* ns_len, char* label_buf, int64_t label_cap,
                           int64_t* label_len);
 
+/* Host threads pas_decode_args may use for one large body: the structural index and the
+ * items of a NodeList are split over them (about one per MB of body; results identical to
+ * one thread).  n = 0: automatic (up to 16, the GPU box's CPU share per GPU); process-wide.
+ * pas_decode_threads: the count a body of that size gets. */
+int pas_decode_set_threads(int32_t n);
+int32_t pas_decode_threads(int64_t body_len);
+
 /* containerRequests of a v1.Pod JSON (gpuscheduler/utils.go:14-32): per container, the
  * requests named gpu.intel.com/... as AsInt64 values (ok ignored), in the pas_gas_fit layout
  * req[max_containers][n_kinds] / req_mask[max_containers] for kinds[0 .. n_kinds), and

@@ -32,10 +32,13 @@
 // decode but not this one — parity unpinned for such bodies, which no kube-scheduler sends).
 #include <emmintrin.h>
 
+#include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <string>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 #include "pas.h"
@@ -458,11 +461,6 @@ struct pas_name_table {
 
 namespace {
 
-bool set_bit(uint64_t* bits, int32_t n) {
-  if (bits) bits[n >> 6] |= 1ull << (n & 63);
-  return true;
-}
-
 // The request node list being decoded.  A slice decodes element-wise into what it already
 // holds (encoding/json array(): elements past the old length start from zero), so a repeated
 // key keeps earlier values where the new element leaves them unset.
@@ -488,8 +486,12 @@ bool decode_node(Scanner& s, std::string* name) {
   });
 }
 
-// v1.NodeList: items (null sets the slice to nil).
-bool decode_node_list(Scanner& s, NodeList* out, const char* base) {
+struct ItemIndex;
+bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out);
+
+// v1.NodeList: items (null sets the slice to nil).  idx (optional): the body's structural
+// index; the first decode of a NodeList's items array goes through it in parallel.
+bool decode_node_list(Scanner& s, NodeList* out, const char* base, ItemIndex* idx) {
   return s.object([&](std::string_view k) {
     if (fold_match("items", k)) {
       const char c = s.peek();
@@ -499,6 +501,7 @@ bool decode_node_list(Scanner& s, NodeList* out, const char* base) {
         return s.literal("null");
       }
       if (c != '[') return s.mismatch();
+      if (idx && out->names.empty() && fast_items(idx, s, out)) return true;
       size_t n = 0;
       const bool ok = s.array([&](int64_t i) {
         if ((size_t)i >= out->names.size()) {
@@ -528,6 +531,251 @@ bool decode_node_list(Scanner& s, NodeList* out, const char* base) {
     }
     return s.skip();
   });
+}
+
+// ---------------------------------------------------------------------------- parallel items
+//
+// A 100k-node NodeList body is ~90 MB, nearly all of it the items array.  For a large body
+// the decode splits it over host threads without changing what is decoded:
+//   1. Structural index, per 64-byte block (SSE2 masks of quotes, backslashes, brackets,
+//      commas), per chunk of the body in parallel: a chunk's unescaped-quote parity and its
+//      bracket depth change for both possible in-string states at its start (the escape
+//      state at its start is the parity of the backslash run before it); a prefix over the
+//      chunks gives each chunk's in-string state and depth; a second parallel pass records
+//      the commas at depth 3 and the closings of depth-3 containers.
+//   2. The sequential decode runs as before until it reaches an items array at depth 2 (the
+//      Args object, then the NodeList).  Its end is the first depth-3 closing after it; the
+//      depth-3 commas between are the item boundaries.
+//   3. The items are decoded in parallel, each by the same decode_node on its own byte range
+//      (a Scanner at depth 3), which must consume the range exactly (value + whitespace).
+// Every byte outside the items array is decoded sequentially and every byte inside belongs
+// to exactly one item range, so a body accepted this way is valid JSON of the same shape and
+// decodes to the same values.  Anything else (an item failing, a repeated items key, no
+// closing found) returns to the sequential decode of that array, which then reports exactly
+// what the sequential path reports.
+constexpr int64_t kParBytesPerThread = 1 << 20;
+constexpr int kParMaxThreads = 16;  // the GPU box's CPU share per GPU
+std::atomic<int32_t> g_decode_threads{0};  // pas_decode_set_threads; 0 = automatic
+
+int decode_threads_for(int64_t len) {
+  const int32_t set = g_decode_threads.load(std::memory_order_relaxed);
+  const int hw = std::max(1, (int)std::thread::hardware_concurrency());
+  const int64_t t = std::min<int64_t>(set > 0 ? set : std::min(hw, kParMaxThreads),
+                                      len / kParBytesPerThread);
+  return (int)std::max<int64_t>(1, t);
+}
+
+// f(i) for i in [0, n): i = 0 on the calling thread.  Returns false (nothing run on other
+// threads) when a thread cannot be started.
+template <class F>
+bool parallel_for(int n, F&& f) {
+  std::vector<std::thread> th;
+  try {
+    th.reserve((size_t)std::max(n - 1, 0));
+    for (int i = 1; i < n; ++i) th.emplace_back([&f, i] { f(i); });
+  } catch (...) {
+    for (auto& x : th) x.join();
+    return false;
+  }
+  f(0);
+  for (auto& x : th) x.join();
+  return true;
+}
+
+struct Masks {
+  uint64_t quote, bs, open, close, comma;
+};
+
+// 64 bytes at p: '"', '\\', '{' or '[' (c | 0x20 == '{'), '}' or ']', ','.
+inline Masks classify64(const char* p) {
+  Masks m{0, 0, 0, 0, 0};
+  const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\'), o = _mm_set1_epi8('{');
+  const __m128i c = _mm_set1_epi8('}'), k = _mm_set1_epi8(','), lc = _mm_set1_epi8(0x20);
+  for (int i = 0; i < 4; ++i) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * i));
+    const __m128i vl = _mm_or_si128(v, lc);
+    const int sh = 16 * i;
+    m.quote |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, q)) << sh;
+    m.bs |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, b)) << sh;
+    m.open |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(vl, o)) << sh;
+    m.close |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(vl, c)) << sh;
+    m.comma |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, k)) << sh;
+  }
+  return m;
+}
+
+// Bytes of the block escaped by a backslash (carry: the block's first byte is).
+inline uint64_t escaped_mask(uint64_t bs, bool* carry) {
+  if (!bs) {
+    const uint64_t e = *carry ? 1ull : 0ull;
+    *carry = false;
+    return e;
+  }
+  uint64_t e = 0;
+  bool esc = *carry;
+  for (int i = 0; i < 64; ++i) {
+    if (esc) {
+      e |= 1ull << i;
+      esc = false;
+    } else if ((bs >> i) & 1ull) {
+      esc = true;
+    }
+  }
+  *carry = esc;
+  return e;
+}
+
+inline uint64_t prefix_xor(uint64_t x) {
+  x ^= x << 1;
+  x ^= x << 2;
+  x ^= x << 4;
+  x ^= x << 8;
+  x ^= x << 16;
+  x ^= x << 32;
+  return x;
+}
+
+struct ItemIndex {
+  const char* body = nullptr;
+  int64_t len = 0;
+  int threads = 1;
+  bool built = false;
+  std::vector<int64_t> events;  // pos * 2 + 1: closing of a depth-3 container; pos * 2: comma
+
+  // Walks the 64-byte blocks of [b, e) (the last one padded with spaces): f(block start,
+  // masks, escaped bytes), the escape state carried from the backslash run before b.
+  template <class F>
+  void blocks(int64_t b, int64_t e, F&& f) const {
+    int64_t r = b;
+    while (r > 0 && body[r - 1] == '\\') --r;
+    bool carry = ((b - r) & 1) != 0;
+    char pad[64];
+    for (int64_t x = b; x < e; x += 64) {
+      const char* p = body + x;
+      if (e - x < 64) {
+        std::memset(pad, ' ', sizeof pad);
+        std::memcpy(pad, p, (size_t)(e - x));
+        p = pad;
+      }
+      const Masks m = classify64(p);
+      f(x, p, m, escaped_mask(m.bs, &carry));
+    }
+  }
+
+  void build() {
+    const int T = threads;
+    const int64_t cs = ((len + T - 1) / T + 63) & ~int64_t(63);
+    std::vector<int64_t> par(T, 0), d_out(T, 0), d_in(T, 0);
+    // pass 1: quote parity and depth change per chunk, for both start states
+    if (!parallel_for(T, [&](int t) {
+          const int64_t b = std::min(len, t * cs), e = std::min(len, b + cs);
+          uint64_t instr = 0, pq = 0;
+          int64_t dout = 0, din = 0;
+          blocks(b, e, [&](int64_t, const char*, const Masks& m, uint64_t esc) {
+            const uint64_t qu = m.quote & ~esc;
+            const uint64_t mask = prefix_xor(qu) ^ instr;  // 1: inside (start outside)
+            instr = (mask >> 63) ? ~0ull : 0ull;
+            pq ^= (uint64_t)__builtin_popcountll(qu) & 1ull;
+            dout += __builtin_popcountll(m.open & ~mask) - __builtin_popcountll(m.close & ~mask);
+            din += __builtin_popcountll(m.open & mask) - __builtin_popcountll(m.close & mask);
+          });
+          par[t] = (int64_t)pq;
+          d_out[t] = dout;
+          d_in[t] = din;
+        }))
+      return;
+    std::vector<char> in0(T, 0);
+    std::vector<int64_t> depth0(T, 0);
+    for (int t = 1; t < T; ++t) {
+      in0[t] = (char)(in0[t - 1] ^ (par[t - 1] & 1));
+      depth0[t] = depth0[t - 1] + (in0[t - 1] ? d_in[t - 1] : d_out[t - 1]);
+    }
+    // pass 2: depth-3 commas and closings, in body order
+    std::vector<std::vector<int64_t>> ev(T);
+    if (!parallel_for(T, [&](int t) {
+          const int64_t b = std::min(len, t * cs), e = std::min(len, b + cs);
+          uint64_t instr = in0[t] ? ~0ull : 0ull;
+          int64_t depth = depth0[t];
+          std::vector<int64_t>& out = ev[t];
+          blocks(b, e, [&](int64_t x, const char* p, const Masks& m, uint64_t esc) {
+            const uint64_t mask = prefix_xor(m.quote & ~esc) ^ instr;
+            instr = (mask >> 63) ? ~0ull : 0ull;
+            uint64_t bits = (m.open | m.close | m.comma) & ~mask;
+            while (bits) {
+              const int i = __builtin_ctzll(bits);
+              bits &= bits - 1;
+              const char ch = p[i];
+              if (ch == ',') {
+                if (depth == 3) out.push_back((x + i) * 2);
+              } else if (ch == '{' || ch == '[') {
+                ++depth;
+              } else {
+                if (depth == 3) out.push_back((x + i) * 2 + 1);
+                --depth;
+              }
+            }
+          });
+        }))
+      return;
+    size_t total = 0;
+    for (const auto& v : ev) total += v.size();
+    events.reserve(total);
+    for (const auto& v : ev) events.insert(events.end(), v.begin(), v.end());
+    built = true;
+  }
+};
+
+// The items array at s.p ('[' of the first items key of a NodeList at depth 2) decoded in
+// parallel; false (s untouched) to decode it sequentially instead.
+bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
+  if (!idx->built || s.depth != 2) return false;
+  const int64_t p0 = s.p - idx->body;
+  const std::vector<int64_t>& ev = idx->events;
+  auto it = std::lower_bound(ev.begin(), ev.end(), p0 * 2 + 2);
+  std::vector<int64_t> cut{p0};  // '[' , the commas, ']'
+  for (; it != ev.end() && !(*it & 1); ++it) cut.push_back(*it >> 1);
+  if (it == ev.end()) return false;
+  cut.push_back(*it >> 1);
+  const size_t n_items = cut.size() - 1;
+  std::vector<std::string> names(n_items);
+  std::vector<int64_t> spans(2 * n_items);
+  std::atomic<bool> ok{true};
+  bool empty = false;
+  if (n_items == 1) {  // "[]" (whitespace only) or one item
+    Scanner w{idx->body + cut[0] + 1, idx->body + cut[1]};
+    w.ws();
+    empty = w.p == w.end;
+  }
+  const int T = std::max(1, std::min<int>(idx->threads, (int)(n_items / 256)));
+  if (!empty &&
+      !parallel_for(T, [&](int t) {
+        const size_t lo = n_items * (size_t)t / (size_t)T, hi = n_items * (size_t)(t + 1) / (size_t)T;
+        for (size_t i = lo; i < hi && ok.load(std::memory_order_relaxed); ++i) {
+          Scanner w{idx->body + cut[i] + 1, idx->body + cut[i + 1]};
+          w.depth = 3;
+          w.ws();
+          const char* b = w.p;
+          const bool good = decode_node(w, &names[i]);
+          const char* e = w.p;
+          w.ws();
+          if (!good || w.syntax_err || w.type_err || w.p != w.end || e == b) {
+            ok.store(false, std::memory_order_relaxed);
+            return;
+          }
+          spans[2 * i] = (int64_t)(b - idx->body);
+          spans[2 * i + 1] = (int64_t)(e - b);
+        }
+      }))
+    return false;
+  if (!ok.load()) return false;
+  if (empty) {
+    names.clear();
+    spans.clear();
+  }
+  out->names = std::move(names);
+  out->spans = std::move(spans);
+  s.p = idx->body + cut.back() + 1;
+  return true;
 }
 
 // strings.TrimSpace: ASCII spaces and the Unicode White_Space code points.
@@ -612,6 +860,14 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
                      pas_args_info* info) {
   std::memset(info, 0, sizeof *info);
   Scanner s{body, body + len};
+  ItemIndex index;
+  ItemIndex* idx = nullptr;
+  if (which == PAS_ARGS_NODES && (index.threads = decode_threads_for(len)) > 1) {
+    index.body = body;
+    index.len = len;
+    index.build();
+    idx = &index;
+  }
   NodeList nodes;
   std::vector<std::string> node_names;
   bool has_nodes = false, has_names = false;
@@ -651,7 +907,7 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
           nodes.spans.clear();
         }
         has_nodes = true;
-        return decode_node_list(s, &nodes, body);
+        return decode_node_list(s, &nodes, body, idx);
       }
       if (fold_match("NodeNames", k)) {
         const char c = s.peek();
@@ -709,18 +965,41 @@ int pas_decode_args(const pas_name_table* t, const char* body, int64_t len, int3
   if (rc != PAS_OK) return rc;
   if (cand) std::memset(cand, 0, sizeof(uint64_t) * ((t->names.size() + 63) / 64));
   const bool fits = (int64_t)names.size() <= node_cap;
-  for (size_t i = 0; i < names.size(); ++i) {
-    const int32_t id = t->find(names[i]);
-    if (id < 0)
-      ++info->n_unknown;
-    else
-      set_bit(cand, id);
-    if (fits) req_node[i] = id;
+  // name lookups, split over host threads for a large request (candidate bits or-ed in)
+  const size_t n = names.size();
+  const int T = n >= 16384 ? decode_threads_for(len) : 1;
+  std::vector<int32_t> unknown((size_t)T, 0);
+  auto lookup = [&](int th) {
+    const size_t lo = n * (size_t)th / (size_t)T, hi = n * (size_t)(th + 1) / (size_t)T;
+    for (size_t i = lo; i < hi; ++i) {
+      const int32_t id = t->find(names[i]);
+      if (id < 0)
+        ++unknown[(size_t)th];
+      else if (cand)
+        __atomic_fetch_or(&cand[id >> 6], 1ull << (id & 63), __ATOMIC_RELAXED);
+      if (fits) req_node[i] = id;
+    }
+  };
+  if (T <= 1 || !parallel_for(T, lookup)) {
+    std::fill(unknown.begin(), unknown.end(), 0);
+    if (cand) std::memset(cand, 0, sizeof(uint64_t) * ((t->names.size() + 63) / 64));
+    for (int th = 0; th < T; ++th) lookup(th);
   }
+  for (int32_t u : unknown) info->n_unknown += u;
   if (!fits) return PAS_ECAPACITY;
   if (item_span && !spans.empty())
     std::memcpy(item_span, spans.data(), sizeof(int64_t) * spans.size());
   return PAS_OK;
+}
+
+int pas_decode_set_threads(int32_t n) {
+  if (n < 0) return PAS_EINVAL;
+  g_decode_threads.store(n, std::memory_order_relaxed);
+  return PAS_OK;
+}
+
+int32_t pas_decode_threads(int64_t body_len) {
+  return body_len < 0 ? 1 : (int32_t)decode_threads_for(body_len);
 }
 
 int pas_decode_request_names(const char* body, int64_t len, int32_t which, char* buf,

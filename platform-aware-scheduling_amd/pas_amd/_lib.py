@@ -211,6 +211,8 @@ SIGNATURES = {
     "pas_decode_pod_requests": (
         c_int, [c_char_p, c_int64, c_int32, POINTER(c_char_p), c_int32, _P, _P,
                 POINTER(c_int32), POINTER(c_int32)]),
+    "pas_decode_set_threads": (c_int, [c_int32]),
+    "pas_decode_threads": (c_int32, [c_int64]),
     "pas_set_timing": (c_int, [_P, c_int]),
     "pas_kernel_time": (c_int, [_P, c_int32, POINTER(c_double), POINTER(c_int64)]),
     "pas_reset_timing": (c_int, [_P]),
