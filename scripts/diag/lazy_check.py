@@ -23,8 +23,19 @@ flag = rng.random(gbatch.req_mask.shape) < float(sys.argv[5])
 gbatch.req_mask = gbatch.req_mask | np.where(flag, 0x80000000, 0).astype(np.uint32)
 batch.prio["metric"][::17] = 99
 ctx = pas_amd.Context(0)
+base = int(sys.argv[6]) if len(sys.argv) > 6 else 0
 (kc, nc, lc), (kl, nl, ll) = _lazy_vs_composed(ctx, snap.v_milli, snap.present, batch, gsnap,
-                                               gbatch, batch.cand, k, 0, wl.I915)
+                                               gbatch, batch.cand, k, base, wl.I915)
+print("keys equal", np.array_equal(kc, kl), "nodes equal", np.array_equal(nc, nl),
+      "lens equal", np.array_equal(lc, ll))
+for p in range(len(batch.prio)):
+    if not np.array_equal(kc[p], kl[p]):
+        j = int(np.nonzero(kc[p] != kl[p])[0][0])
+        print("pod", p, "op", batch.prio["op"][p], "len", lc[p], ll[p], "first diff", j,
+              "keys", kc[p, j:j + 3], kl[p, j:j + 3], "nodes", nc[p, j:j + 3], nl[p, j:j + 3])
+        break
+nc = np.where(nc == np.iinfo(np.int32).max, nc, nc - base)
+nl = np.where(nl == np.iinfo(np.int32).max, nl, nl - base)
 words = oracle.gas_fit(gsnap.n_cards, gsnap.cap, gsnap.used, gbatch.req, gbatch.req_mask,
                        gbatch.n_containers, wl.I915)
 fitb = wl.pack_bits((words >> 31).astype(bool))

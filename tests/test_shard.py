@@ -331,8 +331,10 @@ def _lazy_vs_composed(ctx, v, pres, batch, gsnap, gbatch, cand, k, node_base, i9
     C = gbatch.req.shape[1]
     fit_t = torch.empty((P, (n + 63) // 64), dtype=torch.int64, device="cuda")
     ctx.gas_fit_bitmap_device(gen_g, P, C, i915, req_t, mask_t, nc_t, fit_t)
+    ctx.synchronize()  # (the context's stream) before torch's stream reads fit_t
     if cand_t is not None:
         fit_t &= cand_t
+        torch.cuda.synchronize()
     out = []
     for lazy in (False, True):
         key = torch.empty((P, k), dtype=torch.int64, device="cuda")
