@@ -101,6 +101,10 @@ void free_tas(pas_ctx* ctx) {
   TasSnapshot& t = ctx->tas;
   free_ptr(reinterpret_cast<void*&>(t.vals));
   free_ptr(reinterpret_cast<void*&>(t.present));
+  free_ptr(reinterpret_cast<void*&>(t.vals_t));
+  free_ptr(reinterpret_cast<void*&>(t.pres_t));
+  t.t_bytes = 0;
+  t.t_epoch = 0;
   free_ptr(reinterpret_cast<void*&>(t.cnt));
   free_ptr(reinterpret_cast<void*&>(t.sorted));
   free_ptr(reinterpret_cast<void*&>(t.perm));

@@ -60,6 +60,14 @@ struct TasSnapshot {
   size_t sort_tmp_bytes = 0;
   void* scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
+  // node-major copies for per-node gathers (tas_gas_topk.hip), built by the first call that
+  // needs them after a change: vals_t int64 [N][M], pres_t uint64 [N][ceil(M / 64)].
+  // `epoch` counts snapshot changes, `t_epoch` is the epoch the copies were built at.
+  uint64_t epoch = 1;
+  uint64_t t_epoch = 0;
+  int64_t* vals_t = nullptr;
+  uint64_t* pres_t = nullptr;
+  size_t t_bytes = 0;
 };
 
 // Device-resident GAS snapshot (node-major):
@@ -164,6 +172,11 @@ int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
                     int32_t k, int32_t node_base, int64_t* d_key, int32_t* d_node,
                     int32_t* d_len, hipStream_t s);
+// The eval prep's grouping alone: pods bucketed by prioritize order row (metric x asc / desc
+// / index), desc[2 pos] = {pod, order * M + metric or -1, present count, 0},
+// desc[2 pos + 1] = {rule_off[pod], rule_off[pod + 1], 0, 0}; keys [P] scratch.
+int tas_group_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_prio,
+                     const int32_t* d_rule_off, int4* d_desc, int2* d_keys, hipStream_t s);
 int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
                         const int32_t* d_rule_off, const pas_rule* d_prio,
                         const uint64_t* d_cand, int32_t max_containers, int32_t i915_index,

@@ -9,14 +9,21 @@
 //
 // The composed path (pas_gas_fit_bitmap_device -> pas_tas_topk_device) evaluates every
 // (pod, node): a fit bit for each of the shard's nodes and the pod's whole LDS pass bitmap,
-// although only the first k passing nodes of the order are kept.  Here a wave owns a pod and
-// walks its order row (the snapshot's per-metric order, tas_snapshot.hip) 64 positions at a
-// time: each lane evaluates its position's node directly — candidate bit, every dontschedule
-// rule of the pod (EvaluateRule on the node's value: one gather per rule), then the GAS first
-// fit on the node's card usage (only for lanes still passing) — and the wave stops once k
-// nodes are kept.  The result is the same list: the k first positions of the order whose
-// node passes both filters.  With filter and fit rates near 1 (C5: ~0.93 and ~0.97) a pod
-// needs one round, ~64 node evaluations instead of the shard's N.
+// although only the first k passing nodes of the order are kept.  Here half a wave (32
+// lanes) owns a pod and walks its order row (the snapshot's per-metric order,
+// tas_snapshot.hip) 32 positions at a time: each lane evaluates its position's node directly
+// — candidate bit, every dontschedule rule of the pod (EvaluateRule on the node's value),
+// then the GAS first fit on the node's card usage (only for lanes still passing) — and the
+// pod stops once k nodes are kept.  The result is the same list: the k first positions of
+// the order whose node passes both filters.  With filter and fit rates near 1 (C5: ~0.93
+// and ~0.97) a pod with k = 16 needs one round, 32 node evaluations instead of the shard's N.
+//
+// The node values come from node-major copies of the snapshot (vals_t [N][M], pres_t
+// [N][M/64], built once per snapshot change): a lane's rules read its node's own row (the
+// 16 metrics of a 128-byte line together) and one presence word, instead of one line per
+// rule in the metric-major columns.  Pods are bucketed by order row (the eval prep's
+// grouping) and each XCD takes a contiguous run of the buckets, so the first positions of a
+// row — the nodes every pod of that row evaluates — stay in that XCD's L2.
 //
 // Records: key = order key of the node's value under the pod's operator (tas_topk.hip),
 // node = global id (local + node_base); past len: key INT64_MAX, node INT32_MAX.
@@ -43,7 +50,10 @@ struct LazyTopkParams {
   const int32_t* perm;   // [3][M][R] snapshot orders
   const int32_t* cnt;    // [M]
   const int64_t* vals;   // [M][N]
-  const uint64_t* present;
+  const int64_t* vals_t;    // [N][M]
+  const uint64_t* pres_t;   // [N][WM]
+  int32_t WM;
+  const int4* desc;       // [2P] pods bucketed by order row (tas_group_launch)
   // GAS snapshot (same nodes) and the pods' requests
   int32_t K, Q, C, i915;
   const int32_t* n_cards;
@@ -134,97 +144,141 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
   return true;
 }
 
+constexpr int kPodLanes = 32;                // lanes per pod (order positions per round)
+constexpr int kPodsPerWave = 64 / kPodLanes;
+constexpr int kPodsPerBlock = kWaves * kPodsPerWave;
+
 template <int KMAX>
 __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
   const int lane = threadIdx.x & 63;
-  const int32_t p = (int32_t)blockIdx.x * kWaves + (int32_t)(threadIdx.x >> 6);
-  if (p >= a.n_pods) return;  // wave-uniform
+  const int half = lane / kPodLanes, sub = lane % kPodLanes;
+  // XCD-aware: blocks b and b + 8 share an XCD; each XCD takes a contiguous run of the
+  // bucketed pod list (MI355X_MICROARCH.md)
+  const int32_t nb = gridDim.x, b = blockIdx.x;
+  const int32_t xcd = b & 7, per = nb >> 3, rem = nb & 7;
+  const int32_t slot = xcd * per + min(xcd, rem) + (b >> 3);
+  const int32_t pos = slot * kPodsPerBlock + (int32_t)(threadIdx.x >> 6) * kPodsPerWave + half;
+  const bool have = pos < a.n_pods;
+  const int4 d0 = have ? a.desc[2 * pos] : make_int4(0, -1, 0, 0);
+  const int4 d1 = have ? a.desc[2 * pos + 1] : make_int4(0, 0, 0, 0);
+  const int32_t p = d0.x;
   const int32_t k = a.k;
-  int64_t* keys = a.key_out + (int64_t)p * k;
-  int32_t* nodes = a.node_out + (int64_t)p * k;
   const pas_rule pr = a.prio[p];
-  // no scheduling rule / metric not cached: empty list (telemetryscheduler.go:92-96)
-  const bool listed = pr.metric >= 0 && pr.metric < a.M;
-  int32_t c0 = listed ? a.cnt[pr.metric] : 0;
-  // a pod past PAS_GAS_MAX_SELECTIONS is not evaluated (its fit bits are 0, as
-  // pas_gas_fit_bitmap_device leaves them)
-  {
+  // bucket -1: no scheduling rule / metric not cached / no node has it: empty list
+  // (telemetryscheduler.go:92-96); d0.z = the metric's present count
+  int32_t c0 = (have && d0.y >= 0) ? d0.z : 0;
+  if (c0 > 0) {  // a pod past PAS_GAS_MAX_SELECTIONS is not evaluated (fit bits 0)
     int64_t steps = 0;
     for (int32_t c = 0; c < a.ncont[p]; ++c) {
-      const int64_t b = (int64_t)p * a.C + c;
-      const uint32_t m = a.mask[b];
+      const int64_t bb = (int64_t)p * a.C + c;
+      const uint32_t m = a.mask[bb];
       if (a.i915 >= 0 && m != 0u && ((m >> a.i915) & 1u)) {
-        const int64_t v = a.req[b * a.Q + a.i915];
+        const int64_t v = a.req[bb * a.Q + a.i915];
         if (v > 0) steps += min(v, (int64_t)PAS_GAS_MAX_SELECTIONS + 1);
       }
     }
     if (steps > PAS_GAS_MAX_SELECTIONS) c0 = 0;
   }
-  const int32_t r0 = a.rule_off[p], r1 = a.rule_off[p + 1];
-  const int32_t* row =
-      a.perm + ((int64_t)(pr.op == PAS_OP_GREATER_THAN ? kOrderDesc
-                          : pr.op == PAS_OP_LESS_THAN  ? kOrderAsc
-                                                       : kOrderIndex) *
-                    a.M +
-                (listed ? pr.metric : 0)) *
-                   a.R;
-  const int64_t* mcol = a.vals + (int64_t)(listed ? pr.metric : 0) * a.N;
+  const int32_t r0 = d1.x, r1 = d1.y;
+  const int32_t* row = a.perm + (int64_t)(d0.y >= 0 ? d0.y : 0) * a.R;
+  const int64_t* mcol = a.vals + (int64_t)(d0.y >= 0 ? pr.metric : 0) * a.N;
+  int64_t* keys = a.key_out + (int64_t)p * k;
+  int32_t* nodes = a.node_out + (int64_t)p * k;
+  const uint64_t half_mask = half ? ~0ull << 32 : 0xFFFFFFFFull;
+  const uint64_t below = half_mask & ((1ull << lane) - 1ull);
   int32_t kept = 0;
-  for (int32_t j0 = 0; j0 < c0 && kept < k; j0 += 64) {
-    const int32_t j = j0 + lane;
-    const bool valid = j < c0;
+  for (int32_t j0 = 0; __ballot(j0 < c0 && kept < k); j0 += kPodLanes) {
+    const int32_t j = j0 + sub;
+    const bool active = j0 < c0 && kept < k;  // (uniform within the pod's half)
+    const bool valid = active && j < c0;
     const int32_t n = valid ? row[j] : 0;
     bool ok = valid;
     if (a.cand) ok = ok && ((a.cand[(int64_t)p * a.W64 + (n >> 6)] >> (n & 63)) & 1ull);
     // dontschedule.Violated (strategy.go:25-44) at this node: any rule whose metric the node
     // has and whose EvaluateRule holds; rules on metrics outside the cache or with an
-    // unknown operator are skipped.  kRuleBatch rules' gathers in flight at once.
+    // unknown operator are skipped.  kRuleBatch rules' loads in flight at once.
+    const int64_t* vrow = a.vals_t + (int64_t)n * a.M;
+    const uint64_t* prow = a.pres_t + (int64_t)n * a.WM;
     bool viol = false;
-    for (int32_t rb = r0; rb < r1; rb += kRuleBatch) {
+    for (int32_t rb = r0; __ballot(ok && rb < r1); rb += kRuleBatch) {
       pas_rule ru[kRuleBatch];
       int64_t v[kRuleBatch];
       uint64_t pw[kRuleBatch];
 #pragma unroll
-      for (int u = 0; u < kRuleBatch; ++u) ru[u] = a.rules[min(rb + u, r1 - 1)];
+      for (int u = 0; u < kRuleBatch; ++u) ru[u] = a.rules[max(min(rb + u, r1 - 1), 0)];
 #pragma unroll
       for (int u = 0; u < kRuleBatch; ++u) {
         const int32_t m = (ru[u].metric >= 0 && ru[u].metric < a.M) ? ru[u].metric : 0;
-        v[u] = a.vals[(int64_t)m * a.N + n];
-        pw[u] = a.present[(int64_t)m * a.W64 + (n >> 6)];
+        v[u] = vrow[m];
+        pw[u] = prow[m >> 6];
       }
 #pragma unroll
       for (int u = 0; u < kRuleBatch; ++u) {
         const pas_rule rule = ru[u];
-        if (rule.metric < 0 || rule.metric >= a.M || rule.op < 0 || rule.op > 2) continue;
+        if (rb + u >= r1 || rule.metric < 0 || rule.metric >= a.M || rule.op < 0 || rule.op > 2)
+          continue;
         int64_t tm = 0;
         const int sat = target_milli(rule.target, &tm);
         bool hit;
         if (rule.op == PAS_OP_LESS_THAN) hit = sat > 0 || (sat == 0 && v[u] < tm);
         else if (rule.op == PAS_OP_GREATER_THAN) hit = sat < 0 || (sat == 0 && v[u] > tm);
         else hit = sat == 0 && v[u] == tm;
-        viol = viol || (hit && ((pw[u] >> (n & 63)) & 1ull));
+        viol = viol || (hit && ((pw[u] >> (rule.metric & 63)) & 1ull));
       }
     }
     ok = ok && !viol;
     if (ok) ok = lane_fit<KMAX>(a, p, n);
-    const uint64_t keep = __ballot(ok);
+    const uint64_t keep = __ballot(ok) & half_mask;
     if (ok) {
-      const int32_t rank = kept + (int32_t)__builtin_amdgcn_mbcnt_hi(
-                                      (uint32_t)(keep >> 32),
-                                      __builtin_amdgcn_mbcnt_lo((uint32_t)keep, 0u));
+      const int32_t rank = kept + __popcll(keep & below);
       if (rank < k) {
         nodes[rank] = n + a.node_base;
         keys[rank] = order_key(pr.op, mcol[n]);
       }
     }
-    kept += (int32_t)__popcll(keep);
+    kept += active ? __popcll(keep) : 0;
   }
+  if (!have) return;
   const int32_t len = min(kept, k);
-  for (int32_t i = len + lane; i < k; i += 64) {
+  for (int32_t i = len + sub; i < k; i += kPodLanes) {
     keys[i] = INT64_MAX;
     nodes[i] = INT32_MAX;
   }
-  if (lane == 0) a.len_out[p] = len;
+  if (sub == 0) a.len_out[p] = len;
+}
+
+// vals [M][N] -> vals_t [N][M] through 64 x 64 LDS tiles (coalesced both ways)
+__global__ __launch_bounds__(kTpb) void transpose_vals_kernel(int32_t N, int32_t M,
+                                                               const int64_t* __restrict__ vals,
+                                                               int64_t* __restrict__ vals_t) {
+  __shared__ int64_t tile[64][65];
+  const int32_t n0 = blockIdx.x * 64, m0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += kWaves) {
+    const int32_t m = m0 + r, n = n0 + tx;
+    tile[r][tx] = (m < M && n < N) ? vals[(int64_t)m * N + n] : 0;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += kWaves) {
+    const int32_t n = n0 + r, m = m0 + tx;
+    if (n < N && m < M) vals_t[(int64_t)n * M + m] = tile[tx][r];
+  }
+}
+
+// present [M][W64] -> pres_t [N][WM]: bit m of node n's word m / 64
+__global__ __launch_bounds__(kTpb) void transpose_present_kernel(
+    int32_t N, int32_t M, int32_t W64, int32_t WM, const uint64_t* __restrict__ present,
+    uint64_t* __restrict__ pres_t) {
+  const int32_t n = blockIdx.x * kTpb + threadIdx.x;
+  if (n >= N) return;
+  for (int32_t w = 0; w < WM; ++w) {
+    uint64_t word = 0;
+    for (int32_t j = 0; j < 64 && w * 64 + j < M; ++j) {
+      const uint64_t bit = (present[(int64_t)(w * 64 + j) * W64 + (n >> 6)] >> (n & 63)) & 1ull;
+      word |= bit << j;
+    }
+    pres_t[(int64_t)n * WM + w] = word;
+  }
 }
 
 }  // namespace
@@ -236,14 +290,57 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
                         const int32_t* d_n_containers, int32_t k, int32_t node_base,
                         int64_t* d_key, int32_t* d_node, int32_t* d_len, hipStream_t s) {
   if (n_pods == 0) return PAS_OK;
-  const TasSnapshot& t = ctx->tas;
+  TasSnapshot& t = ctx->tas;
   const GasSnapshot& g = ctx->gas;
+  const int32_t N = t.n_nodes, M = t.n_metrics;
+  const int32_t WM = (M + 63) / 64;
+  // node-major copies, once per snapshot change
+  if (t.t_epoch != t.epoch && N > 0 && M > 0) {
+    const size_t bv = sizeof(int64_t) * (size_t)N * M, bp = sizeof(uint64_t) * (size_t)N * WM;
+    if (t.t_bytes != bv + bp) {
+      if (t.vals_t) {
+        PAS_HIP(ctx, hipStreamSynchronize(s));
+        PAS_HIP(ctx, hipFree(t.vals_t));
+        PAS_HIP(ctx, hipFree(t.pres_t));
+        t.vals_t = nullptr;
+        t.pres_t = nullptr;
+      }
+      t.t_bytes = 0;
+      PAS_HIP(ctx, hipMalloc(&t.vals_t, bv));
+      PAS_HIP(ctx, hipMalloc(&t.pres_t, bp));
+      t.t_bytes = bv + bp;
+    }
+    transpose_vals_kernel<<<dim3((unsigned)((N + 63) / 64), (unsigned)((M + 63) / 64)), kTpb, 0,
+                            s>>>(N, M, t.vals, t.vals_t);
+    transpose_present_kernel<<<(unsigned)((N + kTpb - 1) / kTpb), kTpb, 0, s>>>(
+        N, M, (int32_t)w64(N), WM, t.present, t.pres_t);
+    PAS_HIP(ctx, hipGetLastError());
+    t.t_epoch = t.epoch;
+  }
+  // scratch: desc [2P] | keys [P]
+  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
+  const size_t b_desc = al(sizeof(int4) * 2 * (size_t)n_pods), b_keys = al(sizeof(int2) * n_pods);
+  if (b_desc + b_keys > ctx->aux_bytes) {
+    if (ctx->aux) {
+      PAS_HIP(ctx, hipStreamSynchronize(s));
+      PAS_HIP(ctx, hipFree(ctx->aux));
+      ctx->aux = nullptr;
+      ctx->aux_bytes = 0;
+    }
+    PAS_HIP(ctx, hipMalloc(&ctx->aux, b_desc + b_keys));
+    ctx->aux_bytes = b_desc + b_keys;
+  }
+  int4* d_desc = static_cast<int4*>(ctx->aux);
+  int2* d_keys = reinterpret_cast<int2*>(static_cast<char*>(ctx->aux) + b_desc);
+  TimedLaunch tl;
+  timing_begin(ctx, s, PAS_K_TAS_GAS_TOPK, &tl);
+  if (int rc = tas_group_launch(ctx, n_pods, d_prio, d_rule_off, d_desc, d_keys, s)) return rc;
   LazyTopkParams a;
   a.n_pods = n_pods;
-  a.N = t.n_nodes;
-  a.M = t.n_metrics;
+  a.N = N;
+  a.M = M;
   a.R = t.row;
-  a.W64 = (int32_t)w64(t.n_nodes);
+  a.W64 = (int32_t)w64(N);
   a.k = k;
   a.node_base = node_base;
   a.rules = d_rules;
@@ -253,7 +350,10 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
   a.perm = t.perm;
   a.cnt = t.cnt;
   a.vals = t.vals;
-  a.present = t.present;
+  a.vals_t = t.vals_t;
+  a.pres_t = t.pres_t;
+  a.WM = WM;
+  a.desc = d_desc;
   a.K = g.max_cards;
   a.Q = g.n_res;
   a.C = max_containers;
@@ -267,9 +367,7 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
   a.key_out = d_key;
   a.node_out = d_node;
   a.len_out = d_len;
-  TimedLaunch tl;
-  timing_begin(ctx, s, PAS_K_TAS_GAS_TOPK, &tl);
-  const unsigned grid = (unsigned)((n_pods + kWaves - 1) / kWaves);
+  const unsigned grid = (unsigned)((n_pods + kPodsPerBlock - 1) / kPodsPerBlock);
   if (a.K <= 8)
     tas_gas_topk_kernel<8><<<grid, kTpb, 0, s>>>(a);
   else if (a.K <= 16)

@@ -241,6 +241,7 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
   }
   t.gen = gen;
   t.valid = true;
+  ++t.epoch;
   return PAS_OK;
 }
 
@@ -267,6 +268,7 @@ int tas_snapshot_update(pas_ctx* ctx, uint64_t gen, int32_t n_cols, const int32_
   }
   t.gen = gen;
   t.valid = true;
+  ++t.epoch;
   return PAS_OK;
 }
 
