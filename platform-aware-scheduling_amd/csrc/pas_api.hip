@@ -1094,7 +1094,7 @@ int pas_tas_gas_topk_device(pas_ctx* ctx, uint64_t tas_gen, uint64_t gas_gen, in
       !d_top_len || !d_n_containers || (max_containers > 0 && (!d_req || !d_req_mask)))
     return set_error(ctx, PAS_EINVAL, "pas_tas_gas_topk_device: null argument");
   if ((rc = activate(ctx))) return rc;
-  return tas_gas_topk_launch(ctx, n_pods, d_rules, d_rule_off, d_prio, d_cand, max_containers,
+  return tas_gas_topk_launch(ctx, n_pods, n_rules, d_rules, d_rule_off, d_prio, d_cand, max_containers,
                              i915_index, d_req, d_req_mask, d_n_containers, k, node_base,
                              d_top_key, d_top_node, d_top_len, pick_stream(ctx, hip_stream));
 }

@@ -174,10 +174,13 @@ int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
                     int32_t* d_len, hipStream_t s);
 // The eval prep's grouping alone: pods bucketed by prioritize order row (metric x asc / desc
 // / index), desc[2 pos] = {pod, order * M + metric or -1, present count, 0},
-// desc[2 pos + 1] = {rule_off[pod], rule_off[pod + 1], 0, 0}; keys [P] scratch.
+// desc[2 pos + 1] = {rule_off[pod], rule_off[pod + 1], 0, 0}; keys [P] scratch.  With
+// d_ranges, also every rule's range of the metric's ascending order (EvaluateRule, a3):
+// ranges[r] = {first, end} positions of the nodes the rule selects.
 int tas_group_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_prio,
-                     const int32_t* d_rule_off, int4* d_desc, int2* d_keys, hipStream_t s);
-int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
+                     const int32_t* d_rule_off, int4* d_desc, int2* d_keys, int32_t n_rules,
+                     const pas_rule* d_rules, int2* d_ranges, hipStream_t s);
+int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
                         const int32_t* d_rule_off, const pas_rule* d_prio,
                         const uint64_t* d_cand, int32_t max_containers, int32_t i915_index,
                         const int64_t* d_req, const uint32_t* d_req_mask,

@@ -869,19 +869,23 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
 }
 
 int tas_group_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_prio,
-                     const int32_t* d_rule_off, int4* d_desc, int2* d_keys, hipStream_t s) {
+                     const int32_t* d_rule_off, int4* d_desc, int2* d_keys, int32_t n_rules,
+                     const pas_rule* d_rules, int2* d_ranges, hipStream_t s) {
   const TasSnapshot& t = ctx->tas;
   const int32_t M = t.n_metrics;
   if (M > kMaxGroupMetrics)
     return set_error(ctx, PAS_ECAPACITY, "more than 4096 metric columns");
   const uint32_t flags = PAS_TAS_FILTER | PAS_TAS_PRIORITIZE;
-  RangesParams rp{0, M, t.row, nullptr, t.cnt, t.sorted, t.f1k, t.f32, nullptr};
+  const int32_t range_rules = d_ranges ? n_rules : 0;
+  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges};
   GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, 0};
   const size_t group_lds = sizeof(int32_t) * ((size_t)3 * M + 1 + (size_t)M);
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_prep_kernel),
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)group_lds));
-  tas_prep_kernel<<<1, kGroupTpb, group_lds, s>>>(gp, rp);
+  constexpr int kRulesPerBlock = kGroupTpb / kRuleLanes;
+  const unsigned blocks = 1u + (unsigned)((range_rules + kRulesPerBlock - 1) / kRulesPerBlock);
+  tas_prep_kernel<<<blocks, kGroupTpb, group_lds, s>>>(gp, rp);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
 }

@@ -54,6 +54,7 @@ struct LazyTopkParams {
   const uint64_t* pres_t;   // [N][WM]
   int32_t WM;
   const int4* desc;       // [2P] pods bucketed by order row (tas_group_launch)
+  const int2* ranges;     // [n_rules] each rule's range of its metric's ascending order
   // GAS snapshot (same nodes) and the pods' requests
   int32_t K, Q, C, i915;
   const int32_t* n_cards;
@@ -180,6 +181,34 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
     if (steps > PAS_GAS_MAX_SELECTIONS) c0 = 0;
   }
   const int32_t r0 = d1.x, r1 = d1.y;
+  // Rules on the prioritize metric itself select one contiguous range of a sorted order row
+  // (EvaluateRule over the ascending column, a3): a pod whose rule excludes the top of its
+  // own order (e.g. GreaterThan on the metric it prioritizes by GreaterThan) would walk
+  // thousands of violating positions.  Such ranges (asc positions from the prep's search,
+  // mirrored for the descending row) are jumped over at the start of each round; the rule
+  // check per node still runs, so the skip only saves rounds.
+  constexpr int kSkip = 4;
+  int32_t slo[kSkip], shi[kSkip], ns = 0;
+#pragma unroll
+  for (int i = 0; i < kSkip; ++i) slo[i] = shi[i] = 0;
+  const int ord = d0.y >= 0 ? d0.y / a.M : kOrderIndex;
+  if (c0 > 0 && ord != kOrderIndex) {
+    for (int32_t r = r0; r < r1; ++r) {
+      const pas_rule ru = a.rules[r];
+      if (ru.metric != pr.metric || ru.op < 0 || ru.op > 2) continue;
+      const int2 g = a.ranges[r];
+      const int32_t lo = ord == kOrderDesc ? c0 - g.y : g.x;
+      const int32_t hi = ord == kOrderDesc ? c0 - g.x : g.y;
+      if (hi <= lo) continue;
+#pragma unroll
+      for (int i = 0; i < kSkip; ++i)
+        if (i == ns) {
+          slo[i] = lo;
+          shi[i] = hi;
+        }
+      ns = min(ns + 1, kSkip);
+    }
+  }
   const int32_t* row = a.perm + (int64_t)(d0.y >= 0 ? d0.y : 0) * a.R;
   const int64_t* mcol = a.vals + (int64_t)(d0.y >= 0 ? pr.metric : 0) * a.N;
   int64_t* keys = a.key_out + (int64_t)p * k;
@@ -187,9 +216,15 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
   const uint64_t half_mask = half ? ~0ull << 32 : 0xFFFFFFFFull;
   const uint64_t below = half_mask & ((1ull << lane) - 1ull);
   int32_t kept = 0;
-  for (int32_t j0 = 0; __ballot(j0 < c0 && kept < k); j0 += kPodLanes) {
-    const int32_t j = j0 + sub;
+  for (int32_t j0 = 0;; j0 += kPodLanes) {
+#pragma unroll
+    for (int it = 0; it < kSkip; ++it)
+#pragma unroll
+      for (int i = 0; i < kSkip; ++i)
+        if (i < ns && j0 >= slo[i] && j0 < shi[i]) j0 = shi[i];
     const bool active = j0 < c0 && kept < k;  // (uniform within the pod's half)
+    if (!__ballot(active)) break;
+    const int32_t j = j0 + sub;
     const bool valid = active && j < c0;
     const int32_t n = valid ? row[j] : 0;
     bool ok = valid;
@@ -283,7 +318,7 @@ __global__ __launch_bounds__(kTpb) void transpose_present_kernel(
 
 }  // namespace
 
-int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
+int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
                         const int32_t* d_rule_off, const pas_rule* d_prio,
                         const uint64_t* d_cand, int32_t max_containers, int32_t i915_index,
                         const int64_t* d_req, const uint32_t* d_req_mask,
@@ -317,24 +352,28 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
     PAS_HIP(ctx, hipGetLastError());
     t.t_epoch = t.epoch;
   }
-  // scratch: desc [2P] | keys [P]
+  // scratch: desc [2P] | keys [P] | ranges [n_rules]
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t b_desc = al(sizeof(int4) * 2 * (size_t)n_pods), b_keys = al(sizeof(int2) * n_pods);
-  if (b_desc + b_keys > ctx->aux_bytes) {
+  const size_t b_rng = al(sizeof(int2) * (size_t)std::max(n_rules, 1));
+  if (b_desc + b_keys + b_rng > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
       PAS_HIP(ctx, hipFree(ctx->aux));
       ctx->aux = nullptr;
       ctx->aux_bytes = 0;
     }
-    PAS_HIP(ctx, hipMalloc(&ctx->aux, b_desc + b_keys));
-    ctx->aux_bytes = b_desc + b_keys;
+    PAS_HIP(ctx, hipMalloc(&ctx->aux, b_desc + b_keys + b_rng));
+    ctx->aux_bytes = b_desc + b_keys + b_rng;
   }
   int4* d_desc = static_cast<int4*>(ctx->aux);
   int2* d_keys = reinterpret_cast<int2*>(static_cast<char*>(ctx->aux) + b_desc);
+  int2* d_ranges = reinterpret_cast<int2*>(static_cast<char*>(ctx->aux) + b_desc + b_keys);
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_GAS_TOPK, &tl);
-  if (int rc = tas_group_launch(ctx, n_pods, d_prio, d_rule_off, d_desc, d_keys, s)) return rc;
+  if (int rc = tas_group_launch(ctx, n_pods, d_prio, d_rule_off, d_desc, d_keys, n_rules, d_rules,
+                                n_rules > 0 ? d_ranges : nullptr, s))
+    return rc;
   LazyTopkParams a;
   a.n_pods = n_pods;
   a.N = N;
@@ -354,6 +393,7 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_rules,
   a.pres_t = t.pres_t;
   a.WM = WM;
   a.desc = d_desc;
+  a.ranges = d_ranges;
   a.K = g.max_cards;
   a.Q = g.n_res;
   a.C = max_containers;
