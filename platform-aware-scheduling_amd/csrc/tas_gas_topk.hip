@@ -37,6 +37,9 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+#ifndef PAS_LAZY_GROUP
+#define PAS_LAZY_GROUP 1  // pods bucketed by order row first (0: index order)
+#endif
 constexpr int kWaves = kTpb / 64;
 constexpr int kRuleBatch = 8;  // rule gathers in flight per lane
 constexpr int kMaxRes = PAS_GAS_MAX_RES;
@@ -54,7 +57,9 @@ struct LazyTopkParams {
   const uint64_t* pres_t;   // [N][WM]
   int32_t WM;
   const int4* desc;       // [2P] pods bucketed by order row (tas_group_launch)
-  const int2* ranges;     // [n_rules] each rule's range of its metric's ascending order
+  const int64_t* sorted;  // [M][R] ascending present values; fences f1k [M][R/1024], f32
+  const int64_t* f1k;
+  const int64_t* f32;
   // GAS snapshot (same nodes) and the pods' requests
   int32_t K, Q, C, i915;
   const int32_t* n_cards;
@@ -145,6 +150,50 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
   return true;
 }
 
+// Positions [lb, ub) of value t (milli) in metric m's ascending column (c present values),
+// found by the pod's 32 lanes in three rounds of loads, as the eval prep's range search does
+// (tas_eval.hip ranges_group): the 1024-stride fences, the 32-stride fences of one block, the
+// 32 values of one 32-block.  lb = values < t, ub = values <= t.
+__device__ void half_bounds(const LazyTopkParams& a, int32_t m, int32_t c, int64_t t, int sub,
+                            uint64_t half_mask, int32_t* lb, int32_t* ub) {
+  const int64_t* sv = a.sorted + (int64_t)m * a.R;
+  const int64_t* f1 = a.f1k + (int64_t)m * (a.R >> 10);
+  const int64_t* f2 = a.f32 + (int64_t)m * (a.R >> 5);
+  const int32_t na = (c + 1023) >> 10, nb = (c + 31) >> 5;
+  int32_t cl = 0, cu = 0;
+  for (int32_t i0 = 0; i0 < na; i0 += 8 * 32) {
+    int64_t v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = f1[min(i0 + u * 32 + sub, max(na - 1, 0))];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool in = i0 + u * 32 + sub < na;
+      cl += in && v[u] < t;
+      cu += in && v[u] <= t;
+    }
+  }
+#pragma unroll
+  for (int off = 16; off > 0; off >>= 1) {  // (xor within the half)
+    cl += __shfl_xor(cl, off, 64);
+    cu += __shfl_xor(cu, off, 64);
+  }
+  const int32_t n1l = cl, n1u = cu;
+  const int32_t b1l = max(n1l - 1, 0), b1u = max(n1u - 1, 0);
+  const int32_t e2l = n1l ? min(32, nb - b1l * 32) : 0, e2u = n1u ? min(32, nb - b1u * 32) : 0;
+  const int64_t x2l = f2[b1l * 32 + min(sub, max(e2l - 1, 0))];
+  const int64_t x2u = f2[b1u * 32 + min(sub, max(e2u - 1, 0))];
+  const int32_t n2l = __popcll(__ballot(sub < e2l && x2l < t) & half_mask);
+  const int32_t n2u = __popcll(__ballot(sub < e2u && x2u <= t) & half_mask);
+  const int32_t b2l = b1l * 32 + max(n2l - 1, 0), b2u = b1u * 32 + max(n2u - 1, 0);
+  const int32_t e3l = n1l ? min(32, c - b2l * 32) : 0, e3u = n1u ? min(32, c - b2u * 32) : 0;
+  const int64_t x3l = sv[b2l * 32 + min(sub, max(e3l - 1, 0))];
+  const int64_t x3u = sv[b2u * 32 + min(sub, max(e3u - 1, 0))];
+  const int32_t n3l = __popcll(__ballot(sub < e3l && x3l < t) & half_mask);
+  const int32_t n3u = __popcll(__ballot(sub < e3u && x3u <= t) & half_mask);
+  *lb = n1l ? b2l * 32 + n3l : 0;
+  *ub = n1u ? b2u * 32 + n3u : 0;
+}
+
 constexpr int kPodLanes = 32;                // lanes per pod (order positions per round)
 constexpr int kPodsPerWave = 64 / kPodLanes;
 constexpr int kPodsPerBlock = kWaves * kPodsPerWave;
@@ -159,9 +208,24 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
   const int32_t xcd = b & 7, per = nb >> 3, rem = nb & 7;
   const int32_t slot = xcd * per + min(xcd, rem) + (b >> 3);
   const int32_t pos = slot * kPodsPerBlock + (int32_t)(threadIdx.x >> 6) * kPodsPerWave + half;
+  const uint64_t half_mask = half ? ~0ull << 32 : 0xFFFFFFFFull;
+  const uint64_t below = half_mask & ((1ull << lane) - 1ull);
   const bool have = pos < a.n_pods;
-  const int4 d0 = have ? a.desc[2 * pos] : make_int4(0, -1, 0, 0);
-  const int4 d1 = have ? a.desc[2 * pos + 1] : make_int4(0, 0, 0, 0);
+  int4 d0 = make_int4(0, -1, 0, 0), d1 = make_int4(0, 0, 0, 0);
+  if (a.desc) {  // bucketed by order row
+    if (have) {
+      d0 = a.desc[2 * pos];
+      d1 = a.desc[2 * pos + 1];
+    }
+  } else if (have) {  // index order: the same descriptor, computed here
+    const pas_rule q = a.prio[pos];
+    const int32_t cq = (q.metric >= 0 && q.metric < a.M) ? a.cnt[q.metric] : 0;
+    const int oq = q.op == PAS_OP_GREATER_THAN ? kOrderDesc
+                   : q.op == PAS_OP_LESS_THAN  ? kOrderAsc
+                                               : kOrderIndex;
+    d0 = make_int4(pos, cq > 0 ? oq * a.M + q.metric : -1, cq, 0);
+    d1 = make_int4(a.rule_off[pos], a.rule_off[pos + 1], 0, 0);
+  }
   const int32_t p = d0.x;
   const int32_t k = a.k;
   const pas_rule pr = a.prio[p];
@@ -192,29 +256,37 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
 #pragma unroll
   for (int i = 0; i < kSkip; ++i) slo[i] = shi[i] = 0;
   const int ord = d0.y >= 0 ? d0.y / a.M : kOrderIndex;
-  if (c0 > 0 && ord != kOrderIndex) {
-    for (int32_t r = r0; r < r1; ++r) {
-      const pas_rule ru = a.rules[r];
-      if (ru.metric != pr.metric || ru.op < 0 || ru.op > 2) continue;
-      const int2 g = a.ranges[r];
-      const int32_t lo = ord == kOrderDesc ? c0 - g.y : g.x;
-      const int32_t hi = ord == kOrderDesc ? c0 - g.x : g.y;
-      if (hi <= lo) continue;
+  const bool sorted_row = c0 > 0 && ord != kOrderIndex;
+  for (int32_t r = r0; __ballot(sorted_row && r < r1); ++r) {
+    const pas_rule ru = a.rules[min(r, max(r1 - 1, 0))];
+    const bool same = sorted_row && r < r1 && ru.metric == pr.metric && ru.op >= 0 && ru.op <= 2;
+    if (!__ballot(same)) continue;
+    int64_t tm = 0;
+    const int sat = target_milli(ru.target, &tm);
+    int32_t lb = 0, ub = 0;
+    half_bounds(a, same ? pr.metric : 0, same ? c0 : 0, tm, sub, half_mask, &lb, &ub);
+    if (sat != 0) lb = ub = sat > 0 ? c0 : 0;
+    if (same) {
+      // the rule's nodes in ascending positions, mirrored for the descending row
+      const int32_t gx = ru.op == PAS_OP_LESS_THAN ? 0 : ru.op == PAS_OP_GREATER_THAN ? ub : lb;
+      const int32_t gy = ru.op == PAS_OP_LESS_THAN ? lb : ru.op == PAS_OP_GREATER_THAN ? c0 : ub;
+      const int32_t lo = ord == kOrderDesc ? c0 - gy : gx;
+      const int32_t hi = ord == kOrderDesc ? c0 - gx : gy;
+      if (hi > lo) {
 #pragma unroll
-      for (int i = 0; i < kSkip; ++i)
-        if (i == ns) {
-          slo[i] = lo;
-          shi[i] = hi;
-        }
-      ns = min(ns + 1, kSkip);
+        for (int i = 0; i < kSkip; ++i)
+          if (i == ns) {
+            slo[i] = lo;
+            shi[i] = hi;
+          }
+        ns = min(ns + 1, kSkip);
+      }
     }
   }
   const int32_t* row = a.perm + (int64_t)(d0.y >= 0 ? d0.y : 0) * a.R;
   const int64_t* mcol = a.vals + (int64_t)(d0.y >= 0 ? pr.metric : 0) * a.N;
   int64_t* keys = a.key_out + (int64_t)p * k;
   int32_t* nodes = a.node_out + (int64_t)p * k;
-  const uint64_t half_mask = half ? ~0ull << 32 : 0xFFFFFFFFull;
-  const uint64_t below = half_mask & ((1ull << lane) - 1ull);
   int32_t kept = 0;
   for (int32_t j0 = 0;; j0 += kPodLanes) {
 #pragma unroll
@@ -352,11 +424,11 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
     PAS_HIP(ctx, hipGetLastError());
     t.t_epoch = t.epoch;
   }
-  // scratch: desc [2P] | keys [P] | ranges [n_rules]
+  // scratch: desc [2P] | keys [P] of the grouping
   auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
   const size_t b_desc = al(sizeof(int4) * 2 * (size_t)n_pods), b_keys = al(sizeof(int2) * n_pods);
-  const size_t b_rng = al(sizeof(int2) * (size_t)std::max(n_rules, 1));
-  if (b_desc + b_keys + b_rng > ctx->aux_bytes) {
+  const size_t b_rng = 0;
+  if (PAS_LAZY_GROUP && b_desc + b_keys + b_rng > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
       PAS_HIP(ctx, hipFree(ctx->aux));
@@ -368,12 +440,13 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
   }
   int4* d_desc = static_cast<int4*>(ctx->aux);
   int2* d_keys = reinterpret_cast<int2*>(static_cast<char*>(ctx->aux) + b_desc);
-  int2* d_ranges = reinterpret_cast<int2*>(static_cast<char*>(ctx->aux) + b_desc + b_keys);
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_GAS_TOPK, &tl);
-  if (int rc = tas_group_launch(ctx, n_pods, d_prio, d_rule_off, d_desc, d_keys, n_rules, d_rules,
-                                n_rules > 0 ? d_ranges : nullptr, s))
-    return rc;
+  if (PAS_LAZY_GROUP) {
+    if (int rc = tas_group_launch(ctx, n_pods, d_prio, d_rule_off, d_desc, d_keys, 0, nullptr,
+                                  nullptr, s))
+      return rc;
+  }
   LazyTopkParams a;
   a.n_pods = n_pods;
   a.N = N;
@@ -392,8 +465,10 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
   a.vals_t = t.vals_t;
   a.pres_t = t.pres_t;
   a.WM = WM;
-  a.desc = d_desc;
-  a.ranges = d_ranges;
+  a.desc = PAS_LAZY_GROUP ? d_desc : nullptr;
+  a.sorted = t.sorted;
+  a.f1k = t.f1k;
+  a.f32 = t.f32;
   a.K = g.max_cards;
   a.Q = g.n_res;
   a.C = max_containers;
