@@ -38,7 +38,8 @@ namespace {
 
 constexpr int kTpb = 256;
 #ifndef PAS_LAZY_GROUP
-#define PAS_LAZY_GROUP 1  // pods bucketed by order row first (0: index order)
+#define PAS_LAZY_GROUP 0  // 1: pods bucketed by order row first (measured slower: the one-block
+                          // grouping of 64k pods costs more than the L2 locality gains)
 #endif
 constexpr int kWaves = kTpb / 64;
 constexpr int kRuleBatch = 8;  // rule gathers in flight per lane
