@@ -32,6 +32,18 @@
 // decode but not this one — parity unpinned for such bodies, which no kube-scheduler sends).
 #include <emmintrin.h>
 
+#ifdef PAS_DECODE_TRACE  // diagnostic builds: phase times of the threaded decode on stderr
+#include <chrono>
+#include <cstdio>
+#define PAS_TRACE_T0(v) const auto v = std::chrono::steady_clock::now()
+#define PAS_TRACE_MS(msg, v)                                                       \
+  std::fprintf(stderr, "decode %s %.3f ms\n", msg,                                \
+               std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v).count())
+#else
+#define PAS_TRACE_T0(v)
+#define PAS_TRACE_MS(msg, v)
+#endif
+
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -747,6 +759,7 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
     empty = w.p == w.end;
   }
   const int T = std::max(1, std::min<int>(idx->threads, (int)(n_items / 256)));
+  PAS_TRACE_T0(t_items);
   if (!empty &&
       !parallel_for(T, [&](int t) {
         const size_t lo = n_items * (size_t)t / (size_t)T, hi = n_items * (size_t)(t + 1) / (size_t)T;
@@ -767,6 +780,7 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
         }
       }))
     return false;
+  PAS_TRACE_MS("items", t_items);
   if (!ok.load()) return false;
   if (empty) {
     names.clear();
@@ -865,7 +879,9 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
   if (which == PAS_ARGS_NODES && (index.threads = decode_threads_for(len)) > 1) {
     index.body = body;
     index.len = len;
+    PAS_TRACE_T0(t_index);
     index.build();
+    PAS_TRACE_MS("index", t_index);
     idx = &index;
   }
   NodeList nodes;
@@ -980,11 +996,13 @@ int pas_decode_args(const pas_name_table* t, const char* body, int64_t len, int3
       if (fits) req_node[i] = id;
     }
   };
+  PAS_TRACE_T0(t_lookup);
   if (T <= 1 || !parallel_for(T, lookup)) {
     std::fill(unknown.begin(), unknown.end(), 0);
     if (cand) std::memset(cand, 0, sizeof(uint64_t) * ((t->names.size() + 63) / 64));
     for (int th = 0; th < T; ++th) lookup(th);
   }
+  PAS_TRACE_MS("lookups", t_lookup);
   for (int32_t u : unknown) info->n_unknown += u;
   if (!fits) return PAS_ECAPACITY;
   if (item_span && !spans.empty())
