@@ -44,9 +44,14 @@
 #define PAS_TRACE_MS(msg, v)
 #endif
 
+#include <unistd.h>
+
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstdint>
+#include <functional>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -500,6 +505,7 @@ bool decode_node(Scanner& s, std::string* name) {
 
 struct ItemIndex;
 bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out);
+void item_list_changed(ItemIndex* idx);
 
 // v1.NodeList: items (null sets the slice to nil).  idx (optional): the body's structural
 // index; the first decode of a NodeList's items array goes through it in parallel.
@@ -507,6 +513,7 @@ bool decode_node_list(Scanner& s, NodeList* out, const char* base, ItemIndex* id
   return s.object([&](std::string_view k) {
     if (fold_match("items", k)) {
       const char c = s.peek();
+      if (idx) item_list_changed(idx);
       if (c == 'n') {
         out->names.clear();
         out->spans.clear();
@@ -577,20 +584,111 @@ int decode_threads_for(int64_t len) {
   return (int)std::max<int64_t>(1, t);
 }
 
-// f(i) for i in [0, n): i = 0 on the calling thread.  Returns false (nothing run on other
-// threads) when a thread cannot be started.
+// Worker threads kept across calls (a decode runs four parallel steps; starting 15 threads
+// per step cost ~0.3 ms each on the GPU box).  One parallel step at a time uses the pool; a
+// concurrent call (another goroutine's request) starts threads of its own instead.  After a
+// fork the child gets a new pool (the parent's workers do not exist there).
+class WorkerPool {
+ public:
+  static WorkerPool* get() {
+    static std::mutex mk;
+    static WorkerPool* pool = nullptr;
+    std::lock_guard<std::mutex> g(mk);
+    if (!pool || pool->pid_ != getpid()) pool = new WorkerPool();  // (never freed: process-wide)
+    return pool;
+  }
+  // Runs f(i) for i in [0, n) on the caller and up to n - 1 workers; false if the pool is busy
+  // or cannot grow (nothing run).
+  bool run(int n, const std::function<void(int)>& f) {
+    std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    try {
+      while ((int)workers_.size() < n - 1) workers_.emplace_back([this] { loop(); });
+    } catch (...) {
+      return false;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      task_ = &f;
+      n_ = n;
+      next_.store(0);
+      pending_ = n;
+      ++epoch_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(m_);
+    done_.wait(g, [this] { return pending_ == 0; });
+    task_ = nullptr;
+    return true;
+  }
+
+ private:
+  WorkerPool() : pid_(getpid()) {}
+  void work() {
+    for (int i; (i = next_.fetch_add(1)) < n_;) {
+      (*task_)(i);
+      std::lock_guard<std::mutex> g(m_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(m_);
+        cv_.wait(g, [&] { return epoch_ != seen && task_ != nullptr; });
+        seen = epoch_;
+      }
+      work();
+    }
+  }
+  const pid_t pid_;
+  std::mutex busy_, m_;
+  std::condition_variable cv_, done_;
+  std::vector<std::thread> workers_;
+  const std::function<void(int)>* task_ = nullptr;
+  int n_ = 0, pending_ = 0;
+  std::atomic<int> next_{0};
+  uint64_t epoch_ = 0;
+};
+
+// f(i) for i in [0, n), on the pool (or fresh threads when it is busy).  Returns false
+// (nothing run) when no thread can be started.
 template <class F>
 bool parallel_for(int n, F&& f) {
-  std::vector<std::thread> th;
-  try {
-    th.reserve((size_t)std::max(n - 1, 0));
-    for (int i = 1; i < n; ++i) th.emplace_back([&f, i] { f(i); });
-  } catch (...) {
+#ifdef PAS_DECODE_TRACE
+  std::vector<double> busy((size_t)n, 0.0);
+  PAS_TRACE_T0(t_spawn);
+  auto g = [&](int i) {
+    PAS_TRACE_T0(t_run);
+    f(i);
+    busy[(size_t)i] =
+        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_run).count();
+  };
+#else
+  auto& g = f;
+#endif
+  const std::function<void(int)> fn = [&g](int i) { g(i); };
+  bool ran = n <= 1 ? (g(0), true) : WorkerPool::get()->run(n, fn);
+  if (!ran) {
+    std::vector<std::thread> th;
+    try {
+      th.reserve((size_t)std::max(n - 1, 0));
+      for (int i = 1; i < n; ++i) th.emplace_back([&g, i] { g(i); });
+    } catch (...) {
+      for (auto& x : th) x.join();
+      return false;
+    }
+    g(0);
     for (auto& x : th) x.join();
-    return false;
   }
-  f(0);
-  for (auto& x : th) x.join();
+#ifdef PAS_DECODE_TRACE
+  PAS_TRACE_MS("parallel step", t_spawn);
+  std::fprintf(stderr, "decode busy max %.3f min %.3f ms (n=%d)\n",
+               *std::max_element(busy.begin(), busy.end()),
+               *std::min_element(busy.begin(), busy.end()), n);
+#endif
   return true;
 }
 
@@ -653,6 +751,11 @@ struct ItemIndex {
   int threads = 1;
   bool built = false;
   std::vector<int64_t> events;  // pos * 2 + 1: closing of a depth-3 container; pos * 2: comma
+  // the items' snapshot ids, looked up by the threads that decoded them (table set): valid
+  // while no later key changed the list (ids_mods == mods)
+  const pas_name_table* table = nullptr;
+  std::vector<int32_t> ids;
+  uint64_t mods = 0, ids_mods = ~0ull;
 
   // Walks the 64-byte blocks of [b, e) (the last one padded with spaces): f(block start,
   // masks, escaped bytes), the escape state carried from the backslash run before b.
@@ -709,23 +812,25 @@ struct ItemIndex {
           uint64_t instr = in0[t] ? ~0ull : 0ull;
           int64_t depth = depth0[t];
           std::vector<int64_t>& out = ev[t];
-          blocks(b, e, [&](int64_t x, const char* p, const Masks& m, uint64_t esc) {
+          blocks(b, e, [&](int64_t x, const char*, const Masks& m, uint64_t esc) {
             const uint64_t mask = prefix_xor(m.quote & ~esc) ^ instr;
             instr = (mask >> 63) ? ~0ull : 0ull;
-            uint64_t bits = (m.open | m.close | m.comma) & ~mask;
-            while (bits) {
-              const int i = __builtin_ctzll(bits);
-              bits &= bits - 1;
-              const char ch = p[i];
-              if (ch == ',') {
-                if (depth == 3) out.push_back((x + i) * 2);
-              } else if (ch == '{' || ch == '[') {
-                ++depth;
-              } else {
-                if (depth == 3) out.push_back((x + i) * 2 + 1);
-                --depth;
+            const uint64_t op = m.open & ~mask, cl = m.close & ~mask;
+            const int no = __builtin_popcountll(op), nc = __builtin_popcountll(cl);
+            // the depth stays within [depth - nc, depth + no] in this block: most blocks lie
+            // inside an item (depth >= 4) and hold no depth-3 comma or closing
+            if (depth - nc <= 3 && depth + no >= 3) {
+              uint64_t ev = (cl | m.comma) & ~mask;
+              while (ev) {
+                const int i = __builtin_ctzll(ev);
+                const uint64_t bit = 1ull << i, below = bit - 1;
+                ev &= ev - 1;
+                // depth just before byte i
+                if (depth + __builtin_popcountll(op & below) - __builtin_popcountll(cl & below) == 3)
+                  out.push_back((x + i) * 2 + ((cl & bit) ? 1 : 0));
               }
             }
+            depth += no - nc;
           });
         }))
       return;
@@ -736,6 +841,8 @@ struct ItemIndex {
     built = true;
   }
 };
+
+void item_list_changed(ItemIndex* idx) { ++idx->mods; }
 
 // The items array at s.p ('[' of the first items key of a NodeList at depth 2) decoded in
 // parallel; false (s untouched) to decode it sequentially instead.
@@ -751,6 +858,7 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
   const size_t n_items = cut.size() - 1;
   std::vector<std::string> names(n_items);
   std::vector<int64_t> spans(2 * n_items);
+  std::vector<int32_t> ids(idx->table ? n_items : 0);
   std::atomic<bool> ok{true};
   bool empty = false;
   if (n_items == 1) {  // "[]" (whitespace only) or one item
@@ -758,7 +866,11 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
     w.ws();
     empty = w.p == w.end;
   }
+#ifdef PAS_DECODE_ITEMS_T1  // diagnostic: the items on one thread
+  const int T = 1;
+#else
   const int T = std::max(1, std::min<int>(idx->threads, (int)(n_items / 256)));
+#endif
   PAS_TRACE_T0(t_items);
   if (!empty &&
       !parallel_for(T, [&](int t) {
@@ -777,6 +889,7 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
           }
           spans[2 * i] = (int64_t)(b - idx->body);
           spans[2 * i + 1] = (int64_t)(e - b);
+          if (idx->table) ids[i] = idx->table->find(names[i]);
         }
       }))
     return false;
@@ -788,6 +901,11 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
   }
   out->names = std::move(names);
   out->spans = std::move(spans);
+  if (idx->table) {
+    if (empty) ids.clear();
+    idx->ids = std::move(ids);
+    idx->ids_mods = idx->mods;
+  }
   s.p = idx->body + cut.back() + 1;
   return true;
 }
@@ -869,9 +987,12 @@ namespace {
 
 // Decode of extender.Args shared by pas_decode_args / pas_decode_request_names: the chosen
 // list's names (unescaped, request order), the item spans and the Pod span.
+// table / ids (optional): the items' snapshot ids, looked up by the decoding threads; *ids
+// is left empty when they were not (small body, or the list changed after the fast path).
 int decode_args_core(const char* body, int64_t len, int32_t which,
                      std::vector<std::string>* names, std::vector<int64_t>* spans,
-                     pas_args_info* info) {
+                     pas_args_info* info, const pas_name_table* table = nullptr,
+                     std::vector<int32_t>* ids = nullptr) {
   std::memset(info, 0, sizeof *info);
   Scanner s{body, body + len};
   ItemIndex index;
@@ -879,6 +1000,7 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
   if (which == PAS_ARGS_NODES && (index.threads = decode_threads_for(len)) > 1) {
     index.body = body;
     index.len = len;
+    index.table = ids ? table : nullptr;
     PAS_TRACE_T0(t_index);
     index.build();
     PAS_TRACE_MS("index", t_index);
@@ -910,6 +1032,7 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
         return true;
       }
       if (fold_match("Nodes", k)) {
+        if (idx) item_list_changed(idx);
         const char c = s.peek();
         if (c == 'n') {
           has_nodes = false;
@@ -955,6 +1078,9 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
     info->pod_len = (int64_t)(pod_e - pod_b);
   }
   if (which == PAS_ARGS_NODES) {
+    if (ids && idx && idx->table && idx->ids_mods == idx->mods &&
+        idx->ids.size() == nodes.names.size())
+      *ids = std::move(idx->ids);
     *names = std::move(nodes.names);
     if (spans) *spans = std::move(nodes.spans);
   } else {
@@ -977,10 +1103,26 @@ int pas_decode_args(const pas_name_table* t, const char* body, int64_t len, int3
     return PAS_EINVAL;
   std::vector<std::string> names;
   std::vector<int64_t> spans;
-  const int rc = decode_args_core(body, len, which, &names, item_span ? &spans : nullptr, info);
+  std::vector<int32_t> ids;
+  const int rc = decode_args_core(body, len, which, &names, item_span ? &spans : nullptr, info,
+                                  t, &ids);
   if (rc != PAS_OK) return rc;
   if (cand) std::memset(cand, 0, sizeof(uint64_t) * ((t->names.size() + 63) / 64));
   const bool fits = (int64_t)names.size() <= node_cap;
+  if (!ids.empty() || names.empty()) {  // looked up by the threads that decoded the items
+    for (size_t i = 0; i < ids.size(); ++i) {
+      const int32_t id = ids[i];
+      if (id < 0)
+        ++info->n_unknown;
+      else if (cand)
+        cand[id >> 6] |= 1ull << (id & 63);
+      if (fits) req_node[i] = id;
+    }
+    if (!fits) return PAS_ECAPACITY;
+    if (item_span && !spans.empty())
+      std::memcpy(item_span, spans.data(), sizeof(int64_t) * spans.size());
+    return PAS_OK;
+  }
   // name lookups, split over host threads for a large request (candidate bits or-ed in)
   const size_t n = names.size();
   const int T = n >= 16384 ? decode_threads_for(len) : 1;
