@@ -244,15 +244,19 @@ int pas_label_patch_json(int32_t n_strategies, const char* const* names, uint64_
 
 #define PAS_GAS_MAX_CARDS 64      /* cards per node (label gpu.intel.com/cards entries) */
 #define PAS_GAS_MAX_RES 4         /* gpu.intel.com/ resource kinds per batch */
-#define PAS_GAS_MAX_SELECTIONS 64 /* card selections per pod: sum over containers of i915 */
+#define PAS_GAS_MAX_SELECTIONS 64 /* card selections per pod reported in cards / side records;
+                                     pods with more are evaluated exactly (PAS_GAS_SEL_LIMIT) */
 #define PAS_GAS_PACKED 8          /* selections / card ranks the packed result word holds */
 #define PAS_REQ_UNKNOWN_KIND 0x80000000u /* req_mask: requests a kind the snapshot lacks */
 /* bits 24-27 of a result word besides a count S <= PAS_GAS_PACKED: */
 #define PAS_GAS_SEL_EXTENDED 15   /* the pod fits (bit 31 set) but its card selection does not
                                      pack: more than 8 selections or a card rank >= 8; the
                                      selection is in the side buffer of pas_gas_fit_ex */
-#define PAS_GAS_SEL_LIMIT 14      /* more than PAS_GAS_MAX_SELECTIONS selections: not evaluated
-                                     (bit 31 clear), counted by pas_gas_limit_count */
+#define PAS_GAS_SEL_LIMIT 14      /* the pod fits (bit 31 set) with more than
+                                     PAS_GAS_MAX_SELECTIONS selections: neither packed nor in
+                                     the side buffer; pas_gas_bind_counts reports them per
+                                     container and card.  Such pods are counted by
+                                     pas_gas_limit_count */
 
 /* Card selection of one (pod, node) that does not fit the packed word (PAS_GAS_SEL_EXTENDED):
  * card[0 .. n_sel) are the ranks of the node's cards, selection by selection (containers in
@@ -311,9 +315,10 @@ int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
  *              "gas-container-cards" annotation (:317-335) in packed form; 0 otherwise.
  * The reference has no limit on selections per pod or cards per node (scheduler.go:200-257;
  * the GPU plugin's -shared-dev-num lets one card take many selections); here nodes may have
- * up to PAS_GAS_MAX_CARDS cards and pods up to PAS_GAS_MAX_SELECTIONS selections.  The host
- * call returns PAS_ECAPACITY for a pod beyond that; the _device calls mark its words
- * PAS_GAS_SEL_LIMIT (bitmap bits 0) and count the pods (pas_gas_limit_count). */
+ * up to PAS_GAS_MAX_CARDS cards, and pods any number of selections (numI915 up to INT64_MAX
+ * per container): a container's selections are runs on ascending cards (a card first fit
+ * passes over never fits again within the container), evaluated in O(cards).  A fitting pod
+ * of more than PAS_GAS_MAX_SELECTIONS selections gets bit 31 | PAS_GAS_SEL_LIMIT << 24. */
 int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out);
@@ -335,8 +340,8 @@ int pas_gas_fit_ex_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t ma
                           pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
                           void* hip_stream);
 
-/* Pods of the last GAS fit call on this context beyond PAS_GAS_MAX_SELECTIONS (their words
- * are PAS_GAS_SEL_LIMIT, their bitmap bits 0).  Waits for the call's stream. */
+/* Pods of the last GAS fit call on this context with more than PAS_GAS_MAX_SELECTIONS
+ * selections (their fitting words are PAS_GAS_SEL_LIMIT).  Waits for the call's stream. */
 int pas_gas_limit_count(pas_ctx* ctx, int64_t* n_pods_out);
 
 /* GAS filter verdicts only, as node bitmaps fit_out[n_pods][W64(n_nodes)] (bit = bit 31 of
@@ -366,13 +371,27 @@ int pas_gas_bind(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_bin
                  int32_t* status_out);
 /* pas_gas_bind plus every bind's full card selection: cards_out[b][0 .. n_sel_out[b]) (ranks,
  * selection by selection; n_sel_out 0 when it does not fit), for selections that do not
- * pack into the result word. */
+ * pack into the result word.  A bind of more than PAS_GAS_MAX_SELECTIONS selections has
+ * n_sel_out -1 and cards_out zero: pas_gas_bind_counts reports it. */
 int pas_gas_bind_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
                     const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
                     int32_t max_containers, int32_t i915_index, const int64_t* req,
                     const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
                     int32_t* status_out, uint8_t* cards_out /*[n_binds][64]*/,
                     int32_t* n_sel_out);
+
+/* pas_gas_bind with every bind's selection as counts, for any number of selections:
+ * counts_out[b][c][k] = the selections container c made on card k (int64; all 0 when the
+ * bind does not fit).  Within a container the selections are in ascending card order (first
+ * fit with one per-GPU request never returns to a card it has passed), so the counts are the
+ * "gas-container-cards" annotation: container c lists card k counts_out[b][c][k] times, in
+ * card order (scheduler.go:200-257, 317-335). */
+int pas_gas_bind_counts(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
+                        const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
+                        int32_t max_containers, int32_t i915_index, const int64_t* req,
+                        const uint32_t* req_mask, const int32_t* n_containers,
+                        uint32_t* res_out, int32_t* status_out,
+                        int64_t* counts_out /*[n_binds][max_containers][max_cards]*/);
 
 /* Pods leaving nodes: Cache.adjustPodResources(remove) (node_resource_cache.go:240-287) with
  * each pod's annotation, in call order.  Container c of release r has cards_per_container
@@ -393,6 +412,17 @@ int pas_gas_release_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t
                        int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
                        const int32_t* n_containers, const int32_t* cards_per_container,
                        const int32_t* cards, int32_t* status_out);
+
+/* pas_gas_release with each annotation as counts[r][c][k] (container c lists card k that many
+ * times; numCards = the row's sum), for annotations of any length.  Negative counts or a row
+ * sum past INT64_MAX: PAS_EINVAL; a count on a card rank >= the node's n_cards: input error
+ * (status PAS_GAS_ERR_INPUT), as a card the label does not list. */
+int pas_gas_release_counts(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to,
+                           int32_t n_releases, const int32_t* rel_pod, const int32_t* rel_node,
+                           int32_t n_pods, int32_t max_containers, const int64_t* req,
+                           const uint32_t* req_mask, const int32_t* n_containers,
+                           const int64_t* counts /*[n_releases][max_containers][max_cards]*/,
+                           int32_t* status_out);
 
 /* Read back the resident usage used[N][K][Q] and its generation. */
 int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out);
@@ -426,8 +456,8 @@ int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
  * the fit bitmaps (intersected with d_cand) as candidates, but evaluated along each pod's
  * order: a node is filtered and fitted only until k nodes are kept, so a pod costs about
  * k / (pass rate) node evaluations instead of the shard's n_nodes.  The GAS arguments are
- * those of pas_gas_fit_device; a pod past PAS_GAS_MAX_SELECTIONS fits no node (len 0).  The
- * two snapshots must hold the same number of nodes (PAS_EINVAL otherwise). */
+ * those of pas_gas_fit_device (any number of selections).  The two snapshots must hold the
+ * same number of nodes (PAS_EINVAL otherwise). */
 int pas_tas_gas_topk_device(pas_ctx* ctx, uint64_t tas_gen, uint64_t gas_gen, int32_t n_pods,
                             int32_t n_rules, const pas_rule* d_rules, const int32_t* d_rule_off,
                             const pas_rule* d_prio, const uint64_t* d_cand,

@@ -51,14 +51,16 @@ def load():
         "or_rm_subtract": (c_int, [POINTER(OrRm), c_int32, c_int64]),
         "or_rm_add_rm": (c_int, [POINTER(OrRm), POINTER(OrRm)]),
         "or_rm_subtract_rm": (c_int, [POINTER(OrRm), POINTER(OrRm)]),
-        "or_rm_divide": (c_int, [POINTER(OrRm), c_int32]),
+        "or_rm_divide": (c_int, [POINTER(OrRm), c_int64]),
         "or_check_resource_capacity": (c_int, [POINTER(OrRm), POINTER(OrRm), POINTER(OrRm)]),
         "or_gas_fit_ex": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
                                   P, P, P, P, P, P]),
         "or_gas_fit": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, c_int32, c_int32,
                                P, P, P, P]),
         "or_gas_bind": (c_int, [c_int32, c_int32, c_int32, P, P, P, c_int32, P, P, c_int32,
-                                c_int32, P, P, P, P, P, P, P]),
+                                c_int32, P, P, P, P, P, P, P, P]),
+        "or_gas_release_counts": (c_int, [c_int32, c_int32, c_int32, P, P, c_int32, P, P,
+                                          c_int32, P, P, P, P, P]),
         "or_gas_release": (c_int, [c_int32, c_int32, c_int32, P, P, c_int32, P, P, c_int32,
                                    P, P, P, P, P, c_int32, P]),
         "or_label_plan": (c_int, [c_int32, c_int32, P, P, P, P, P]),
@@ -142,7 +144,8 @@ SEL_LIMIT = 14
 
 
 def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index, selections=False):
-    """Result words [P][N]; with selections=True also (sel [P][N][64] uint8, nsel [P][N])."""
+    """Result words [P][N]; with selections=True also (sel [P][N][64] uint8, nsel [P][N];
+    nsel -1 and sel zero for a fitting pod of more than 64 selections)."""
     n_cards = np.ascontiguousarray(n_cards, np.int32)
     cap = np.ascontiguousarray(cap, np.int64)
     used = np.ascontiguousarray(used, np.int64)
@@ -163,9 +166,10 @@ def gas_fit(n_cards, cap, used, req, req_mask, n_containers, i915_index, selecti
 
 
 def gas_bind(n_cards, cap, used, req, req_mask, n_containers, i915_index, pods, nodes,
-             selections=False):
+             selections=False, counts=False):
     """Binds in order (bindNode: runSchedulingLogic + adjustPodResources(add)).
-    Returns (used after, result words, statuses) [+ (cards [B][64], nsel [B])]."""
+    Returns (used after, result words, statuses) [+ (cards [B][64], nsel [B])]
+    [+ (counts [B][C][K] selections per container and card,)]."""
     n_cards = np.ascontiguousarray(n_cards, np.int32)
     cap = np.ascontiguousarray(cap, np.int64)
     used = np.array(used, np.int64, copy=True, order="C")
@@ -181,12 +185,14 @@ def gas_bind(n_cards, cap, used, req, req_mask, n_containers, i915_index, pods, 
     st = np.zeros(b, np.int32)
     cards = np.zeros((b, MAX_SEL), np.uint8)
     nsel = np.zeros(b, np.int32)
+    cnt = np.zeros((b, c, k), np.int64)
     rc = load().or_gas_bind(n, k, q, _p(n_cards), _p(cap), _p(used), b, _p(pods), _p(nodes), c,
                             i915_index, _p(req), _p(req_mask), _p(n_containers), _p(res),
-                            _p(st), _p(cards), _p(nsel))
+                            _p(st), _p(cards), _p(nsel), _p(cnt))
     if rc != 0:
         raise ValueError(f"oracle gas_bind failed: {rc}")
-    return (used, res, st, cards, nsel) if selections else (used, res, st)
+    out = (used, res, st) + ((cards, nsel) if selections else ())
+    return out + (cnt,) if counts else out
 
 
 def gas_release(n_cards, used, req, req_mask, n_containers, pods, nodes, cards_per_container,
@@ -211,6 +217,30 @@ def gas_release(n_cards, used, req, req_mask, n_containers, pods, nodes, cards_p
                                cards.shape[1] if r else 8, _p(st))
     if rc != 0:
         raise ValueError(f"oracle gas_release failed: {rc}")
+    return used, st
+
+
+def gas_release_counts(n_cards, used, req, req_mask, n_containers, pods, nodes, counts):
+    """gas_release with each annotation as counts [R][C][K] (cards per container and card).
+    Returns (used after, statuses)."""
+    n_cards = np.ascontiguousarray(n_cards, np.int32)
+    used = np.array(used, np.int64, copy=True, order="C")
+    req = np.ascontiguousarray(req, np.int64)
+    req_mask = np.ascontiguousarray(req_mask, np.uint32)
+    n_containers = np.ascontiguousarray(n_containers, np.int32)
+    pods = np.ascontiguousarray(pods, np.int32)
+    nodes = np.ascontiguousarray(nodes, np.int32)
+    counts = np.ascontiguousarray(counts, np.int64)
+    r = len(pods)
+    n, k, q = used.shape
+    c = req.shape[1]
+    assert counts.shape == (r, c, k)
+    st = np.zeros(r, np.int32)
+    rc = load().or_gas_release_counts(n, k, q, _p(n_cards), _p(used), r, _p(pods), _p(nodes), c,
+                                      _p(req), _p(req_mask), _p(n_containers), _p(counts),
+                                      _p(st))
+    if rc != 0:
+        raise ValueError(f"oracle gas_release_counts failed: {rc}")
     return used, st
 
 

@@ -360,7 +360,7 @@ int or_rm_subtract_rm(or_rm* rm, const or_rm* src) {
   return OR_RM_OK;
 }
 
-int or_rm_divide(or_rm* rm, int32_t divider) {
+int or_rm_divide(or_rm* rm, int64_t divider) {       /* Go int: 64 bits */
   if (divider < 1) return OR_RM_ERR_INPUT;             /* :130-134 */
   if (divider == 1) return OR_RM_OK;
   for (int32_t k = 0; k < OR_RM_MAX_KEYS; ++k)
@@ -386,21 +386,100 @@ int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const o
 
 /* ---- GAS runSchedulingLogic over the packed snapshot ---------------------- */
 
-/* The pod's card selections (getNumI915 summed over its containers, :192-198, 280-338),
- * saturating past OR_GAS_MAX_SEL. */
-static int64_t pod_selections(int32_t n_res, int32_t i915_index, int32_t max_containers,
-                              const int64_t* req, const uint32_t* req_mask,
-                              int32_t n_containers, int32_t p) {
-  int64_t sel = 0;
-  for (int32_t c = 0; c < n_containers; ++c) {
-    const int64_t base = (int64_t)p * max_containers + c;
-    const uint32_t mask = req_mask[base];
-    if (mask == 0 || i915_index < 0 || !(mask >> i915_index & 1u)) continue;
-    const int64_t v = req[base * n_res + i915_index];
-    if (v > 0) sel += v > OR_GAS_MAX_SEL ? OR_GAS_MAX_SEL + 1 : v;
-    if (sel > OR_GAS_MAX_SEL) return OR_GAS_MAX_SEL + 1;
+/* A growable list of card ranks: the pod's selections in order (the annotation). */
+typedef struct {
+  int32_t* v;
+  int64_t n, cap;
+} card_list;
+
+/* More selections than this: the literal loop would not finish in a test's time (the
+ * reference appends numI915 card names one by one); the oracle reports an error instead. */
+#define OR_SEL_LIST_MAX ((int64_t)1 << 26)
+
+static int list_push(card_list* l, int32_t k) {
+  if (l->n >= OR_SEL_LIST_MAX) return -1;
+  if (l->n == l->cap) {
+    const int64_t cap = l->cap ? 2 * l->cap : 256;
+    int32_t* v = (int32_t*)realloc(l->v, (size_t)cap * sizeof(int32_t));
+    if (!v) return -1;
+    l->v = v;
+    l->cap = cap;
   }
-  return sel;
+  l->v[l->n++] = k;
+  return 0;
+}
+
+/* runSchedulingLogic (:280-338) of pod p on node n over the packed snapshot, as the reference
+ * writes it: per container getPerGPUResourceRequest (:180-190), then numI915 times the first
+ * card in sort.Strings order passing checkResourceCapacity on the working copy, which then
+ * takes the request (addRM, :200-257).  No bound on numI915: the loop ends at the first
+ * selection no card fits.  Returns 1 (fits) / 0; the selections go to `sel` and, per
+ * container, their count to cont_n[c] (when not NULL).  -1 on allocation failure. */
+static int fit_one(int32_t max_cards, int32_t n_res, int32_t nc_node, const int64_t* cap_per_gpu,
+                   const int64_t* used, int32_t max_containers, int32_t i915_index,
+                   const int64_t* req, const uint32_t* req_mask, int32_t n_containers,
+                   card_list* sel, int64_t* cont_n) {
+  sel->n = 0;
+  for (int32_t c = 0; cont_n && c < max_containers; ++c) cont_n[c] = 0;
+  /* iCache.FetchNode error (:282-288) / no cards label -> errWontFit (:290-298) */
+  if (nc_node <= 0) return 0;
+  const int32_t ncard = nc_node < max_cards ? nc_node : max_cards;
+  or_rm capacity, node_used[OR_GAS_MAX_CARDS];
+  memset(&capacity, 0, sizeof capacity);
+  for (int32_t q = 0; q < n_res; ++q) {                 /* getPerGPUResourceCapacity */
+    capacity.has[q] = 1;
+    capacity.val[q] = cap_per_gpu[q];
+  }
+  /* readNodeResources deep copy (node_resource_cache.go:474-491) + addEmptyResourceMaps
+   * (:269-275): a fresh copy per (pod, node) */
+  for (int32_t k = 0; k < ncard; ++k) {
+    memset(&node_used[k], 0, sizeof(or_rm));
+    for (int32_t q = 0; q < n_res; ++q) {
+      node_used[k].has[q] = 1;
+      node_used[k].val[q] = used[(int64_t)k * n_res + q];
+    }
+  }
+  for (int32_t c = 0; c < n_containers; ++c) {         /* for i, containerRequest */
+    const uint32_t mask = req_mask[c];
+    if (mask == 0) continue;                            /* len(containerRequest) == 0 -> [] :206-208 */
+    or_rm per_gpu;                                      /* getPerGPUResourceRequest :180-190 */
+    memset(&per_gpu, 0, sizeof per_gpu);
+    for (int32_t q = 0; q < n_res; ++q)
+      if (mask & (1u << q)) { per_gpu.has[q] = 1; per_gpu.val[q] = req[(int64_t)c * n_res + q]; }
+    if (mask & OR_REQ_UNKNOWN_KIND) per_gpu.has[OR_UNKNOWN_KEY] = 1;  /* no capacity key */
+    int64_t num_i915 = 0;                               /* getNumI915 :192-198 */
+    if (i915_index >= 0 && per_gpu.has[i915_index] && per_gpu.val[i915_index] > 0)
+      num_i915 = per_gpu.val[i915_index];
+    if (num_i915 > 1) or_rm_divide(&per_gpu, num_i915);
+    for (int64_t g = 0; g < num_i915; ++g) {            /* for gpuNum := 0; gpuNum < numI915 */
+      int fitted = 0;
+      /* cards in sort.Strings order; stale cards are absent from the packed snapshot, which
+       * equals skipping them (!gpuMap[gpuName] -> continue, :230-234) */
+      for (int32_t k = 0; k < ncard; ++k) {
+        if (or_check_resource_capacity(&per_gpu, &capacity, &node_used[k])) {
+          if (or_rm_add_rm(&node_used[k], &per_gpu) == OR_RM_OK) {
+            fitted = 1;
+            if (list_push(sel, k)) return -1;           /* cards = append(cards, gpuName) */
+            if (cont_n) ++cont_n[c];
+          }
+          break;
+        }
+      }
+      if (!fitted) return 0;                            /* errWontFit :249-253 */
+    }
+  }
+  return 1;
+}
+
+/* The pas_gas_fit word of a fitting selection list. */
+static uint32_t fit_word(const card_list* sel) {
+  if (sel->n > OR_GAS_MAX_SEL) return 0x80000000u | ((uint32_t)OR_GAS_SEL_LIMIT << 24);
+  int packable = sel->n <= 8;
+  for (int64_t j = 0; j < sel->n; ++j) packable = packable && sel->v[j] < 8;
+  if (!packable) return 0x80000000u | ((uint32_t)OR_GAS_SEL_EXTENDED << 24);
+  uint32_t word = 0x80000000u | ((uint32_t)sel->n << 24);
+  for (int64_t j = 0; j < sel->n; ++j) word |= (uint32_t)sel->v[j] << (3 * j);
+  return word;
 }
 
 /* Builds the reference's maps from the packed layout: capacity has every resource kind
@@ -413,87 +492,27 @@ int or_gas_fit_ex(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32
                   const uint32_t* req_mask, const int32_t* n_containers, uint32_t* res_out,
                   uint8_t* sel_out, int32_t* nsel_out) {
   if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
-  or_rm node_used[OR_GAS_MAX_CARDS];
-  uint8_t sel[OR_GAS_MAX_SEL];
-  for (int32_t p = 0; p < n_pods; ++p) {
-    const int64_t total = pod_selections(n_res, i915_index, max_containers, req, req_mask,
-                                         n_containers[p], p);
+  card_list sel = {0};
+  int rc = 0;
+  for (int32_t p = 0; p < n_pods && !rc; ++p) {
     for (int32_t n = 0; n < n_nodes; ++n) {
       const int64_t pn = (int64_t)p * n_nodes + n;
-      if (nsel_out) nsel_out[pn] = 0;
-      if (total > OR_GAS_MAX_SEL) {                 /* beyond the build's documented limit */
-        res_out[pn] = (uint32_t)OR_GAS_SEL_LIMIT << 24;
-        continue;
+      const int f = fit_one(max_cards, n_res, n_cards[n], cap_per_gpu + (int64_t)n * n_res,
+                            used + (int64_t)n * max_cards * n_res, max_containers, i915_index,
+                            req + (int64_t)p * max_containers * n_res,
+                            req_mask + (int64_t)p * max_containers, n_containers[p], &sel, NULL);
+      if (f < 0) { rc = -3; break; }
+      res_out[pn] = f ? fit_word(&sel) : 0u;
+      if (nsel_out) nsel_out[pn] = !f ? 0 : sel.n > OR_GAS_MAX_SEL ? -1 : (int32_t)sel.n;
+      if (sel_out) {
+        memset(sel_out + pn * OR_GAS_MAX_SEL, 0, OR_GAS_MAX_SEL);
+        if (f && sel.n <= OR_GAS_MAX_SEL)
+          for (int64_t j = 0; j < sel.n; ++j) sel_out[pn * OR_GAS_MAX_SEL + j] = (uint8_t)sel.v[j];
       }
-      int fits = 1;
-      int32_t nsel = 0;
-      /* iCache.FetchNode error (:282-288) / no cards label -> errWontFit (:290-298) */
-      if (n_cards[n] <= 0) fits = 0;
-      const int32_t ncard = n_cards[n] < max_cards ? n_cards[n] : max_cards;
-      or_rm capacity;
-      memset(&capacity, 0, sizeof capacity);
-      if (fits) {
-        for (int32_t q = 0; q < n_res; ++q) {         /* getPerGPUResourceCapacity */
-          capacity.has[q] = 1;
-          capacity.val[q] = cap_per_gpu[(int64_t)n * n_res + q];
-        }
-        /* readNodeResources deep copy (node_resource_cache.go:474-491) +
-         * addEmptyResourceMaps (:269-275): a fresh copy per (pod, node) */
-        for (int32_t k = 0; k < ncard; ++k) {
-          memset(&node_used[k], 0, sizeof(or_rm));
-          for (int32_t q = 0; q < n_res; ++q) {
-            const int64_t u = used[((int64_t)n * max_cards + k) * n_res + q];
-            node_used[k].has[q] = 1;
-            node_used[k].val[q] = u;
-          }
-        }
-      }
-      for (int32_t c = 0; fits && c < n_containers[p]; ++c) {   /* for i, containerRequest */
-        const int64_t base = ((int64_t)p * max_containers + c);
-        const uint32_t mask = req_mask[base];
-        if (mask == 0) continue;                /* len(containerRequest) == 0 -> [] :206-208 */
-        or_rm per_gpu;                          /* getPerGPUResourceRequest :180-190 */
-        memset(&per_gpu, 0, sizeof per_gpu);
-        for (int32_t q = 0; q < n_res; ++q)
-          if (mask & (1u << q)) { per_gpu.has[q] = 1; per_gpu.val[q] = req[base * n_res + q]; }
-        if (mask & OR_REQ_UNKNOWN_KIND) per_gpu.has[OR_UNKNOWN_KEY] = 1;  /* no capacity key */
-        int64_t num_i915 = 0;                   /* getNumI915 :192-198 */
-        if (i915_index >= 0 && per_gpu.has[i915_index] && per_gpu.val[i915_index] > 0)
-          num_i915 = per_gpu.val[i915_index];
-        if (num_i915 > 1) or_rm_divide(&per_gpu, (int32_t)num_i915);
-        for (int64_t g = 0; g < num_i915; ++g) {  /* for gpuNum := 0; gpuNum < numI915 */
-          int fitted = 0;
-          /* cards in sort.Strings order; stale cards are absent from the packed snapshot,
-           * which equals skipping them (!gpuMap[gpuName] -> continue, :230-234) */
-          for (int32_t k = 0; k < ncard; ++k) {
-            if (or_check_resource_capacity(&per_gpu, &capacity, &node_used[k])) {
-              if (or_rm_add_rm(&node_used[k], &per_gpu) == OR_RM_OK) {
-                fitted = 1;
-                sel[nsel++] = (uint8_t)k;       /* cards = append(cards, gpuName) */
-              }
-              break;
-            }
-          }
-          if (!fitted) { fits = 0; break; }    /* errWontFit :249-253 */
-        }
-      }
-      uint32_t word = 0;
-      if (fits) {
-        int packable = nsel <= 8;
-        for (int32_t j = 0; j < nsel; ++j) packable = packable && sel[j] < 8;
-        if (packable) {
-          word = 0x80000000u | ((uint32_t)nsel << 24);
-          for (int32_t j = 0; j < nsel; ++j) word |= (uint32_t)sel[j] << (3 * j);
-        } else {
-          word = 0x80000000u | ((uint32_t)OR_GAS_SEL_EXTENDED << 24);
-        }
-        if (sel_out) memcpy(sel_out + pn * OR_GAS_MAX_SEL, sel, (size_t)nsel);
-        if (nsel_out) nsel_out[pn] = nsel;
-      }
-      res_out[pn] = word;
     }
   }
-  return 0;
+  free(sel.v);
+  return rc;
 }
 
 int or_gas_fit(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
@@ -532,41 +551,44 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
                 const int32_t* bind_pod, const int32_t* bind_node, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out, int32_t* status,
-                uint8_t* cards_out, int32_t* nsel_out) {
+                uint8_t* cards_out, int32_t* nsel_out, int64_t* counts_out) {
   if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
+  card_list sel = {0};
+  int64_t* cont_n = (int64_t*)calloc((size_t)(max_containers > 0 ? max_containers : 1),
+                                     sizeof(int64_t));
+  if (!cont_n) return -3;
+  int rc = 0;
+  const int64_t ck = (int64_t)max_containers * max_cards;
   for (int32_t b = 0; b < n_binds; ++b) {
     const int32_t p = bind_pod[b], n = bind_node[b];
-    if (n < 0 || n >= n_nodes) return -1;
+    if (n < 0 || n >= n_nodes) { rc = -1; break; }
     int64_t* u = used + (int64_t)n * max_cards * n_res;
-    uint32_t word = 0;
-    uint8_t sel[OR_GAS_MAX_SEL];
-    int32_t nsel = 0;
     if (cards_out) memset(cards_out + (int64_t)b * OR_GAS_MAX_SEL, 0, OR_GAS_MAX_SEL);
     if (nsel_out) nsel_out[b] = 0;
+    if (counts_out)
+      for (int64_t j = 0; j < ck; ++j) counts_out[b * ck + j] = 0;
     /* runSchedulingLogic(pod, node) on the current usage */
-    if (or_gas_fit_ex(1, max_cards, n_res, n_cards + n, cap_per_gpu + (int64_t)n * n_res, u, 1,
-                      max_containers, i915_index, req + (int64_t)p * max_containers * n_res,
-                      req_mask + (int64_t)p * max_containers, n_containers + p, &word, sel,
-                      &nsel) != 0)
-      return -2;
-    res_out[b] = word;
-    if (!(word >> 31)) { status[b] = OR_GAS_WONT_FIT; continue; }
+    const int f = fit_one(max_cards, n_res, n_cards[n], cap_per_gpu + (int64_t)n * n_res, u,
+                          max_containers, i915_index, req + (int64_t)p * max_containers * n_res,
+                          req_mask + (int64_t)p * max_containers, n_containers[p], &sel, cont_n);
+    if (f < 0) { rc = -3; break; }
+    res_out[b] = f ? fit_word(&sel) : 0u;
+    if (!f) { status[b] = OR_GAS_WONT_FIT; continue; }
     /* adjustPodResources(add): the annotation lists, per container, the cards of its
      * selections (numCards = numI915); checked on a copy, then applied */
     or_rm maps[OR_GAS_MAX_CARDS];
     node_maps(max_cards, n_res, n_cards[n], u, maps);
-    int32_t s_i = 0, err = OR_RM_OK;
+    int64_t s_i = 0;
+    int32_t err = OR_RM_OK;
     for (int32_t c = 0; c < n_containers[p] && !err; ++c) {
       const int64_t base = (int64_t)p * max_containers + c;
+      const int64_t k_c = cont_n[c];
+      if (k_c <= 0) continue;                       /* empty segment: skipped */
       or_rm r;
       container_map(n_res, req + base * n_res, req_mask[base], &r);
-      int64_t k_c = 0;
-      if (req_mask[base] && i915_index >= 0 && r.has[i915_index] && r.val[i915_index] > 0)
-        k_c = r.val[i915_index];
-      if (k_c <= 0) continue;                       /* empty segment: skipped */
-      or_rm_divide(&r, (int32_t)k_c);
+      or_rm_divide(&r, k_c);
       for (int64_t g = 0; g < k_c && !err; ++g, ++s_i)
-        err = or_rm_add_rm(&maps[sel[s_i]], &r);
+        err = or_rm_add_rm(&maps[sel.v[s_i]], &r);
     }
     if (err) {                                       /* nothing changes */
       status[b] = err == OR_RM_ERR_OVERFLOW ? OR_GAS_ERR_OVERFLOW : OR_GAS_ERR_INPUT;
@@ -574,11 +596,51 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
     }
     for (int32_t k = 0; k < n_cards[n]; ++k)
       for (int32_t q = 0; q < n_res; ++q) u[(int64_t)k * n_res + q] = maps[k].val[q];
-    if (cards_out) memcpy(cards_out + (int64_t)b * OR_GAS_MAX_SEL, sel, (size_t)nsel);
-    if (nsel_out) nsel_out[b] = nsel;
+    if (cards_out && sel.n <= OR_GAS_MAX_SEL)
+      for (int64_t j = 0; j < sel.n; ++j) cards_out[(int64_t)b * OR_GAS_MAX_SEL + j] = (uint8_t)sel.v[j];
+    if (nsel_out) nsel_out[b] = sel.n > OR_GAS_MAX_SEL ? -1 : (int32_t)sel.n;
+    if (counts_out) {
+      int64_t j = 0;
+      for (int32_t c = 0; c < n_containers[p]; ++c)
+        for (int64_t g = 0; g < cont_n[c]; ++g, ++j) ++counts_out[b * ck + (int64_t)c * max_cards + sel.v[j]];
+    }
     status[b] = OR_GAS_OK;
   }
-  return 0;
+  free(sel.v);
+  free(cont_n);
+  return rc;
+}
+
+/* One pod leaving node n: container c's annotation segment is cards[off .. off + cpc[c]). */
+static int32_t release_one(int32_t max_cards, int32_t n_res, int32_t nc_node, int64_t* u,
+                           int32_t n_containers, const int64_t* req, const uint32_t* req_mask,
+                           const int64_t* cpc, const int32_t* cards, int64_t n_cards_list) {
+  const int32_t ncard = nc_node > 0 ? nc_node : 0;
+  or_rm maps[OR_GAS_MAX_CARDS], stale;
+  node_maps(max_cards, n_res, ncard, u, maps);
+  int64_t off = 0;
+  int32_t err = OR_RM_OK;
+  for (int32_t c = 0; c < n_containers && !err; ++c) {
+    const int64_t k_c = cpc[c];
+    if (k_c <= 0) continue;                          /* empty segment */
+    or_rm q;
+    container_map(n_res, req + (int64_t)c * n_res, req_mask[c], &q);
+    or_rm_divide(&q, k_c);
+    for (int64_t j = 0; j < k_c && !err; ++j) {
+      const int32_t k = off + j < n_cards_list ? cards[off + j] : -1;
+      if (k >= 0 && k < ncard) {
+        err = or_rm_subtract_rm(&maps[k], &q);
+      } else {                                       /* new empty map for the card */
+        memset(&stale, 0, sizeof stale);
+        err = or_rm_subtract_rm(&stale, &q);
+      }
+    }
+    off += k_c;
+  }
+  if (err) return OR_GAS_ERR_INPUT;
+  for (int32_t k = 0; k < ncard; ++k)
+    for (int32_t q = 0; q < n_res; ++q) u[(int64_t)k * n_res + q] = maps[k].val[q];
+  return OR_GAS_OK;
 }
 
 int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
@@ -588,36 +650,55 @@ int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int3
                    const int32_t* cards_per_container, const int32_t* cards, int32_t cards_stride,
                    int32_t* status) {
   if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
+  int64_t* cpc = (int64_t*)calloc((size_t)(max_containers > 0 ? max_containers : 1),
+                                  sizeof(int64_t));
+  if (!cpc) return -3;
+  int rc = 0;
   for (int32_t r = 0; r < n_rel; ++r) {
     const int32_t p = rel_pod[r], n = rel_node[r];
-    if (n < 0 || n >= n_nodes) return -1;
-    int64_t* u = used + (int64_t)n * max_cards * n_res;
-    const int32_t ncard = n_cards[n] > 0 ? n_cards[n] : 0;
-    or_rm maps[OR_GAS_MAX_CARDS], stale;
-    node_maps(max_cards, n_res, ncard, u, maps);
-    int32_t off = 0, err = OR_RM_OK;
-    for (int32_t c = 0; c < n_containers[p] && !err; ++c) {
-      const int64_t base = (int64_t)p * max_containers + c;
-      const int32_t k_c = cards_per_container[(int64_t)r * max_containers + c];
-      if (k_c <= 0) continue;                        /* empty segment */
-      or_rm q;
-      container_map(n_res, req + base * n_res, req_mask[base], &q);
-      or_rm_divide(&q, k_c);
-      for (int32_t j = 0; j < k_c && !err; ++j) {
-        const int32_t k = off + j < cards_stride ? cards[(int64_t)r * cards_stride + off + j] : -1;
-        if (k >= 0 && k < ncard) {
-          err = or_rm_subtract_rm(&maps[k], &q);
-        } else {                                     /* new empty map for the card */
-          memset(&stale, 0, sizeof stale);
-          err = or_rm_subtract_rm(&stale, &q);
-        }
-      }
-      off += k_c;
-    }
-    if (err) { status[r] = OR_GAS_ERR_INPUT; continue; }
-    for (int32_t k = 0; k < ncard; ++k)
-      for (int32_t q = 0; q < n_res; ++q) u[(int64_t)k * n_res + q] = maps[k].val[q];
-    status[r] = OR_GAS_OK;
+    if (n < 0 || n >= n_nodes) { rc = -1; break; }
+    for (int32_t c = 0; c < max_containers; ++c)
+      cpc[c] = cards_per_container[(int64_t)r * max_containers + c];
+    status[r] = release_one(max_cards, n_res, n_cards[n], used + (int64_t)n * max_cards * n_res,
+                            n_containers[p], req + (int64_t)p * max_containers * n_res,
+                            req_mask + (int64_t)p * max_containers, cpc,
+                            cards + (int64_t)r * cards_stride, cards_stride);
   }
-  return 0;
+  free(cpc);
+  return rc;
+}
+
+int or_gas_release_counts(int32_t n_nodes, int32_t max_cards, int32_t n_res,
+                          const int32_t* n_cards, int64_t* used, int32_t n_rel,
+                          const int32_t* rel_pod, const int32_t* rel_node,
+                          int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
+                          const int32_t* n_containers, const int64_t* counts, int32_t* status) {
+  if (max_cards > OR_GAS_MAX_CARDS || n_res > OR_UNKNOWN_KEY) return -1;
+  int64_t* cpc = (int64_t*)calloc((size_t)(max_containers > 0 ? max_containers : 1),
+                                  sizeof(int64_t));
+  card_list list = {0};
+  int rc = cpc ? 0 : -3;
+  const int64_t ck = (int64_t)max_containers * max_cards;
+  for (int32_t r = 0; r < n_rel && !rc; ++r) {
+    const int32_t p = rel_pod[r], n = rel_node[r];
+    if (n < 0 || n >= n_nodes) { rc = -1; break; }
+    /* the annotation the counts stand for: per container, card k counts[r][c][k] times, in
+     * card order */
+    list.n = 0;
+    for (int32_t c = 0; c < max_containers && !rc; ++c) {
+      cpc[c] = 0;
+      for (int32_t k = 0; k < max_cards && !rc; ++k) {
+        const int64_t t = counts[r * ck + (int64_t)c * max_cards + k];
+        for (int64_t j = 0; j < t && !rc; ++j) rc = list_push(&list, k) ? -3 : 0;
+        cpc[c] += t > 0 ? t : 0;
+      }
+    }
+    if (rc) break;
+    status[r] = release_one(max_cards, n_res, n_cards[n], used + (int64_t)n * max_cards * n_res,
+                            n_containers[p], req + (int64_t)p * max_containers * n_res,
+                            req_mask + (int64_t)p * max_containers, cpc, list.v, list.n);
+  }
+  free(list.v);
+  free(cpc);
+  return rc;
 }

@@ -103,7 +103,7 @@ int or_rm_add(or_rm* rm, int32_t key, int64_t value);         /* resource_map.go
 int or_rm_subtract(or_rm* rm, int32_t key, int64_t value);    /* resource_map.go:103-127 */
 int or_rm_add_rm(or_rm* rm, const or_rm* src);                /* resource_map.go:38-53 */
 int or_rm_subtract_rm(or_rm* rm, const or_rm* src);           /* resource_map.go:58-73 */
-int or_rm_divide(or_rm* rm, int32_t divider);                 /* resource_map.go:129-145 */
+int or_rm_divide(or_rm* rm, int64_t divider);                 /* resource_map.go:129-145 */
 /* checkResourceCapacity (gpuscheduler/scheduler.go:341-383). */
 int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const or_rm* used);
 
@@ -120,9 +120,11 @@ int or_check_resource_capacity(const or_rm* need, const or_rm* capacity, const o
 
 /* GAS filter over every (pod, node) of a packed snapshot, one runSchedulingLogic
  * (scheduler.go:280-338) each; same layouts and result encoding as pas_gas_fit (words of
- * selections that do not pack: OR_GAS_SEL_EXTENDED; pods with more than 64 selections:
- * OR_GAS_SEL_LIMIT, not evaluated).  or_gas_fit_ex also returns every fitting pair's full
- * selection: sel_out[P][N][64] card ranks, nsel_out[P][N] counts (NULL: not wanted). */
+ * selections that do not pack: OR_GAS_SEL_EXTENDED; fitting pods with more than 64
+ * selections: bit 31 | OR_GAS_SEL_LIMIT << 24).  No bound on numI915 (the loop ends at the
+ * first selection no card fits).  or_gas_fit_ex also returns every fitting pair's full
+ * selection: sel_out[P][N][64] card ranks, nsel_out[P][N] counts (-1 past 64 selections,
+ * sel_out then zero; NULL: not wanted). */
 int or_gas_fit_ex(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t* n_cards,
                   const int64_t* cap_per_gpu, const int64_t* used, int32_t n_pods,
                   int32_t max_containers, int32_t i915_index, const int64_t* req,
@@ -146,7 +148,10 @@ int or_gas_bind(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int32_t
                 const int32_t* bind_pod, const int32_t* bind_node, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out, int32_t* status,
-                uint8_t* cards_out /*[n_binds][64] or NULL*/, int32_t* nsel_out);
+                uint8_t* cards_out /*[n_binds][64] or NULL*/, int32_t* nsel_out,
+                int64_t* counts_out /*[n_binds][max_containers][max_cards] or NULL*/);
+/* cards_out / nsel_out as or_gas_fit_ex's sel_out / nsel_out; counts_out[b][c][k] = the
+ * selections of container c on card k (any count). */
 /* Cache.adjustPodResources(remove) (node_resource_cache.go:240-287) for pods leaving nodes,
  * in order: container c's cards are cards[r][off .. off + n_cc[r][c]) (off = sum of the
  * earlier containers' counts; ranks into the node's cards); its request / n_cc is
@@ -159,6 +164,13 @@ int or_gas_release(int32_t n_nodes, int32_t max_cards, int32_t n_res, const int3
                    const uint32_t* req_mask, const int32_t* n_containers,
                    const int32_t* cards_per_container, const int32_t* cards,
                    int32_t cards_stride /*8 or 64*/, int32_t* status);
+/* or_gas_release with the annotation as counts[r][c][k] (container c lists card k that many
+ * times, in card order) — annotations of any length. */
+int or_gas_release_counts(int32_t n_nodes, int32_t max_cards, int32_t n_res,
+                          const int32_t* n_cards, int64_t* used, int32_t n_rel,
+                          const int32_t* rel_pod, const int32_t* rel_node,
+                          int32_t max_containers, const int64_t* req, const uint32_t* req_mask,
+                          const int32_t* n_containers, const int64_t* counts, int32_t* status);
 
 #ifdef __cplusplus
 }

@@ -15,6 +15,7 @@
 // This is latency work (a few thousand operations per call at most), not a hot kernel.
 #include <hip/hip_runtime.h>
 
+#include "gas_runs.h"
 #include "pas_internal.h"
 
 namespace pas {
@@ -49,6 +50,8 @@ struct BindArgs {
   int32_t* status;         // [n_ops]
   uint8_t* cards_out;      // bind_ex: [n_ops][PAS_GAS_MAX_SELECTIONS] or null
   int32_t* nsel_out;       // bind_ex: [n_ops] or null
+  int64_t* counts_out;     // bind_counts: [n_ops][C][K] or null
+  const int64_t* counts;   // release_counts: [n_ops][C][K] (else cpc / cards)
 };
 
 // KMAX: the snapshot's max_cards rounded up to 8 / 16 / 64 (the per-thread copies live in
@@ -75,11 +78,14 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
       for (int q = 0; q < Q; ++q) w[k][q] = u[k][q];
     bool fits = ncard > 0;  // FetchNode error / no cards label (:282-298)
     uint32_t word = 0;
-    int32_t nsel = 0;
+    int64_t nsel = 0;
     bool packable = true;
     uint8_t* sel_out = a.cards_out ? a.cards_out + (int64_t)op * PAS_GAS_MAX_SELECTIONS : nullptr;
     if (sel_out)
       for (int j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) sel_out[j] = 0;
+    int64_t* cnt = a.counts_out ? a.counts_out + (int64_t)op * C * K : nullptr;
+    if (cnt)
+      for (int64_t j = 0; j < (int64_t)C * K; ++j) cnt[j] = 0;
     for (int32_t c = 0; fits && c < a.ncont[p]; ++c) {
       const int64_t b = (int64_t)p * C + c;
       const uint32_t m = a.mask[b];
@@ -90,6 +96,14 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
       if (a.i915 >= 0 && ((m >> a.i915) & 1u) && r[a.i915] > 0) num = r[a.i915];
       if (num > 1)
         for (int q = 0; q < Q; ++q) r[q] /= num;  // getPerGPUResourceRequest (:180-190)
+      if (num > kRunsFrom) {  // more than PAS_GAS_MAX_SELECTIONS: card runs (gas_runs.h)
+        fits = container_runs<KMAX>(Q, m, r, num, cap, w, ncard, [&](int k, int64_t t) {
+          if (cnt) cnt[(int64_t)c * K + k] += t;
+        });
+        nsel += num;
+        packable = false;
+        continue;
+      }
       for (int64_t g = 0; g < num; ++g) {
         int chosen = -1;
         for (int k = 0; k < ncard && chosen < 0; ++k) {
@@ -107,6 +121,7 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
         if (nsel < PAS_GAS_PACKED) word |= (uint32_t)chosen << (3 * nsel);
         packable = packable && chosen < PAS_GAS_PACKED;
         if (sel_out && nsel < PAS_GAS_MAX_SELECTIONS) sel_out[nsel] = (uint8_t)chosen;
+        if (cnt) cnt[(int64_t)c * K + chosen] += 1;
         ++nsel;
       }
     }
@@ -116,13 +131,20 @@ __global__ __launch_bounds__(kTpb) void gas_bind_kernel(int32_t n_seg, BindArgs 
       if (a.nsel_out) a.nsel_out[op] = 0;
       if (sel_out)  // the selections of a bind that did not fit are not reported
         for (int j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) sel_out[j] = 0;
+      if (cnt)
+        for (int64_t j = 0; j < (int64_t)C * K; ++j) cnt[j] = 0;
       continue;
     }
-    // the pas_gas_fit word: selections that do not pack are PAS_GAS_SEL_EXTENDED
+    // the pas_gas_fit word: selections that do not pack are PAS_GAS_SEL_EXTENDED, more than
+    // PAS_GAS_MAX_SELECTIONS PAS_GAS_SEL_LIMIT (cards_out zero, n_sel -1: counts_out has them)
+    const bool wide = nsel > PAS_GAS_MAX_SELECTIONS;
     a.res_out[op] = nsel <= PAS_GAS_PACKED && packable
                         ? 0x80000000u | ((uint32_t)nsel << 24) | word
-                        : 0x80000000u | ((uint32_t)PAS_GAS_SEL_EXTENDED << 24);
-    if (a.nsel_out) a.nsel_out[op] = nsel;
+                        : 0x80000000u | ((uint32_t)(wide ? PAS_GAS_SEL_LIMIT
+                                                         : PAS_GAS_SEL_EXTENDED) << 24);
+    if (a.nsel_out) a.nsel_out[op] = wide ? -1 : (int32_t)nsel;
+    if (sel_out && wide)
+      for (int j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) sel_out[j] = 0;
     // adjustPodResources(add) with that annotation adds request / numCards (= numI915) to
     // each selected card: exactly the working copy's takes, which cannot overflow after the
     // capacity checks
@@ -153,7 +175,32 @@ __global__ __launch_bounds__(kTpb) void gas_release_kernel(int32_t n_seg, BindAr
       for (int q = 0; q < Q; ++q) w[k][q] = u[k][q];
     bool ok = true;
     int32_t off = 0;
-    for (int32_t c = 0; ok && c < a.ncont[p]; ++c) {
+    if (a.counts) {  // the annotation as counts per container and card (any length)
+      const int64_t* cnt = a.counts + (int64_t)op * C * K;
+      for (int32_t c = 0; ok && c < a.ncont[p]; ++c) {
+        int64_t kc = 0;  // numCards (the host checked that the sum does not overflow)
+        for (int k = 0; k < K; ++k) kc += cnt[(int64_t)c * K + k];
+        if (kc <= 0) continue;  // empty annotation segment
+        const int64_t b = (int64_t)p * C + c;
+        const uint32_t m = a.mask[b];
+        if (m & PAS_REQ_UNKNOWN_KIND) ok = false;
+        int64_t r[kMaxRes];
+        for (int q = 0; q < Q; ++q) r[q] = a.req[b * Q + q] / kc;  // divide(numCards)
+        for (int k = 0; ok && k < K; ++k) {
+          const int64_t t = cnt[(int64_t)c * K + k];
+          if (t <= 0) continue;
+          for (int q = 0; q < Q; ++q) {
+            if (!((m >> q) & 1u)) continue;
+            if (r[q] < 0 || k >= ncard) {  // negative amount / a card the label lacks
+              ok = false;
+              break;
+            }
+            w[k][q] = subtract_times(w[k][q], r[q], t);
+          }
+        }
+      }
+    }
+    for (int32_t c = 0; !a.counts && ok && c < a.ncont[p]; ++c) {
       const int32_t kc = a.cpc[(int64_t)op * C + c];
       if (kc <= 0) continue;  // empty annotation segment
       const int64_t b = (int64_t)p * C + c;
@@ -198,13 +245,13 @@ int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_con
                       const uint32_t* d_mask, const int32_t* d_ncont, const int32_t* d_cpc,
                       const int32_t* d_cards, int32_t cards_stride, uint32_t* d_res,
                       int32_t* d_status, uint8_t* d_cards_out, int32_t* d_nsel_out,
-                      hipStream_t s) {
+                      int64_t* d_counts_out, const int64_t* d_counts, hipStream_t s) {
   if (n_seg == 0) return PAS_OK;
   GasSnapshot& g = ctx->gas;
   BindArgs a{g.max_cards, g.n_res,  max_containers, i915_index, d_order, d_seg_off,
              d_pod,       d_node,   g.n_cards,      g.cap,      g.used,  d_req,
              d_mask,      d_ncont,  d_cpc,          d_cards,    cards_stride,
-             d_res,       d_status, d_cards_out,    d_nsel_out};
+             d_res,       d_status, d_cards_out,    d_nsel_out, d_counts_out, d_counts};
   const unsigned blocks = (unsigned)((n_seg + kTpb - 1) / kTpb);
 #define PAS_COMMIT(KM)                                       \
   if (release)                                               \

@@ -34,6 +34,7 @@
 // so that kernel keeps every kind: it is not bound by its compares.
 #include <hip/hip_runtime.h>
 
+#include "gas_runs.h"
 #include "pas_internal.h"
 
 namespace pas {
@@ -186,9 +187,8 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
 // list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
 // [n_res + 1][kClasses][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list
 // and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
-// go to the row sels[list][slot][8] of its list position.  More
-// than PAS_GAS_MAX_SELECTIONS selections are beyond the packed result and keep only the
-// count.  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
+// go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
+// PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
 __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
                                 int32_t i915, const int64_t* __restrict__ req,
                                 const uint32_t* __restrict__ mask,
@@ -1230,8 +1230,9 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
 // (every node) and nodes with more than 8 cards (every other pod).  One thread per pair runs
 // runSchedulingLogic (scheduler.go:280-338) as the reference writes it: per container
 // getPerGPUResourceRequest, then per gpuNum the first card in lexicographic order passing
-// checkResourceCapacity (:341-383) on the usage with the pod's earlier takes (addRM), no
-// limit but PAS_GAS_MAX_SELECTIONS / PAS_GAS_MAX_CARDS.  The state is private (KMAX cards;
+// checkResourceCapacity (:341-383) on the usage with the pod's earlier takes (addRM); a
+// container of more than PAS_GAS_MAX_SELECTIONS selections as card runs (gas_runs.h), its
+// pod's word then PAS_GAS_SEL_LIMIT.  The state is private (KMAX cards;
 // 64-card snapshots put it in scratch): this is the rare path, not a hot kernel.  Words
 // overwrite the fast kernels' zeros; bitmap bits are or-ed in; selections that do not pack
 // go to the side buffer.
@@ -1268,7 +1269,7 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
   const int32_t Q = a.Q;
   uint32_t word = 0u;
   uint8_t sel[PAS_GAS_MAX_SELECTIONS];
-  int32_t nsel = 0;
+  int64_t nsel = 0;  // the first PAS_GAS_MAX_SELECTIONS are recorded
   bool fits = false;
   const int32_t nc = a.n_cards[n];
   if (nc > 0) {  // FetchNode error / no cards label (:282-298)
@@ -1289,6 +1290,11 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
       if (a.i915 >= 0 && ((m >> a.i915) & 1u) && r[a.i915] > 0) num = r[a.i915];
       if (num > 1)
         for (int q = 0; q < Q; ++q) r[q] /= num;  // getPerGPUResourceRequest (:180-190)
+      if (num > kRunsFrom) {  // the pod has more than PAS_GAS_MAX_SELECTIONS: count only
+        fits = container_runs<KMAX>(Q, m, r, num, cap, w, ncard,
+                                    [&](int, int64_t t) { nsel += t; });
+        continue;
+      }
       for (int64_t g = 0; g < num; ++g) {
         int chosen = -1;
         for (int k = 0; k < ncard && chosen < 0; ++k) {
@@ -1303,11 +1309,14 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
         }
         for (int q = 0; q < Q; ++q)
           if ((m >> q) & 1u) w[chosen][q] += r[q];  // addRM after a passing check
-        sel[nsel++] = (uint8_t)chosen;
+        if (nsel < PAS_GAS_MAX_SELECTIONS) sel[nsel] = (uint8_t)chosen;
+        ++nsel;
       }
     }
   }
-  if (fits) {
+  if (fits && nsel > PAS_GAS_MAX_SELECTIONS) {
+    word = 0x80000000u | ((uint32_t)PAS_GAS_SEL_LIMIT << 24);  // selection reported at bind
+  } else if (fits) {
     bool packable = nsel <= kPacked;
     for (int32_t j = 0; j < nsel; ++j) packable = packable && sel[j] < kMaxCards;
     if (packable) {
@@ -1321,7 +1330,7 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
           pas_gas_selection& rec = a.side[slot];
           rec.pod = p;
           rec.node = n;
-          rec.n_sel = nsel;
+          rec.n_sel = (int32_t)nsel;
           rec.reserved = 0;
           for (int32_t j = 0; j < PAS_GAS_MAX_SELECTIONS; ++j) rec.card[j] = j < nsel ? sel[j] : 0;
         }
@@ -1348,11 +1357,8 @@ __global__ __launch_bounds__(64) void gas_fit_generic_kernel(GenericArgs a) {
     if (i < seg_a) {  // a pod with more than 8 selections, every node
       p = a.big_pods[i / a.N];
       n = (int32_t)(i % a.N);
-      if (a.pod_steps[p] > PAS_GAS_MAX_SELECTIONS) {  // beyond the documented limit
-        if (!a.fit) a.res[(int64_t)p * a.N + n] = (uint32_t)PAS_GAS_SEL_LIMIT << 24;
-        if (n == 0) atomicAdd(a.limit_count, 1ull);
-        continue;
-      }
+      // more than PAS_GAS_MAX_SELECTIONS: evaluated, counted (pas_gas_limit_count)
+      if (n == 0 && a.pod_steps[p] > PAS_GAS_MAX_SELECTIONS) atomicAdd(a.limit_count, 1ull);
     } else {  // a node with more than 8 cards, every pod the fast kernels evaluated
       const int64_t j = i - seg_a;
       p = (int32_t)(j / nbn);

@@ -645,7 +645,8 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
                       const int64_t* req, const uint32_t* req_mask, const int32_t* n_containers,
                       const int32_t* cpc, const int32_t* cards, int32_t cards_stride,
                       uint32_t* res_out, int32_t* status_out, uint8_t* cards_out,
-                      int32_t* nsel_out, const char* fn) {
+                      int32_t* nsel_out, int64_t* counts_out, const int64_t* counts,
+                      const char* fn) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_gas_gen(ctx, gen_from);
   if (rc) return rc;
@@ -655,8 +656,9 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
     return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad shape");
   if (n_ops > 0 && (!op_pod || !op_node || !status_out || !n_containers ||
                     (max_containers > 0 && (!req || !req_mask)) ||
-                    (release ? (!cpc || !cards) : !res_out)))
+                    (release ? (!counts && (!cpc || !cards)) : !res_out)))
     return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
+  const int32_t K = g.max_cards;
   std::vector<int32_t> order((size_t)n_ops);
   for (int32_t i = 0; i < n_ops; ++i) {
     order[(size_t)i] = i;
@@ -665,25 +667,32 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
     const int32_t p = op_pod[i];
     if (n_containers[p] < 0 || n_containers[p] > max_containers)
       return set_error(ctx, PAS_EINVAL, std::string(fn) + ": n_containers out of range");
-    // selections (bind) / annotation cards (release), saturating past the limit
-    const int64_t limit = release ? cards_stride : PAS_GAS_MAX_SELECTIONS;
+    // annotation cards of a release: within the card list (cards[i][cards_stride]), or per
+    // container a count sum that fits int64 (counts form).  Binds have no selection limit.
+    const int64_t limit = cards_stride;
     int64_t sel = 0;
     for (int32_t c = 0; c < n_containers[p]; ++c) {
       const int64_t b = (int64_t)p * max_containers + c;
       if ((req_mask[b] & ~PAS_REQ_UNKNOWN_KIND) >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
-      int64_t v = 0;
-      if (release) {
-        v = cpc[(int64_t)i * max_containers + c];
-        if (v < 0) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": negative card count");
-      } else if (i915_index >= 0 && req_mask[b] && (req_mask[b] >> i915_index & 1u)) {
-        v = std::max<int64_t>(req[b * Q + i915_index], 0);
+      if (!release) continue;
+      if (counts) {
+        int64_t kc = 0;
+        for (int32_t k = 0; k < K; ++k) {
+          const int64_t t = counts[((int64_t)i * max_containers + c) * K + k];
+          if (t < 0 || kc > INT64_MAX - t)
+            return set_error(ctx, PAS_EINVAL, std::string(fn) + ": card counts negative or "
+                                                               "past int64");
+          kc += t;
+        }
+        continue;
       }
+      const int64_t v = cpc[(int64_t)i * max_containers + c];
+      if (v < 0) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": negative card count");
       sel = std::min(sel + std::min(v, limit + 1), limit + 1);
     }
-    if (sel > limit)
-      return set_error(ctx, release ? PAS_EINVAL : PAS_ECAPACITY,
-                       std::string(fn) + ": more than " + std::to_string(limit) +
-                           " cards for one pod");
+    if (release && !counts && sel > limit)
+      return set_error(ctx, PAS_EINVAL, std::string(fn) + ": more than " +
+                                            std::to_string(limit) + " cards for one pod");
   }
   std::stable_sort(order.begin(), order.end(),
                    [&](int32_t a, int32_t b) { return op_node[a] < op_node[b]; });
@@ -703,8 +712,9 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
   const size_t b_cpc = sizeof(int32_t) * ops * C;
   const size_t b_cards = sizeof(int32_t) * ops * (size_t)cards_stride;
   const size_t b_sel = cards_out ? ops * PAS_GAS_MAX_SELECTIONS : 1;
+  const size_t b_cnt = (counts || counts_out) ? sizeof(int64_t) * ops * C * (size_t)K : 8;
   if ((rc = ensure_scratch(ctx, carve_size({b_req, b_mask, b_nc, b_op, b_op, b_op, b_seg, b_cpc,
-                                            b_cards, b_op, b_op, b_sel, b_op}))))
+                                            b_cards, b_op, b_op, b_sel, b_op, b_cnt}))))
     return rc;
   Carve cv{static_cast<char*>(ctx->scratch)};
   int64_t* d_req = cv.take<int64_t>(pods * C * Q);
@@ -720,6 +730,7 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
   int32_t* d_status = cv.take<int32_t>(ops);
   uint8_t* d_sel = cv.take<uint8_t>(b_sel);
   int32_t* d_nsel = cv.take<int32_t>(ops);
+  int64_t* d_cnt = cv.take<int64_t>(b_cnt / sizeof(int64_t));
   hipStream_t s = ctx->stream;
   if (n_ops > 0) {
     if (max_containers > 0 && n_pods > 0) {
@@ -734,7 +745,10 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
     PAS_HIP(ctx, hipMemcpyAsync(d_node, op_node, b_op, hipMemcpyHostToDevice, s));
     PAS_HIP(ctx, hipMemcpyAsync(d_order, order.data(), b_op, hipMemcpyHostToDevice, s));
     PAS_HIP(ctx, hipMemcpyAsync(d_seg, seg_off.data(), b_seg, hipMemcpyHostToDevice, s));
-    if (release) {
+    if (release && counts) {
+      if (max_containers > 0 && K > 0)
+        PAS_HIP(ctx, hipMemcpyAsync(d_cnt, counts, b_cnt, hipMemcpyHostToDevice, s));
+    } else if (release) {
       if (max_containers > 0)
         PAS_HIP(ctx, hipMemcpyAsync(d_cpc, cpc, sizeof(int32_t) * n_ops * max_containers,
                                     hipMemcpyHostToDevice, s));
@@ -743,10 +757,13 @@ static int gas_commit(pas_ctx* ctx, bool release, uint64_t gen_from, uint64_t ge
     if ((rc = gas_commit_launch(ctx, release, n_seg, max_containers, i915_index, d_order, d_seg,
                                 d_pod, d_node, d_req, d_mask, d_nc, d_cpc, d_cards,
                                 cards_stride, d_res, d_status, cards_out ? d_sel : nullptr,
-                                cards_out ? d_nsel : nullptr, s)))
+                                cards_out ? d_nsel : nullptr, counts_out ? d_cnt : nullptr,
+                                counts ? d_cnt : nullptr, s)))
       return rc;
     if (!release)
       PAS_HIP(ctx, hipMemcpyAsync(res_out, d_res, b_op, hipMemcpyDeviceToHost, s));
+    if (counts_out && max_containers > 0 && K > 0)
+      PAS_HIP(ctx, hipMemcpyAsync(counts_out, d_cnt, b_cnt, hipMemcpyDeviceToHost, s));
     if (cards_out) {
       PAS_HIP(ctx, hipMemcpyAsync(cards_out, d_sel, b_sel, hipMemcpyDeviceToHost, s));
       PAS_HIP(ctx, hipMemcpyAsync(nsel_out, d_nsel, b_op, hipMemcpyDeviceToHost, s));
@@ -766,7 +783,8 @@ int pas_gas_bind(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_bin
                  int32_t* status_out) {
   return gas_commit(ctx, false, gen_from, gen_to, n_binds, bind_pod, bind_node, n_pods,
                     max_containers, i915_index, req, req_mask, n_containers, nullptr, nullptr,
-                    PAS_GAS_PACKED, res_out, status_out, nullptr, nullptr, "pas_gas_bind");
+                    PAS_GAS_PACKED, res_out, status_out, nullptr, nullptr, nullptr, nullptr,
+                    "pas_gas_bind");
 }
 
 int pas_gas_bind_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
@@ -780,7 +798,22 @@ int pas_gas_bind_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_
   return gas_commit(ctx, false, gen_from, gen_to, n_binds, bind_pod, bind_node, n_pods,
                     max_containers, i915_index, req, req_mask, n_containers, nullptr, nullptr,
                     PAS_GAS_PACKED, res_out, status_out, n_binds > 0 ? cards_out : nullptr,
-                    n_sel_out, "pas_gas_bind_ex");
+                    n_sel_out, nullptr, nullptr, "pas_gas_bind_ex");
+}
+
+int pas_gas_bind_counts(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_binds,
+                        const int32_t* bind_pod, const int32_t* bind_node, int32_t n_pods,
+                        int32_t max_containers, int32_t i915_index, const int64_t* req,
+                        const uint32_t* req_mask, const int32_t* n_containers,
+                        uint32_t* res_out, int32_t* status_out, int64_t* counts_out) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_binds > 0 && max_containers > 0 && !counts_out)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_bind_counts: null input");
+  return gas_commit(ctx, false, gen_from, gen_to, n_binds, bind_pod, bind_node, n_pods,
+                    max_containers, i915_index, req, req_mask, n_containers, nullptr, nullptr,
+                    PAS_GAS_PACKED, res_out, status_out, nullptr, nullptr,
+                    n_binds > 0 && max_containers > 0 ? counts_out : nullptr, nullptr,
+                    "pas_gas_bind_counts");
 }
 
 int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
@@ -790,7 +823,8 @@ int pas_gas_release(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_
                     const int32_t* cards, int32_t* status_out) {
   return gas_commit(ctx, true, gen_from, gen_to, n_releases, rel_pod, rel_node, n_pods,
                     max_containers, -1, req, req_mask, n_containers, cards_per_container, cards,
-                    PAS_GAS_PACKED, nullptr, status_out, nullptr, nullptr, "pas_gas_release");
+                    PAS_GAS_PACKED, nullptr, status_out, nullptr, nullptr, nullptr, nullptr,
+                    "pas_gas_release");
 }
 
 int pas_gas_release_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t n_releases,
@@ -800,8 +834,23 @@ int pas_gas_release_ex(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to, int32_t
                        const int32_t* cards, int32_t* status_out) {
   return gas_commit(ctx, true, gen_from, gen_to, n_releases, rel_pod, rel_node, n_pods,
                     max_containers, -1, req, req_mask, n_containers, cards_per_container, cards,
-                    PAS_GAS_MAX_SELECTIONS, nullptr, status_out, nullptr, nullptr,
-                    "pas_gas_release_ex");
+                    PAS_GAS_MAX_SELECTIONS, nullptr, status_out, nullptr, nullptr, nullptr,
+                    nullptr, "pas_gas_release_ex");
+}
+
+int pas_gas_release_counts(pas_ctx* ctx, uint64_t gen_from, uint64_t gen_to,
+                           int32_t n_releases, const int32_t* rel_pod, const int32_t* rel_node,
+                           int32_t n_pods, int32_t max_containers, const int64_t* req,
+                           const uint32_t* req_mask, const int32_t* n_containers,
+                           const int64_t* counts, int32_t* status_out) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_releases > 0 && max_containers > 0 && !counts)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_release_counts: null input");
+  static const int64_t kNone = 0;  // no containers: nothing to read
+  return gas_commit(ctx, true, gen_from, gen_to, n_releases, rel_pod, rel_node, n_pods,
+                    max_containers, -1, req, req_mask, n_containers, nullptr, nullptr, 1,
+                    nullptr, status_out, nullptr, nullptr, nullptr, counts ? counts : &kNone,
+                    "pas_gas_release_counts");
 }
 
 int pas_gas_snapshot_get(pas_ctx* ctx, uint64_t* gen, int64_t* used_out) {
@@ -836,25 +885,14 @@ static int gas_fit_host(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_
   if (!n_containers || !res_out || (max_containers > 0 && (!req || !req_mask)) ||
       (side_cap > 0 && !side))
     return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
-  // Validate the batch; the selections (sum of i915 counts, saturating) bound the
-  // documented limit.
+  // Validate the batch (no limit on card selections: see PAS_GAS_SEL_LIMIT)
   for (int32_t p = 0; p < n_pods; ++p) {
     if (n_containers[p] < 0 || n_containers[p] > max_containers)
       return set_error(ctx, PAS_EINVAL, std::string(fn) + ": n_containers out of range");
-    int64_t sel = 0;
     for (int32_t c = 0; c < n_containers[p]; ++c) {
       const int64_t b = (int64_t)p * max_containers + c;
       if ((req_mask[b] & ~PAS_REQ_UNKNOWN_KIND) >> Q) return set_error(ctx, PAS_EINVAL, std::string(fn) + ": mask bit >= n_res");
-      if (i915_index >= 0 && (req_mask[b] >> i915_index & 1u)) {
-        const int64_t v = std::max<int64_t>(req[b * Q + i915_index], 0);
-        sel = std::min<int64_t>(sel + std::min<int64_t>(v, PAS_GAS_MAX_SELECTIONS + 1),
-                                PAS_GAS_MAX_SELECTIONS + 1);
-      }
     }
-    if (sel > PAS_GAS_MAX_SELECTIONS)
-      return set_error(ctx, PAS_ECAPACITY,
-                       "pod " + std::to_string(p) + " needs more than " +
-                           std::to_string(PAS_GAS_MAX_SELECTIONS) + " card selections");
   }
   if ((rc = activate(ctx))) return rc;
   const int64_t N = ctx->gas.n_nodes;

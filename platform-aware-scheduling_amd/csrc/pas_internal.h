@@ -197,7 +197,7 @@ int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_con
                       const uint32_t* d_mask, const int32_t* d_ncont, const int32_t* d_cpc,
                       const int32_t* d_cards, int32_t cards_stride, uint32_t* d_res,
                       int32_t* d_status, uint8_t* d_cards_out, int32_t* d_nsel_out,
-                      hipStream_t s);
+                      int64_t* d_counts_out, const int64_t* d_counts, hipStream_t s);
 int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
                       const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                       int64_t* d_total, hipStream_t s);

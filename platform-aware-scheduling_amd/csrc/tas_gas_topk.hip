@@ -31,6 +31,7 @@
 
 #include <cstdint>
 
+#include "gas_runs.h"
 #include "pas_internal.h"
 
 namespace pas {
@@ -130,6 +131,10 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
     if (num > 1)
 #pragma unroll
       for (int q = 0; q < kMaxRes; ++q) r[q] /= num;
+    if (num > kRunsFrom) {  // card runs (gas_runs.h)
+      if (!container_runs<KMAX>(Q, m, r, num, cap, w, ncard, [](int, int64_t) {})) return false;
+      continue;
+    }
     for (int64_t g = 0; g < num; ++g) {
       int chosen = -1;
 #pragma unroll kUnroll
@@ -232,19 +237,7 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
   const pas_rule pr = a.prio[p];
   // bucket -1: no scheduling rule / metric not cached / no node has it: empty list
   // (telemetryscheduler.go:92-96); d0.z = the metric's present count
-  int32_t c0 = (have && d0.y >= 0) ? d0.z : 0;
-  if (c0 > 0) {  // a pod past PAS_GAS_MAX_SELECTIONS is not evaluated (fit bits 0)
-    int64_t steps = 0;
-    for (int32_t c = 0; c < a.ncont[p]; ++c) {
-      const int64_t bb = (int64_t)p * a.C + c;
-      const uint32_t m = a.mask[bb];
-      if (a.i915 >= 0 && m != 0u && ((m >> a.i915) & 1u)) {
-        const int64_t v = a.req[bb * a.Q + a.i915];
-        if (v > 0) steps += min(v, (int64_t)PAS_GAS_MAX_SELECTIONS + 1);
-      }
-    }
-    if (steps > PAS_GAS_MAX_SELECTIONS) c0 = 0;
-  }
+  const int32_t c0 = (have && d0.y >= 0) ? d0.z : 0;
   const int32_t r0 = d1.x, r1 = d1.y;
   // Rules on the prioritize metric itself select one contiguous range of a sorted order row
   // (EvaluateRule over the ascending column, a3): a pod whose rule excludes the top of its

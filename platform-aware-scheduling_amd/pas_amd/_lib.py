@@ -170,9 +170,18 @@ SIGNATURES = {
         [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P,
          _P, _P],
     ),
+    "pas_gas_bind_counts": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P,
+         _P],
+    ),
     "pas_gas_release": (
         c_int,
         [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, _P, _P, _P, _P, _P, _P],
+    ),
+    "pas_gas_release_counts": (
+        c_int,
+        [_P, c_uint64, c_uint64, c_int32, _P, _P, c_int32, c_int32, _P, _P, _P, _P, _P],
     ),
     "pas_gas_release_ex": (
         c_int,

@@ -369,10 +369,11 @@ class Context:
 
     def gas_bind(self, gen_from: int, gen_to: int, pods, nodes, req: np.ndarray,
                  req_mask: np.ndarray, n_containers: np.ndarray, i915_index: int,
-                 selections: bool = False):
+                 selections: bool = False, counts: bool = False):
         """GASExtender.bindNode for binds (pods[b] -> nodes[b]) in order, committed into the
         resident usage.  Returns (result words, statuses), plus (cards [B][64], n_sel [B]) with
-        selections=True (pas_gas_bind_ex)."""
+        selections=True (pas_gas_bind_ex), or plus counts [B][C][K] (selections per container
+        and card, any number) with counts=True (pas_gas_bind_counts)."""
         req = np.ascontiguousarray(req, dtype=np.int64)
         p, c, q = req.shape
         req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
@@ -381,6 +382,14 @@ class Context:
         nodes = np.ascontiguousarray(nodes, dtype=np.int32)
         res = np.zeros(len(pods), np.uint32)
         st = np.zeros(len(pods), np.int32)
+        if counts:
+            cnt = np.zeros((len(pods), c, self.gas_shape[1]), np.int64)
+            rc = self._l.pas_gas_bind_counts(self._h, gen_from, gen_to, len(pods), _ptr(pods),
+                                             _ptr(nodes), p, c, i915_index, _ptr(req),
+                                             _ptr(req_mask), _ptr(n_containers), _ptr(res),
+                                             _ptr(st), _ptr(cnt))
+            self._check(rc, "pas_gas_bind_counts")
+            return res, st, cnt
         if not selections:
             rc = self._l.pas_gas_bind(self._h, gen_from, gen_to, len(pods), _ptr(pods),
                                       _ptr(nodes), p, c, i915_index, _ptr(req), _ptr(req_mask),
@@ -416,6 +425,26 @@ class Context:
         rc = fn(self._h, gen_from, gen_to, len(pods), _ptr(pods), _ptr(nodes), p, c, _ptr(req),
                 _ptr(req_mask), _ptr(n_containers), _ptr(cpc), _ptr(cards), _ptr(st))
         self._check(rc, "pas_gas_release_ex" if ex else "pas_gas_release")
+        return st
+
+    def gas_release_counts(self, gen_from: int, gen_to: int, pods, nodes, req: np.ndarray,
+                           req_mask: np.ndarray, n_containers: np.ndarray,
+                           counts) -> np.ndarray:
+        """adjustPodResources(remove) with each annotation as counts [R][C][K] (container c
+        lists card k that many times; pas_gas_release_counts); returns statuses."""
+        req = np.ascontiguousarray(req, dtype=np.int64)
+        p, c, q = req.shape
+        req_mask = np.ascontiguousarray(req_mask, dtype=np.uint32)
+        n_containers = np.ascontiguousarray(n_containers, dtype=np.int32)
+        pods = np.ascontiguousarray(pods, dtype=np.int32)
+        nodes = np.ascontiguousarray(nodes, dtype=np.int32)
+        counts = np.ascontiguousarray(counts, dtype=np.int64).reshape(
+            len(pods), c, self.gas_shape[1])
+        st = np.zeros(len(pods), np.int32)
+        rc = self._l.pas_gas_release_counts(self._h, gen_from, gen_to, len(pods), _ptr(pods),
+                                            _ptr(nodes), p, c, _ptr(req), _ptr(req_mask),
+                                            _ptr(n_containers), _ptr(counts), _ptr(st))
+        self._check(rc, "pas_gas_release_counts")
         return st
 
     def gas_snapshot_get(self):

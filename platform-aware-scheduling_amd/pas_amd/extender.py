@@ -249,15 +249,17 @@ class GASExtender:
         req, mask, ncont, per_container = self._requests(json.dumps(pod).encode())
         if node is None:  # runSchedulingLogic -> FetchNode error (:282-288)
             return 404, self._error(f'node "{node_name}" not found')
-        res, st, cards, nsel = self.ctx.gas_bind(self.gen, self.gen + 1, [0], [node], req, mask,
-                                                 ncont, self.i915, selections=True)
+        # the selection as counts per container and card: any number of selections
+        res, st, cnt = self.ctx.gas_bind(self.gen, self.gen + 1, [0], [node], req, mask, ncont,
+                                         self.i915, counts=True)
         self.gen += 1
         if st[0] != _lib.PAS_GAS_OK:
             return 404, self._error("will not fit")  # errWontFit (:49)
-        from .snapshot import annotation
+        from .snapshot import annotation_counts
+        names = self.card_names[node]
         pod.setdefault("metadata", {}).setdefault("annotations", {})[
-            "gas-container-cards"] = annotation(int(res[0]), per_container, self.card_names[node],
-                                                cards[0, : nsel[0]])
+            "gas-container-cards"] = annotation_counts(cnt[0, :, : len(names)], int(ncont[0]),
+                                                       names)
         return 200, wire.binding_result("")
 
     def prioritize(self, body: bytes) -> Tuple[int, bytes]:

@@ -126,3 +126,14 @@ def annotation(word: int, container_i915: Sequence[int], card_names: Sequence[st
         out.append(",".join(card_names[r] for r in ranks[pos:pos + n]))
         pos += n
     return "|".join(out)
+
+
+def annotation_counts(counts, n_containers: int, card_names: Sequence[str]) -> str:
+    """The "gas-container-cards" annotation from pas_gas_bind_counts' counts [C][K]: container
+    c lists card k counts[c][k] times, in card order (its selections' order: first fit with
+    one per-GPU request never returns to a card it has passed, scheduler.go:200-257)."""
+    out = []
+    for c in range(int(n_containers)):
+        out.append(",".join(card_names[k] for k in range(len(card_names))
+                            for _ in range(int(counts[c][k]))))
+    return "|".join(out)

@@ -195,11 +195,10 @@ def test_bind_errors(ctx):
         with pytest.raises(pas_amd.PasError) as e:
             ctx.gas_bind(kw["gen_from"], gen + 1, [0], kw["nodes"], req, mask, one, 0)
         assert e.value.code == code
-    # more than 64 selections -> capacity
-    with pytest.raises(pas_amd.PasError) as e:
-        ctx.gas_bind(gen, gen + 1, [0], [0], np.array([[[65]]], np.int64), mask, one, 0)
-    assert e.value.code == pas_amd._lib.PAS_ECAPACITY
-    assert ctx.gas_snapshot_get()[0] == gen
+    # more than 64 selections are evaluated: 65 do not fit 2 cards of capacity 10
+    res, st = ctx.gas_bind(gen, gen + 1, [0], [0], np.array([[[65]]], np.int64), mask, one, 0)
+    assert st[0] == pas_amd._lib.PAS_GAS_WONT_FIT and res[0] == 0
+    assert ctx.gas_snapshot_get()[0] == gen + 1
 
 
 @pytest.mark.gpu
