@@ -448,6 +448,18 @@ int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_ru
                         int32_t node_base, int64_t* d_top_key, int32_t* d_top_node,
                         int32_t* d_top_len, void* hip_stream);
 
+/* Full-list prioritize over node shards: the cluster's whole
+ * HostPriorityList per pod from every shard's whole list.  keys / nodes [n_shards][n_pods]
+ * [width] are the shards' records as pas_tas_topk_device writes them with k = width (>= the
+ * widest shard; INT64_MAX / INT32_MAX past each list).  out_node[p][0 .. out_len[p]) = the
+ * merged list (ascending (key, node): the order prioritizeNodesForRule lists,
+ * telemetryscheduler.go:128-149), global node ids, -1 in positions
+ * [out_len[p], n_shards * width); row pitch out_ld >= n_shards * width.  Exact: no
+ * (key, node) pair repeats across shards. */
+int pas_list_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t width,
+                          const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
+                          int64_t out_ld, int32_t* d_out_len, void* hip_stream);
+
 /* The same records for the combined TAS + GAS filter (BASELINE configs[4]): the first k
  * entries of the shard's HostPriorityList over the nodes that pass the pod's dontschedule
  * filter (and d_cand when given) AND fit its GPU request (runSchedulingLogic on the

@@ -193,6 +193,7 @@ void pas_destroy(pas_ctx* ctx) {
   free_gas(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->aux) (void)hipFree(ctx->aux);
+  if (ctx->merge_buf) (void)hipFree(ctx->merge_buf);
   if (ctx->label_part) (void)hipFree(ctx->label_part);
   if (ctx->gas_limit) (void)hipFree(ctx->gas_limit);
   if (ctx->tas_gpass) (void)hipFree(ctx->tas_gpass);
@@ -1150,6 +1151,22 @@ int pas_topk_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_sha
   if (rc) return rc;
   return topk_merge_launch(ctx, n_pods, k, n_shards, d_keys, d_nodes, d_out_node, d_out_len,
                            pick_stream(ctx, hip_stream));
+}
+
+int pas_list_merge_device(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t width,
+                          const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
+                          int64_t out_ld, int32_t* d_out_len, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  if (n_pods < 0 || n_shards < 1 || n_shards > 4096 || width < 1 ||
+      out_ld < (int64_t)n_shards * width || (int64_t)n_shards * width > INT32_MAX)
+    return set_error(ctx, PAS_EINVAL, "pas_list_merge_device: bad shape");
+  if (n_pods == 0) return PAS_OK;
+  if (!d_keys || !d_nodes || !d_out_node || !d_out_len)
+    return set_error(ctx, PAS_EINVAL, "pas_list_merge_device: null argument");
+  int rc = activate(ctx);
+  if (rc) return rc;
+  return list_merge_launch(ctx, n_pods, n_shards, width, d_keys, d_nodes, d_out_node, out_ld,
+                           d_out_len, pick_stream(ctx, hip_stream));
 }
 
 // --------------------------------------------------------------------------- timing

@@ -113,6 +113,8 @@ struct pas_ctx {
   int64_t* label_part = nullptr;  // per-workgroup partial counts of the label plan
   void* tas_gpass = nullptr;  // pass bitmaps of clusters past the LDS bitmap (tas_eval)
   size_t tas_gpass_bytes = 0;
+  void* merge_buf = nullptr;  // ping-pong rows of the full-list merge (tas_list_merge.hip)
+  size_t merge_bytes = 0;
   int64_t* gas_limit = nullptr;     // pods of the last GAS fit past PAS_GAS_MAX_SELECTIONS
   hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
   // timing
@@ -186,6 +188,9 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
                         const int64_t* d_req, const uint32_t* d_req_mask,
                         const int32_t* d_n_containers, int32_t k, int32_t node_base,
                         int64_t* d_key, int32_t* d_node, int32_t* d_len, hipStream_t s);
+int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t width,
+                      const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
+                      int64_t out_ld, int32_t* d_out_len, hipStream_t s);
 int topk_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t k, int32_t n_shards,
                       const int64_t* d_keys, const int32_t* d_nodes, int32_t* d_out_node,
                       int32_t* d_out_len, hipStream_t s);

@@ -198,6 +198,8 @@ SIGNATURES = {
          c_int32, c_int32, _P, _P, _P, _P],
     ),
     "pas_topk_merge_device": (c_int, [_P, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P]),
+    "pas_list_merge_device": (c_int, [_P, c_int32, c_int32, c_int32, _P, _P, _P, c_int64, _P,
+                                      _P]),
     "pas_encode_host_priority_list": (
         c_int, [c_int32, _P, POINTER(c_char_p), c_char_p, c_int64, POINTER(c_int64)]),
     "pas_encode_tas_filter_result": (

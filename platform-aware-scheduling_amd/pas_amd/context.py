@@ -502,3 +502,13 @@ class Context:
                                            _dptr(nodes_t), _dptr(out_node_t), _dptr(out_len_t),
                                            _stream(stream))
         self._check(rc, "pas_topk_merge_device")
+
+    def list_merge_device(self, n_pods: int, n_shards: int, width: int, keys_t, nodes_t,
+                          out_node_t, out_len_t, out_ld: int = 0, stream=None):
+        """Merge of [n_shards][P][width] whole-shard records (pas_tas_topk_device with
+        k = width) into the cluster's full lists out_node [P][>= n_shards * width]."""
+        out_ld = out_ld or n_shards * width
+        rc = self._l.pas_list_merge_device(self._h, n_pods, n_shards, width, _dptr(keys_t),
+                                           _dptr(nodes_t), _dptr(out_node_t), out_ld,
+                                           _dptr(out_len_t), _stream(stream))
+        self._check(rc, "pas_list_merge_device")

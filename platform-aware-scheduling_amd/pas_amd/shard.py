@@ -14,9 +14,16 @@ contiguous node range of the cluster as its resident snapshot and:
     (S x W64 words per shard; shard ranges are multiples of 64 nodes so the words of all
     ranks concatenate into the cluster bitmap).
 
-Collectives are torch.distributed all-gathers: RCCL ("nccl") over xGMI between GPUs; with
-the gloo backend (CPU tests, or several ranks sharing one GPU) the device buffers are staged
-through host memory.
+  * full-list prioritize (C2 semantics over node shards): every rank lists each pod's whole
+    shard HostPriorityList as records (pas_tas_topk_device with k = the widest shard), an
+    all-to-all sends each pod's records to the rank that owns the pod (pods in contiguous
+    slices), and the owner merges the shards' runs into the cluster list
+    (pas_list_merge_device).  The lists stay pod-sharded: [P][N] int32 over the whole batch
+    need not fit one GPU.
+
+Collectives are torch.distributed all-gathers / all-to-alls: RCCL ("nccl") over xGMI between
+GPUs; with the gloo backend (CPU tests, or several ranks sharing one GPU) the device buffers
+are staged through host memory.
 """
 from typing import Tuple
 
@@ -49,6 +56,91 @@ def _all_gather(t: torch.Tensor, world: int) -> torch.Tensor:
     return torch.cat(parts).to(flat.device)
 
 
+def _all_to_all(t: torch.Tensor, world: int) -> torch.Tensor:
+    """t [world, ...]: chunk t[q] goes to rank q; returns [world, ...] with out[s] = the chunk
+    rank s sent to this rank."""
+    if world == 1:
+        return t
+    import torch.distributed as dist
+    flat = t.contiguous()
+    if dist.get_backend() == "nccl":
+        out = torch.empty_like(flat)
+        dist.all_to_all_single(out, flat)
+        return out
+    host = flat.cpu()
+    parts = [torch.empty_like(host) for _ in range(world)]
+    dist.all_gather(parts, host)
+    r = dist.get_rank()
+    return torch.stack([part[r] for part in parts]).to(flat.device)
+
+
+def pod_slice(n_pods: int, world: int, rank: int) -> Tuple[int, int]:
+    """Pods [p0, p1) whose full lists `rank` owns: contiguous slices of ceil(P / world)."""
+    per = (n_pods + world - 1) // world
+    return min(n_pods, rank * per), min(n_pods, (rank + 1) * per)
+
+
+class ShardedFullList:
+    """Per-pod full HostPriorityList over a node-sharded TAS snapshot (one instance per rank).
+
+    The rank's Context holds nodes [node_base, node_base + n_local); `width` >= every rank's
+    n_local (node_range's first shard).  `run` returns (p0, p1, nodes [p1 - p0][world * width]
+    int32 global node ids, -1 past len, lens [p1 - p0] int32) for the pods this rank owns
+    (pod_slice)."""
+
+    def __init__(self, ctx, width: int, world: int, rank: int, node_base: int, device="cuda"):
+        self.ctx, self.width, self.world, self.rank = ctx, width, world, rank
+        self.node_base = node_base
+        self.device = device
+        self._bufs = {}
+
+    def _buf(self, name, shape, dtype):
+        return _cached(self._bufs, name, shape, dtype, self.device)
+
+    def run(self, gen: int, n_pods: int, n_rules: int, rules_t, rule_off_t, prio_t, cand_t=None,
+            stream=None):
+        w, world = self.width, self.world
+        per = (n_pods + world - 1) // world
+        on_gpu = torch.cuda.is_available() and str(self.device).startswith("cuda")
+        cur = torch.cuda.current_stream() if on_gpu else None
+        if stream is None:
+            stream = cur
+        # records of every pod over this shard, pods past n_pods (slice padding) all sentinels
+        key = self._buf("key", (world * per, w), torch.int64)
+        node = self._buf("node", (world * per, w), torch.int32)
+        ln = self._buf("len", (world * per,), torch.int32)
+        key[n_pods:].fill_(2**63 - 1)
+        node[n_pods:].fill_(2**31 - 1)
+        if on_gpu and stream != cur:
+            stream.wait_stream(cur)
+        self.ctx.tas_topk_device(gen, n_pods, n_rules, rules_t, rule_off_t, prio_t, cand_t, w,
+                                 self.node_base, key, node, ln, stream)
+        if on_gpu and stream != cur:
+            cur.wait_stream(stream)
+        # [owner rank][its pods][w] -> [shard][my pods][w]
+        keys_in = _all_to_all(key.view(world, per, w), world)
+        nodes_in = _all_to_all(node.view(world, per, w), world)
+        if on_gpu and stream != cur:
+            stream.wait_stream(cur)
+        p0, p1 = pod_slice(n_pods, world, self.rank)
+        out_node = self._buf("out_node", (per, world * w), torch.int32)
+        out_len = self._buf("out_len", (per,), torch.int32)
+        if per:
+            self.ctx.list_merge_device(per, world, w, keys_in, nodes_in, out_node, out_len,
+                                       stream=stream)
+        if on_gpu and stream != cur:
+            cur.wait_stream(stream)
+        return p0, p1, out_node[:p1 - p0], out_len[:p1 - p0]
+
+
+def _cached(bufs, name, shape, dtype, device):
+    b = bufs.get(name)
+    if b is None or tuple(b.shape) != tuple(shape):
+        b = torch.empty(shape, dtype=dtype, device=device)
+        bufs[name] = b
+    return b
+
+
 class ShardedTopK:
     """Per-pod global top-k over a node-sharded TAS snapshot (one instance per rank).
 
@@ -63,11 +155,7 @@ class ShardedTopK:
         self._bufs = {}
 
     def _buf(self, name, shape, dtype):
-        b = self._bufs.get(name)
-        if b is None or tuple(b.shape) != tuple(shape):
-            b = torch.empty(shape, dtype=dtype, device=self.device)
-            self._bufs[name] = b
-        return b
+        return _cached(self._bufs, name, shape, dtype, self.device)
 
     def run(self, gen: int, n_pods: int, n_rules: int, rules_t, rule_off_t, prio_t, cand_t=None,
             stream=None):

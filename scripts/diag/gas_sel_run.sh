@@ -1,8 +1,9 @@
 #!/bin/bash
-# GPU run of the GAS test files (fit, wide shapes, many selections, commit, shard top-k, extender).
+# GPU run of the GAS / shard test files (fit, wide shapes, many selections, commit, shard
+# top-k and full lists, extender).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gas_many_selections.py tests/test_gas_wide.py \
+timeout -k 10 900 python -u -m pytest tests/test_gas_many_selections.py tests/test_gas_wide.py \
   tests/test_gas_gpu.py tests/test_gas_commit.py tests/test_shard.py tests/test_extender.py \
   -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gas_sel.log 2>&1
 rc=$?; tail -25 gpurun_out/gas_sel.log; exit $rc

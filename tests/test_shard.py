@@ -382,3 +382,200 @@ def test_tas_gas_topk_equals_composition(ctx, k, n, cards, cand_frac):
     for a, b in zip(composed, lazy):
         np.testing.assert_array_equal(b, a)
     assert (composed[2] > 0).mean() > 0.4
+
+
+# ------------------------------------------------------------------- full lists over shards
+
+
+def test_pod_slice_partitions():
+    from pas_amd.shard import pod_slice
+    for n in (0, 1, 5, 64, 1001):
+        for world in (1, 2, 3, 8):
+            rs = [pod_slice(n, world, r) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == n
+            for (a0, a1), (b0, b1) in zip(rs, rs[1:]):
+                assert a1 == b0 and a0 <= a1
+
+
+def merge_full(keys_in, nodes_in):
+    """Reference merge of [S][P][w] shard runs: each pod's real records in (key, node) order."""
+    S, P, w = keys_in.shape
+    out = []
+    for p in range(P):
+        recs = [(int(keys_in[s, p, j]), int(nodes_in[s, p, j])) for s in range(S)
+                for j in range(w) if nodes_in[s, p, j] != np.iinfo(np.int32).max]
+        out.append([nd for _, nd in sorted(recs)])
+    return out
+
+
+def _gloo_full_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK=str(rank))
+    for p in (os.path.join(ROOT, "platform-aware-scheduling_amd"), os.path.join(ROOT, "oracle"),
+              os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import oracle
+    from pas_amd import distrib
+    from pas_amd.shard import _all_to_all, node_range, pod_slice
+
+    distrib.setup("gloo")
+    snap, batch = make_case(0xF1, 1300, 5, 11, 3, cand_frac=0.9)
+    v, pres = snap.v_milli, snap.present
+    n = v.shape[1]
+    n0, n1 = node_range(n, world, rank)
+    a0, a1 = node_range(n, world, 0)
+    w = a1 - a0  # the widest shard
+    P = len(batch.prio)
+    per = (P + world - 1) // world
+    keys = np.full((world * per, w), np.iinfo(np.int64).max, np.int64)
+    nodes = np.full((world * per, w), np.iinfo(np.int32).max, np.int32)
+    k, nd = records(oracle, v, pres, batch.rules, batch.rule_off, batch.prio, batch.cand, n0, n1,
+                    w)
+    keys[:P], nodes[:P] = k, nd
+    keys_in = _all_to_all(torch.from_numpy(keys).view(world, per, w), world).numpy()
+    nodes_in = _all_to_all(torch.from_numpy(nodes).view(world, per, w), world).numpy()
+    p0, p1 = pod_slice(P, world, rank)
+    merged = merge_full(keys_in, nodes_in)[:p1 - p0]
+    padded = np.full((max(p1 - p0, 0), n), -1, np.int64)
+    for i, lst in enumerate(merged):
+        padded[i, :len(lst)] = lst
+    np.save(os.path.join(out_dir, f"full{rank}.npy"), padded)
+    distrib.teardown(world)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_full_lists_over_gloo(tmp_path, oracle, world):
+    """The all-to-all of whole-shard records to the pods' owners, merged, gives the oracle's
+    cluster HostPriorityList for every pod (CPU, gloo; the oracle as the shard evaluator)."""
+    from pas_amd.shard import pod_slice
+    mp.spawn(_gloo_full_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+             join=True)
+    snap, batch = make_case(0xF1, 1300, 5, 11, 3, cand_frac=0.9)
+    _, order, lens = oracle.tas_eval(snap.v_milli, snap.present, batch.rules, batch.rule_off,
+                                     batch.prio, batch.cand, 3)
+    P = len(batch.prio)
+    for r in range(world):
+        p0, p1 = pod_slice(P, world, r)
+        got = np.load(tmp_path / f"full{r}.npy")
+        for i, p in enumerate(range(p0, p1)):
+            m = int(lens[p])
+            np.testing.assert_array_equal(got[i, :m], order[p, :m])
+            assert (got[i, m:] == -1).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("S,w", [(1, 5), (2, 1), (2, 1500), (3, 700), (5, 300), (8, 1024),
+                                 (8, 1025), (4, 3000)])
+def test_list_merge_kernel(ctx, S, w):
+    """pas_list_merge_device vs a sort of the union: random sorted runs with tied keys, keys
+    at INT64_MAX, empty and full runs, tile boundaries (1024 outputs per workgroup)."""
+    rng = np.random.default_rng(S * 1000 + w)
+    P = 6
+    keys = np.full((S, P, w), np.iinfo(np.int64).max, np.int64)
+    nodes = np.full((S, P, w), np.iinfo(np.int32).max, np.int32)
+    perm = rng.permutation(S * w * 4).astype(np.int32)
+    for p in range(P):
+        ids = perm[p * 0: S * w * 4].reshape(-1)[: S * w].reshape(S, w)
+        for s in range(S):
+            ln = [0, w, int(rng.integers(0, w + 1))][(p + s) % 3]
+            k = rng.integers(-5, 5, size=ln).astype(np.int64) * (2**61)  # many ties
+            k[rng.random(ln) < 0.05] = np.iinfo(np.int64).max  # real records at the max key
+            order = np.lexsort((ids[s, :ln], k))
+            keys[s, p, :ln] = k[order]
+            nodes[s, p, :ln] = ids[s, :ln][order]
+    want = merge_full(keys, nodes)
+    ld = S * w + 3
+    out = torch.full((P, ld), -7, dtype=torch.int32, device="cuda")
+    ln = torch.empty(P, dtype=torch.int32, device="cuda")
+    ctx.list_merge_device(P, S, w, _dev(keys), _dev(nodes), out, ln, out_ld=ld)
+    ctx.synchronize()
+    got, got_l = out.cpu().numpy(), ln.cpu().numpy()
+    for p in range(P):
+        m = len(want[p])
+        assert got_l[p] == m
+        np.testing.assert_array_equal(got[p, :m], want[p])
+        assert (got[p, m:S * w] == -1).all() and (got[p, S * w:] == -7).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_full_list_over_shards_equals_global(ctx, oracle, world):
+    """Whole-shard device records of every shard, merged on device, equal the oracle's
+    full HostPriorityList over the cluster for every pod."""
+    from pas_amd.shard import node_range
+    snap, batch = make_case(0xF2 + world, 4100, 6, 40, 5, cand_frac=0.85)
+    v, pres = snap.v_milli, snap.present
+    n = v.shape[1]
+    a0, a1 = node_range(n, world, 0)
+    w = a1 - a0
+    recs = [_shard_records_gpu(v, pres, batch, batch.cand, *node_range(n, world, r), w, 11)
+            for r in range(world)]
+    keys_all = torch.stack([a for a, _, _ in recs])
+    nodes_all = torch.stack([b for _, b, _ in recs])
+    P = len(batch.prio)
+    out = torch.empty((P, world * w), dtype=torch.int32, device="cuda")
+    ln = torch.empty(P, dtype=torch.int32, device="cuda")
+    ctx.list_merge_device(P, world, w, keys_all, nodes_all, out, ln)
+    ctx.synchronize()
+    _, order, lens = oracle.tas_eval(v, pres, batch.rules, batch.rule_off, batch.prio,
+                                     batch.cand, 3)
+    got, got_l = out.cpu().numpy(), ln.cpu().numpy()
+    np.testing.assert_array_equal(got_l, lens)
+    for p in range(P):
+        m = int(lens[p])
+        np.testing.assert_array_equal(got[p, :m], order[p, :m])
+        assert (got[p, m:] == -1).all()
+
+
+def _gpu_full_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world),
+                      RANK=str(rank), LOCAL_RANK="0")
+    for p in (os.path.join(ROOT, "platform-aware-scheduling_amd"), os.path.join(ROOT, "tests")):
+        sys.path.insert(0, p)
+    import pas_amd
+    from pas_amd import distrib
+    from pas_amd.shard import ShardedFullList, node_range
+
+    distrib.setup("gloo")  # ranks share the box's one GPU: collectives through host memory
+    torch.cuda.set_device(0)
+    snap, batch = make_case(0xF3, 5000, 6, 21, 5, cand_frac=0.85)
+    v, pres = snap.v_milli, snap.present
+    n = v.shape[1]
+    n0, n1 = node_range(n, world, rank)
+    a0, a1 = node_range(n, world, 0)
+    sv, sp = shard_snapshot(v, pres, n0, n1)
+    with pas_amd.Context(0) as c:
+        c.tas_snapshot_set(3, sv, sp)
+        rules_t, off_t, prio_t, cand_t = _rule_tensors(batch, shard_cand(batch.cand, n, n0, n1))
+        fl = ShardedFullList(c, a1 - a0, world, rank, n0)
+        s = torch.cuda.Stream() if rank == 0 else None
+        p0, p1, out, ln = fl.run(3, len(batch.prio), len(batch.rules), rules_t, off_t, prio_t,
+                                 cand_t, stream=s)
+        torch.cuda.synchronize()
+        np.save(os.path.join(out_dir, f"fl{rank}.npy"), out.cpu().numpy())
+        np.save(os.path.join(out_dir, f"fll{rank}.npy"), ln.cpu().numpy())
+        np.save(os.path.join(out_dir, f"flp{rank}.npy"), np.array([p0, p1]))
+    distrib.teardown(world)
+
+
+@pytest.mark.gpu
+def test_sharded_full_list_two_ranks_one_gpu(tmp_path, oracle):
+    """ShardedFullList end to end in two processes (gloo between them, one GPU): each rank
+    returns the cluster's full lists of its pod slice."""
+    world = 2
+    mp.spawn(_gpu_full_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+             join=True)
+    snap, batch = make_case(0xF3, 5000, 6, 21, 5, cand_frac=0.85)
+    _, order, lens = oracle.tas_eval(snap.v_milli, snap.present, batch.rules, batch.rule_off,
+                                     batch.prio, batch.cand, 3)
+    seen = 0
+    for r in range(world):
+        out, ln = np.load(tmp_path / f"fl{r}.npy"), np.load(tmp_path / f"fll{r}.npy")
+        p0, p1 = np.load(tmp_path / f"flp{r}.npy")
+        for i, p in enumerate(range(p0, p1)):
+            m = int(lens[p])
+            assert ln[i] == m
+            np.testing.assert_array_equal(out[i, :m], order[p, :m])
+            assert (out[i, m:] == -1).all()
+            seen += 1
+    assert seen == len(batch.prio)
