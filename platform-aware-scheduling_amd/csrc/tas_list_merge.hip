@@ -79,25 +79,37 @@ __device__ int64_t cut(const RunRef& a, const RunRef& b, int64_t w, int64_t d) {
   return lo;
 }
 
+// The cuts of every tile boundary of a round, [P][n_pairs][tiles + 1], one thread each (the
+// dependent binary-search loads of all boundaries in flight at once, ahead of the merge).
+__global__ void cuts_kernel(Runs in, int64_t w, int32_t n_pairs, int32_t tiles, int64_t n_cuts,
+                            int64_t* __restrict__ cuts) {
+  const int64_t t = (int64_t)blockIdx.x * kTpb + threadIdx.x;
+  if (t >= n_cuts) return;
+  const int32_t e = (int32_t)(t % (tiles + 1));
+  const int32_t m = (int32_t)((t / (tiles + 1)) % n_pairs);
+  const int32_t p = (int32_t)(t / ((int64_t)(tiles + 1) * n_pairs));
+  const RunRef A = run_ref(in, p, 2 * m), B = run_ref(in, p, 2 * m + 1);
+  cuts[t] = cut(A, B, w, min((int64_t)e * kTile, 2 * w));
+}
+
 // One round: pairs (2m, 2m + 1) of runs of width w -> run m of width 2w.  Blocks: (pod, pair,
 // tile) in x.  Output: out_key/out_node [P][...] with row pitch out_pitch, or (final round,
 // out_key null) the node ids only, sentinels as -1, positions < out_cols.
 __global__ __launch_bounds__(kTpb) void merge_round_kernel(Runs in, int64_t w, int32_t n_pairs,
-                                                           int32_t tiles, int64_t* out_key,
-                                                           int32_t* out_node, int64_t out_pitch,
-                                                           int64_t out_cols) {
+                                                           int32_t tiles,
+                                                           const int64_t* __restrict__ cuts,
+                                                           int64_t* out_key, int32_t* out_node,
+                                                           int64_t out_pitch, int64_t out_cols) {
   __shared__ int64_t sk[kTile];
   __shared__ int32_t sn[kTile];
-  __shared__ int64_t cuts[2];
   const int64_t b = blockIdx.x;
   const int32_t tile = (int32_t)(b % tiles);
   const int32_t m = (int32_t)((b / tiles) % n_pairs);
   const int32_t p = (int32_t)(b / ((int64_t)tiles * n_pairs));
   const RunRef A = run_ref(in, p, 2 * m), B = run_ref(in, p, 2 * m + 1);
   const int64_t d0 = (int64_t)tile * kTile, d1 = min(d0 + kTile, 2 * w);
-  if (threadIdx.x < 2) cuts[threadIdx.x] = cut(A, B, w, threadIdx.x ? d1 : d0);
-  __syncthreads();
-  const int64_t a0 = cuts[0], a1 = cuts[1];
+  const int64_t* bc = cuts + (b / tiles) * (tiles + 1) + tile;
+  const int64_t a0 = bc[0], a1 = bc[1];
   const int64_t b0 = d0 - a0, b1 = d1 - a1;
   const int32_t na = (int32_t)(a1 - a0), nb = (int32_t)(b1 - b0);
   for (int32_t i = threadIdx.x; i < na + nb; i += kTpb) {
@@ -174,12 +186,16 @@ int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t wi
   list_len_kernel<<<(n_pods + kTpb - 1) / kTpb, kTpb, 0, s>>>(n_pods, in, n_shards, width,
                                                              d_out_len);
   PAS_HIP(ctx, hipGetLastError());
-  // ping-pong rows [P][sp * width] for the rounds before the last
+  // the tile cuts of a round, then ping-pong rows [P][sp * width] for the rounds before the
+  // last.  A round has n_pairs * (tiles + 1) <= sp * width / kTile + 2 * n_pairs cuts per pod.
   int64_t* key_buf[2] = {nullptr, nullptr};
   int32_t* node_buf[2] = {nullptr, nullptr};
-  if (rounds > 1) {
-    const size_t half = (size_t)n_pods * row;
-    const size_t need = 2 * half * (sizeof(int64_t) + sizeof(int32_t));
+  const int64_t max_cuts = (int64_t)n_pods * ((row + kTile - 1) / kTile + 2 * sp + 2);
+  int64_t* cut_buf = nullptr;
+  {
+    const size_t half = rounds > 1 ? (size_t)n_pods * row : 0;
+    const size_t need =
+        2 * half * (sizeof(int64_t) + sizeof(int32_t)) + sizeof(int64_t) * (size_t)max_cuts;
     if (need > ctx->merge_bytes) {
       if (ctx->merge_buf) {
         PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -191,28 +207,32 @@ int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t wi
       ctx->merge_bytes = need;
     }
     char* base = static_cast<char*>(ctx->merge_buf);
-    key_buf[0] = reinterpret_cast<int64_t*>(base);
+    cut_buf = reinterpret_cast<int64_t*>(base);
+    key_buf[0] = cut_buf + max_cuts;
     key_buf[1] = key_buf[0] + half;
     node_buf[0] = reinterpret_cast<int32_t*>(key_buf[1] + half);
     node_buf[1] = node_buf[0] + half;
   }
-  if (rounds == 0) {  // one shard: its list is the cluster's; the pair (run 0, an empty run)
-    const int32_t tiles = (int32_t)((2 * (int64_t)width + kTile - 1) / kTile);
-    merge_round_kernel<<<(unsigned)((int64_t)n_pods * tiles), kTpb, 0, s>>>(
-        in, width, 1, tiles, nullptr, d_out_node, out_ld, cols);
+  auto round = [&](const Runs& rin, int64_t w, int32_t n_pairs, int64_t* ok, int32_t* on,
+                   int64_t pitch) -> int {
+    const int32_t tiles = (int32_t)((2 * w + kTile - 1) / kTile);
+    const int64_t n_cuts = (int64_t)n_pods * n_pairs * (tiles + 1);
+    cuts_kernel<<<(unsigned)((n_cuts + kTpb - 1) / kTpb), kTpb, 0, s>>>(rin, w, n_pairs, tiles,
+                                                                       n_cuts, cut_buf);
+    merge_round_kernel<<<(unsigned)((int64_t)n_pods * n_pairs * tiles), kTpb, 0, s>>>(
+        rin, w, n_pairs, tiles, cut_buf, ok, on, pitch, cols);
     PAS_HIP(ctx, hipGetLastError());
     return PAS_OK;
-  }
+  };
+  if (rounds == 0)  // one shard: its list is the cluster's; the pair (run 0, an empty run)
+    return round(in, width, 1, nullptr, d_out_node, out_ld);
   for (int32_t r = 0; r < rounds; ++r) {
     const int64_t w = (int64_t)width << r;
     const int32_t n_pairs = (int32_t)(sp >> (r + 1));
-    const int32_t tiles = (int32_t)((2 * w + kTile - 1) / kTile);
     const bool last = r == rounds - 1;
-    int64_t* ok = last ? nullptr : key_buf[r & 1];
-    int32_t* on = last ? d_out_node : node_buf[r & 1];
-    merge_round_kernel<<<(unsigned)((int64_t)n_pods * n_pairs * tiles), kTpb, 0, s>>>(
-        in, w, n_pairs, tiles, ok, on, last ? out_ld : row, cols);
-    PAS_HIP(ctx, hipGetLastError());
+    if (int rc = round(in, w, n_pairs, last ? nullptr : key_buf[r & 1],
+                       last ? d_out_node : node_buf[r & 1], last ? out_ld : row))
+      return rc;
     // the next round reads this round's rows: run i of width 2w at row offset i * 2w
     in = Runs{key_buf[r & 1], node_buf[r & 1], 2 * w, row, (int32_t)(sp >> (r + 1))};
   }
