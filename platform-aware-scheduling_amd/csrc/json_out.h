@@ -40,23 +40,23 @@ struct JsonOut {
     while (n) put(tmp[--n]);
   }
 
-  // UTF-8 sequence length at s (1..4) if valid per Go's utf8.DecodeRuneInString, else 0;
-  // *rune gets the code point.
-  static int utf8_len(const unsigned char* s, uint32_t* rune) {
+  // UTF-8 sequence length at s (1..4, within the `avail` bytes left) if valid per Go's
+  // utf8.DecodeRuneInString, else 0; *rune gets the code point.
+  static int utf8_len(const unsigned char* s, int64_t avail, uint32_t* rune) {
     const unsigned char c = s[0];
     if (c < 0x80) { *rune = c; return 1; }
-    auto cont = [](unsigned char x) { return (x & 0xC0) == 0x80; };
-    if (c >= 0xC2 && c <= 0xDF && cont(s[1])) {
+    auto cont = [&](int i) { return i < avail && (s[i] & 0xC0) == 0x80; };
+    if (c >= 0xC2 && c <= 0xDF && cont(1)) {
       *rune = ((c & 0x1Fu) << 6) | (s[1] & 0x3Fu);
       return 2;
     }
-    if (c >= 0xE0 && c <= 0xEF && cont(s[1]) && cont(s[2])) {
+    if (c >= 0xE0 && c <= 0xEF && cont(1) && cont(2)) {
       const uint32_t r = ((c & 0x0Fu) << 12) | ((s[1] & 0x3Fu) << 6) | (s[2] & 0x3Fu);
       if (r < 0x800 || (r >= 0xD800 && r <= 0xDFFF)) return 0;  // overlong / surrogate
       *rune = r;
       return 3;
     }
-    if (c >= 0xF0 && c <= 0xF4 && cont(s[1]) && cont(s[2]) && cont(s[3])) {
+    if (c >= 0xF0 && c <= 0xF4 && cont(1) && cont(2) && cont(3)) {
       const uint32_t r = ((c & 0x07u) << 18) | ((s[1] & 0x3Fu) << 12) | ((s[2] & 0x3Fu) << 6) |
                          (s[3] & 0x3Fu);
       if (r < 0x10000 || r > 0x10FFFF) return 0;
@@ -67,10 +67,14 @@ struct JsonOut {
   }
 
   // String body (no quotes) of the NUL-terminated s.
-  void str_body(const char* s) {
+  void str_body(const char* s) { str_body_n(s, (int64_t)std::strlen(s)); }
+
+  // String body (no quotes) of the n bytes at s.
+  void str_body_n(const char* s, int64_t n) {
     static const char hex[] = "0123456789abcdef";
     const unsigned char* p = reinterpret_cast<const unsigned char*>(s);
-    while (*p) {
+    const unsigned char* end = p + n;
+    while (p < end) {
       const unsigned char c = *p;
       if (c < 0x80) {
         switch (c) {
@@ -92,22 +96,27 @@ struct JsonOut {
         continue;
       }
       uint32_t r = 0;
-      const int n = utf8_len(p, &r);
-      if (n == 0) {
+      const int len = utf8_len(p, end - p, &r);
+      if (len == 0) {
         lit("\\ufffd");
         ++p;
       } else if (r == 0x2028 || r == 0x2029) {
         lit(r == 0x2028 ? "\\u2028" : "\\u2029");
-        p += n;
+        p += len;
       } else {
-        raw(reinterpret_cast<const char*>(p), n);
-        p += n;
+        raw(reinterpret_cast<const char*>(p), len);
+        p += len;
       }
     }
   }
   void str(const char* s) {
     put('"');
     str_body(s);
+    put('"');
+  }
+  void str_n(const char* s, int64_t n) {
+    put('"');
+    str_body_n(s, n);
     put('"');
   }
 };

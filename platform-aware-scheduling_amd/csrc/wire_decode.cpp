@@ -58,6 +58,7 @@
 #include <thread>
 #include <vector>
 
+#include "host_pool.h"
 #include "pas.h"
 
 namespace {
@@ -691,6 +692,14 @@ bool parallel_for(int n, F&& f) {
 #endif
   return true;
 }
+
+}  // namespace
+
+int pas::host_threads_for(int64_t bytes) { return decode_threads_for(bytes); }
+
+bool pas::host_parallel(int n, const std::function<void(int)>& f) { return parallel_for(n, f); }
+
+namespace {
 
 struct Masks {
   uint64_t quote, bs, open, close, comma;

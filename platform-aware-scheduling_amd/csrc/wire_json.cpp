@@ -27,6 +27,7 @@
 #include <string>
 #include <vector>
 
+#include "host_pool.h"
 #include "json_out.h"
 #include "pas.h"
 
@@ -105,14 +106,34 @@ int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const u
     o.lit("null");
   } else {
     o.put('[');
-    bool first = true;
+    // the passing nodes' JSON, comma-separated: offsets first, then the copies over host
+    // threads (chunks of about equal bytes); bytes past cap are counted, not stored
+    std::vector<int32_t> item;
+    std::vector<int64_t> at;
+    int64_t pos = o.pos;
     for (int32_t i = 0; i < n_req; ++i) {
       const int32_t n = req_node[i];
       if (!passed(pass, n)) continue;
-      if (!first) o.put(',');
-      first = false;
-      o.raw(node_json[n], node_json_len[n]);
+      if (!item.empty()) ++pos;  // the comma before it
+      item.push_back(n);
+      at.push_back(pos);
+      pos += node_json_len[n];
     }
+    const int64_t begin = o.pos, end = pos;
+    const int T = (int)std::min<int64_t>(pas::host_threads_for(end - begin), (int64_t)item.size());
+    auto copy = [&](int t) {
+      const int64_t lo = begin + (end - begin) * t / T;
+      const int64_t hi = t == T - 1 ? INT64_MAX : begin + (end - begin) * (t + 1) / T;
+      size_t j = std::lower_bound(at.begin(), at.end(), lo) - at.begin();
+      for (; j < item.size() && at[j] < hi; ++j) {
+        const int64_t a = at[j], len = node_json_len[item[j]];
+        if (j > 0 && a - 1 < cap) buf[a - 1] = ',';
+        if (a < cap) std::memcpy(buf + a, node_json[item[j]], (size_t)std::min(len, cap - a));
+      }
+    };
+    if (T <= 1 || !pas::host_parallel(T, copy))
+      for (int t = 0; t < std::max(T, 1); ++t) copy(t);
+    o.pos = end;
     o.put(']');
   }
   o.lit("},\"NodeNames\":[");
@@ -129,8 +150,7 @@ int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const u
     for (;;) {
       const char* sp = std::strchr(p, ' ');
       const int64_t len = sp ? sp - p : (int64_t)std::strlen(p);
-      std::string piece(p, (size_t)len);
-      o.str(piece.c_str());
+      o.str_n(p, len);
       o.put(',');
       if (!sp) break;
       p = sp + 1;
