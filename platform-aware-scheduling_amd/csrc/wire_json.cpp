@@ -53,6 +53,40 @@ void failed_nodes(pas::JsonOut& o, std::vector<const char*>& names, const char* 
   o.put('}');
 }
 
+// Items [0, n) joined by `sep` (0: none), encode(o, i) writing item i.  Many items are split
+// over host threads: each thread encodes a contiguous range into a buffer of its own (a
+// counting pass for the size, then the writing pass), and the pieces are appended in order.
+template <class F>
+void encode_items(pas::JsonOut& o, int64_t n, char sep, int64_t bytes_per_item, F&& encode) {
+  const int T = n >= 4096 ? (int)std::min<int64_t>(pas::host_threads_for(n * bytes_per_item),
+                                                   n / 1024)
+                          : 1;
+  auto range = [&](pas::JsonOut& w, int64_t i0, int64_t i1) {
+    for (int64_t i = i0; i < i1; ++i) {
+      if (i && sep) w.put(sep);
+      encode(w, i);
+    }
+  };
+  if (T <= 1) {
+    range(o, 0, n);
+    return;
+  }
+  std::vector<std::string> part((size_t)T);
+  auto run = [&](int t) {
+    const int64_t i0 = n * t / T, i1 = n * (t + 1) / T;
+    pas::JsonOut count{nullptr, 0};
+    range(count, i0, i1);
+    part[(size_t)t].resize((size_t)count.pos);
+    pas::JsonOut w{part[(size_t)t].data(), count.pos};
+    range(w, i0, i1);
+  };
+  if (!pas::host_parallel(T, run)) {
+    range(o, 0, n);
+    return;
+  }
+  for (const std::string& s : part) o.raw(s.data(), (int64_t)s.size());
+}
+
 int finish(pas::JsonOut& o, int64_t* out_len) {
   o.put('\n');  // json.Encoder terminates each value with a newline
   *out_len = o.pos;
@@ -75,14 +109,13 @@ int pas_encode_host_priority_list(int32_t len, const int32_t* order, const char*
     if (order[i] < 0 || !names[order[i]]) return PAS_EINVAL;
   pas::JsonOut o{buf, cap};
   o.put('[');
-  for (int32_t i = 0; i < len; ++i) {
-    if (i) o.put(',');
-    o.lit("{\"Host\":");
-    o.str(names[order[i]]);
-    o.lit(",\"Score\":");
-    o.integer(10 - (int64_t)i);  // Score: 10 - i (telemetryscheduler.go:145-147)
-    o.put('}');
-  }
+  encode_items(o, len, ',', 40, [&](pas::JsonOut& w, int64_t i) {
+    w.lit("{\"Host\":");
+    w.str(names[order[i]]);
+    w.lit(",\"Score\":");
+    w.integer(10 - i);  // Score: 10 - i (telemetryscheduler.go:145-147)
+    w.put('}');
+  });
   o.put(']');
   return finish(o, out_len);
 }
@@ -138,24 +171,24 @@ int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const u
   }
   o.lit("},\"NodeNames\":[");
   std::vector<const char*> failed;
+  std::vector<const char*> ok_names;
   for (int32_t i = 0; i < n_req; ++i) {
     const int32_t n = req_node[i];
-    if (!passed(pass, n)) {
-      failed.push_back(names[n]);
-      continue;
-    }
-    // availableNodeNames += node.Name + " ", later split on " ": a name with spaces
-    // becomes several entries
-    const char* p = names[n];
+    (passed(pass, n) ? ok_names : failed).push_back(names[n]);
+  }
+  // availableNodeNames += node.Name + " ", later split on " ": a name with spaces becomes
+  // several entries; each followed by a comma, then the final "" of the split
+  encode_items(o, (int64_t)ok_names.size(), 0, 24, [&](pas::JsonOut& w, int64_t i) {
+    const char* p = ok_names[(size_t)i];
     for (;;) {
       const char* sp = std::strchr(p, ' ');
       const int64_t len = sp ? sp - p : (int64_t)std::strlen(p);
-      o.str_n(p, len);
-      o.put(',');
+      w.str_n(p, len);
+      w.put(',');
       if (!sp) break;
       p = sp + 1;
     }
-  }
+  });
   o.lit("\"\"],\"FailedNodes\":");
   // strings.Join([]string{"Node violates"}, policy.Name) is "Node violates" (:206)
   failed_nodes(o, failed, "Node violates");

@@ -84,3 +84,48 @@ def test_capacity_past_the_parallel_copy(table, cut):
         assert out_len == len(full)
         assert rc == (_lib.PAS_OK if cap >= len(full) else _lib.PAS_ECAPACITY)
         assert got[:cap] == full[:cap]
+
+
+def _with_threads(threads, fn):
+    lib = _lib.load()
+    assert lib.pas_decode_set_threads(threads) == 0
+    try:
+        return fn()
+    finally:
+        lib.pas_decode_set_threads(0)
+
+
+def test_host_priority_list_threads():
+    # HostPriorityList of 60k entries ({"Host":..,"Score":10-i}, Score past -59 990), names
+    # with escapes and multi-byte code points
+    rng = np.random.default_rng(4)
+    names = [f"né-{i}" + ("<&>" if i % 7 == 0 else "") + ('"' if i % 11 == 0 else "")
+             for i in range(70000)]
+    table = wire.NodeTable(names)
+    order = rng.permutation(70000)[:60000].astype(np.int32)
+    one = _with_threads(1, lambda: wire.host_priority_list(order, table))
+    want = (json.dumps([{"Host": names[o], "Score": 10 - i} for i, o in enumerate(order)],
+                       separators=(",", ":"), ensure_ascii=False)
+            .replace("<", "\\u003c").replace(">", "\\u003e").replace("&", "\\u0026")
+            .encode() + b"\n")
+    assert one == want
+    for threads in (3, 16):
+        assert _with_threads(threads, lambda: wire.host_priority_list(order, table)) == one
+
+
+def test_node_names_with_spaces_threads(table):
+    # NodeNames is strings.Split of "name name ... " on " ": names with spaces split
+    t, names, objs = table
+    spaced = [n.replace("-0", " 0") if i % 5 == 0 else n for i, n in enumerate(names)]
+    t2 = wire.NodeTable(spaced, objs)
+    n = len(names)
+    req = np.arange(n, dtype=np.int32)
+    passed = np.random.default_rng(9).random(n) < 0.8
+    row = np.packbits(passed, bitorder="little")
+    row = np.pad(row, (0, (-len(row)) % 8)).view(np.uint64)
+    one = encode(t2, req, row, 1)
+    got = json.loads(one)
+    want_names = " ".join(spaced[i] for i in range(n) if passed[i]) + " "
+    assert got["NodeNames"] == want_names.split(" ")
+    for threads in (2, 16):
+        assert encode(t2, req, row, threads) == one
