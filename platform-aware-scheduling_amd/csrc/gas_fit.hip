@@ -360,7 +360,8 @@ __global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K,
                                                            const int64_t* __restrict__ used,
                                                            unsigned long long* __restrict__ gflip,
                                                            int32_t* __restrict__ big_nodes,
-                                                           int32_t* __restrict__ n_big_nodes) {
+                                                           int32_t* __restrict__ n_big_nodes,
+                                                           int64_t* __restrict__ free_t) {
   __shared__ int64_t red[kTpb / 64][PAS_GAS_MAX_RES];
   const int32_t n = blockIdx.x * kTpb + threadIdx.x;
   const int32_t nc = n < N ? min(n_cards[n], K) : 0;
@@ -373,6 +374,12 @@ __global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K,
       const int64_t f = (c > 0 && u >= 0) ? c - u : -1;
       m = f < m ? f : m;
     }
+    // the card-major copy (as load_free: -1 for cards the node does not have)
+    if (n < N)
+      for (int k = 0; k < kMaxCards; ++k) {
+        const int64_t u = k < nc ? used[((int64_t)n * K + k) * n_res + q] : -1;
+        free_t[((int64_t)k * n_res + q) * N + n] = (c > 0 && u >= 0) ? c - u : -1;
+      }
     for (int off = 32; off > 0; off >>= 1) {
       const int64_t o = __shfl_xor(m, off, 64);
       m = o < m ? o : m;
@@ -403,6 +410,21 @@ __device__ __forceinline__ void load_free(int32_t n, bool valid, int32_t ncard, 
     for (int q = 0; q < Q; ++q) {
       const int64_t u = k < ncard ? used[((int64_t)n * K + k) * Q + q] : -1;
       free[k][q] = (cap_r[q] > 0 && u >= 0) ? cap_r[q] - u : -1;
+    }
+}
+
+// The same from the card-major copy (GasSnapshot::free_t, one coalesced load per card and kind).
+template <int Q>
+__device__ __forceinline__ void load_free_t(int32_t n, bool valid, int32_t N,
+                                            const int64_t* __restrict__ free_t,
+                                            int64_t (&free)[kMaxCards][Q]) {
+  const int32_t nn = valid ? n : 0;
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int64_t f = free_t[((int64_t)k * Q + q) * N + nn];
+      free[k][q] = valid ? f : -1;
     }
 }
 
@@ -456,7 +478,7 @@ __device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t*
                                            int64_t p, int32_t N, int32_t n, bool valid,
                                            uint32_t out) {
   if (PAS_GAS_ABLATE & 1) {
-    if (out == 0x7fffffffu) res[n] = out;  // keeps the work alive; never true
+    if (out == (uint32_t)p * 2654435761u + 0x7fu) res[n] = out;  // keeps the work alive
     return;
   }
   if (kBits) {
@@ -1183,7 +1205,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
   }
 }
 
-template <int Q, bool kBits, int L = 0>
+template <int Q, bool kBits, bool kSeqOnly, int L = 0>
 __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
                                             int64_t* tab, uint32_t node_ok,
                                             int32_t N,
@@ -1193,15 +1215,16 @@ __device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q],
                                             const int32_t* __restrict__ counts,
                                             const BlockTile& bt, uint32_t* __restrict__ res,
                                             uint64_t* __restrict__ fit) {
-  multi_list<Q, L / kClasses - 1, L % kClasses, kBits>(
-      free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
-      sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
+  if constexpr (!kSeqOnly || L % kClasses == 2)
+    multi_list<Q, L / kClasses - 1, L % kClasses, kBits>(
+        free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
+        sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
   if constexpr (L + 1 < (Q + 1) * kClasses)
-    multi_lists<Q, kBits, L + 1>(free, stage, tab, node_ok, N, n, valid, P, multi, sels,
+    multi_lists<Q, kBits, kSeqOnly, L + 1>(free, stage, tab, node_ok, N, n, valid, P, multi, sels,
                                  counts, bt, res, fit);
 }
 
-template <int Q, bool kBits>
+template <int Q, bool kBits, bool kSeqOnly>
 __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
@@ -1220,8 +1243,505 @@ __global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
   // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  multi_lists<Q, kBits>(free, stage[wave], tab[wave], node_ok, N, n, valid, P,
-                        multi, sels, counts, bt, res, fit);
+  multi_lists<Q, kBits, kSeqOnly>(free, stage[wave], tab[wave], node_ok, N, n, valid, P,
+                                  multi, sels, counts, bt, res, fit);
+}
+
+// ---------------------------------------------------------------------------- ranked fit
+//
+// Rank compression (exact).  Every compare of the one-selection and closed-form paths is
+// "threshold t <= snapshot free f".  For a multiset T of at most 127 thresholds holding t,
+//   t <= f  <=>  #{t' in T : t' < t} + 1  <=  #{t' in T : t' <= f}
+// (t <= f: the right side counts t and everything below it; t > f: it counts only values
+// below t).  Both ranks fit 7 bits, so the ranks of four cards of one kind pack into a dword
+// as bytes rank + 0x80, and one 32-bit subtraction of the threshold's rank (replicated in
+// every byte) tests the four cards at once: byte k of the difference keeps bit 7 exactly
+// when card k passes, and no byte borrows from the next (each byte of it is >= 1).  A kind a
+// row does not request has rank 0 (always passes); a row whose threshold overflows int64
+// has rank 0x80 (never passes).
+//
+// The pods of each list are cut into groups of at most 127 thresholds per kind (127
+// one-selection pods; 42 two-selection pods of 3 threshold rows; 18 three-selection pods of
+// 7 rows), inside each block's chunk of the list.  gas_rank_prep_kernel sorts a group's
+// thresholds per kind (counting ranks, one wave per group) and writes each threshold's rank;
+// a fit kernel ranks its nodes' free values against the group once (a 7-step binary search
+// per card and kind) and then tests a row against the 8 cards with 2 subtractions per kind
+// and a few bit operations, instead of 8 64-bit compares and 8 mask updates per kind.
+constexpr int kRankMax = 127;       // thresholds per group and kind (7-bit ranks)
+constexpr int kRankItems = 128;     // sorted row length in LDS (padded with INT64_MAX)
+constexpr int kRankMB = 16;         // two/three-selection pods staged per batch (64-B rows)
+
+// A one-selection pod's ranks: g[j] = the rank of its need of compared kind j in every byte.
+struct alignas(16) GasRSingle {
+  uint32_t g[PAS_GAS_MAX_RES];
+  int32_t word;  // as GasSingle::word
+  int32_t pad[3];
+};
+// A two/three-selection pod's ranks: rows 0, 1, 3 (the full-mask rows: a selection's own need)
+// replicated per kind; rows 2, 4, 5, 6 (checked at one chosen card) packed, byte j = kind j.
+struct alignas(16) GasRMulti {
+  uint32_t rep[3][PAS_GAS_MAX_RES];
+  uint32_t pk[4];
+};
+// rword flags (free bits of a multi-list word): the full-mask rows that repeat an earlier one
+constexpr uint32_t kSame01 = 1u << 28, kSame03 = 1u << 29, kSame13 = 1u << 31;
+
+__device__ __forceinline__ int32_t rank_rows(int32_t cls) { return cls == 0 ? 1 : cls == 1 ? 3 : 7; }
+
+// The chunk [b, e) of a list of cnt entries (the split of list_share) and its ng groups of
+// sz (the last one possibly shorter) <= gs pods.
+__device__ __forceinline__ void chunk_groups(int32_t cnt, int32_t chunks, int32_t chunk,
+                                             int32_t gs, int32_t* b, int32_t* e, int32_t* ng,
+                                             int32_t* sz) {
+  const int32_t per = (cnt + chunks - 1) / chunks;
+  *b = min(cnt, chunk * per);
+  *e = min(cnt, *b + per);
+  *ng = (*e - *b + gs - 1) / gs;
+  *sz = *ng > 0 ? (*e - *b + *ng - 1) / *ng : 0;
+}
+
+// The one-selection lists are cut into fixed chunks of kRankMax pods, one group each (a block
+// of the fit kernel ranks its nodes once); the grid covers ceil(P / kRankMax) chunks.
+__device__ __forceinline__ void single_chunk(int32_t cnt, int32_t chunk, int32_t* b, int32_t* e,
+                                             int32_t* ng, int32_t* sz) {
+  *b = min(cnt, chunk * kRankMax);
+  *e = min(cnt, *b + kRankMax);
+  *ng = *e > *b ? 1 : 0;
+  *sz = *e - *b;
+}
+
+// One block per (list slot, chunk, group), a thread per (item, kind).  Slots: [0, NL) the
+// one-selection lists; NL + 2 l + c list l's two- (c = 0) and three-selection (c = 1) pods.  A
+// group's items are its pods' rows (pod-major).  Per compared kind: an item's rank =
+// #{items below it} (+ #{equal items before it} for its sorted position), written as the
+// sorted row (srt_*[item][kind j]) and as the item's rank in its pod's record.  Items of a
+// slot sit after those of the slots before it, so a group's sorted rows are contiguous.
+constexpr int kRankPrepTpb = kRankItems * PAS_GAS_MAX_RES;
+__global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
+    int32_t P, int32_t Q, const int32_t* __restrict__ counts, int32_t ch_s, int32_t ch_m,
+    int32_t maxg, const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
+    const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
+    GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti,
+    int32_t* __restrict__ rword) {
+  __shared__ int64_t v[PAS_GAS_MAX_RES][kRankItems];
+  __shared__ uint32_t pks[kRankItems];
+  const int32_t NL = Q + 1;
+  const int32_t slot = blockIdx.y;
+  const bool one = slot < NL;
+  const int32_t l = one ? slot : (slot - NL) >> 1;
+  const int32_t cls = one ? 0 : 1 + ((slot - NL) & 1);
+  const int32_t R = rank_rows(cls);
+  const int32_t chunks = one ? ch_s : ch_m;
+  const int32_t chunk = blockIdx.x / maxg, gi = blockIdx.x % maxg;
+  if (chunk >= chunks) return;
+  const int32_t ml = l * kClasses + (cls - 1);  // multi list (cls > 0)
+  const int32_t cnt = counts[one ? l : NL + ml];
+  int32_t b, e, ng, sz;
+  if (one) {
+    single_chunk(cnt, chunk, &b, &e, &ng, &sz);
+  } else {
+    chunk_groups(cnt, chunks, chunk, kRankMax / R, &b, &e, &ng, &sz);
+  }
+  if (gi >= ng) return;
+  const int32_t gb = b + gi * sz, ge = min(e, gb + sz);
+  const int32_t n = (ge - gb) * R;
+  int64_t base = 0;
+  if (one) {
+    for (int32_t s = 0; s < l; ++s) base += counts[s];
+  } else {
+    for (int32_t s = 0; s < slot - NL; ++s)
+      base += (int64_t)counts[NL + (s >> 1) * kClasses + (s & 1)] * rank_rows(1 + (s & 1));
+  }
+  base += (int64_t)gb * R;
+  int64_t* srt = one ? srt_s : srt_m;
+  const int32_t skip = l - 1;
+  const int32_t i = threadIdx.x % kRankItems, q = threadIdx.x / kRankItems;
+  const bool kind = q < Q && q != skip;
+  const int32_t j = q - (skip >= 0 && q > skip ? 1 : 0);  // compared-kind index
+  const bool live = kind && i < n;
+  const int32_t pos = gb + (i < n ? i / R : 0), row = i < n ? i % R : 0;
+  const GasThresholds* th = one ? nullptr
+                                : reinterpret_cast<const GasThresholds*>(
+                                      sels + ((int64_t)ml * P + pos) * kPacked + kThRow);
+  // values padded with INT64_MAX (never below an item; equal only to items past the padding)
+  int64_t y = INT64_MAX;
+  if (live) y = one ? single[(int64_t)l * P + pos].cmp[q] : th->th[row][q];
+  v[q][i] = y;
+  if (q == 0) pks[i] = 0u;
+  __syncthreads();
+  uint32_t g = 0u;
+  if (live) {
+    const int32_t n16 = (n + 15) & ~15;
+    int32_t less = 0, eqb = 0;
+    for (int32_t k0 = 0; k0 < n16; k0 += 16) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int64_t x = v[q][k0 + k];
+        less += x < y ? 1 : 0;
+        eqb += (x == y && k0 + k < i) ? 1 : 0;
+      }
+    }
+    srt[(base + less + eqb) * PAS_GAS_MAX_RES + j] = y;
+    const uint32_t over = one ? 0u : (uint32_t)th->over;
+    g = ((over >> row) & 1u) ? 0x80u : (uint32_t)(less + 1);
+    if (one) {
+      rsingle[(int64_t)l * P + pos].g[j] = g * 0x01010101u;
+    } else if (row == 0 || row == 1 || row == 3) {
+      rmulti[(int64_t)(l * 2 + cls - 1) * P + pos].rep[row == 3 ? 2 : row][j] = g * 0x01010101u;
+    } else {
+      atomicOr(&pks[i], g << (8 * j));
+    }
+  }
+  __syncthreads();
+  // one thread per item: the packed rows and the pod word
+  if (threadIdx.x >= kRankItems || i >= n) return;
+  if (one) {
+    rsingle[(int64_t)l * P + pos].word = single[(int64_t)l * P + pos].word;
+    return;
+  }
+  const int64_t mp = (int64_t)(l * 2 + cls - 1) * P + pos;
+  if (row == 2 || row >= 4) rmulti[mp].pk[row == 2 ? 0 : row - 3] = pks[i];
+  if (row == 0) {
+    const uint32_t o = (uint32_t)th->over;
+    rword[mp] = (int32_t)((uint32_t)multi[(int64_t)ml * P + pos] |
+                          (((o >> 8) & 1u) ? kSame01 : 0u) | (((o >> 9) & 1u) ? kSame03 : 0u) |
+                          (((o >> 10) & 1u) ? kSame13 : 0u));
+  }
+}
+
+// The group's sorted rows of the C compared kinds into the wave's LDS slice [C][128]
+// (positions past the group's items: INT64_MAX).
+template <int C>
+__device__ __forceinline__ void load_sorted(const int64_t* __restrict__ srt, int64_t item0,
+                                            int32_t n, int64_t* lds, int lane) {
+  int64_t x[2][C];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int32_t i = lane + 64 * it;
+    const int64_t* p = srt + (item0 + min(i, max(n - 1, 0))) * PAS_GAS_MAX_RES;
+#pragma unroll
+    for (int j = 0; j < C; ++j) x[it][j] = i < n ? p[j] : INT64_MAX;
+  }
+  __builtin_amdgcn_wave_barrier();  // the previous group's reads of the slice are done
+#pragma unroll
+  for (int it = 0; it < 2; ++it)
+#pragma unroll
+    for (int j = 0; j < C; ++j) lds[j * kRankItems + lane + 64 * it] = x[it][j];
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// The node's cards ranked against the group: fa[j] = bytes rank + 0x80 of cards 0, 2, 4, 6
+// (kind j), fb[j] of cards 1, 3, 5, 7.  rank = #{group thresholds <= free} (upper bound in
+// the sorted row; at most n, the padding is INT64_MAX).
+template <int Q, int SKIP, int C>
+__device__ __forceinline__ void rank_cards(const int64_t (&free)[kMaxCards][Q], const int64_t* lds,
+                                           int32_t n, uint32_t (&fa)[C], uint32_t (&fb)[C]) {
+#pragma unroll
+  for (int q = 0, j = 0; q < Q; ++q) {
+    if (q == SKIP) continue;
+    uint32_t a = 0u, b = 0u;
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k) {
+      const int64_t f = free[k][q];
+      int32_t pos = 0;
+#pragma unroll
+      for (int s = kRankItems / 2; s >= 1; s >>= 1)
+        pos = lds[j * kRankItems + pos + s - 1] <= f ? pos + s : pos;
+      const uint32_t r = (uint32_t)min(pos, n) + 0x80u;
+      if (k & 1) b |= r << (8 * (k >> 1));
+      else a |= r << (8 * (k >> 1));
+    }
+    fa[j] = a;
+    fb[j] = b;
+    ++j;
+  }
+}
+
+// Card mask of a row of replicated ranks g[j]: card k passes <=> bit 4k + 3.
+template <int C>
+__device__ __forceinline__ uint32_t rmask(const uint32_t (&fa)[C], const uint32_t (&fb)[C],
+                                          const uint32_t* g) {
+  uint32_t a = 0x80808080u, b = 0x80808080u;
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    a &= fa[j] - g[j];
+    b &= fb[j] - g[j];
+  }
+  return (a >> 4) | b;
+}
+
+// lowest set bit, 0xFFFFFFFF for none (v_ffbl_b32)
+__device__ __forceinline__ uint32_t lowbit(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : ~0u; }
+
+template <int Q, int SKIP, bool kBits>
+__device__ __forceinline__ void rsingle_list(const int64_t (&free)[kMaxCards][Q],
+                                             uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                             const GasRSingle* __restrict__ rs,
+                                             const int64_t* __restrict__ srt, int64_t item0,
+                                             int32_t cnt, const BlockTile& bt, int64_t* lds,
+                                             GasRSingle* stage, uint32_t* __restrict__ res,
+                                             uint64_t* __restrict__ fit) {
+  constexpr int kSkip = Q == 1 ? -1 : SKIP;
+  constexpr int C = Q - (kSkip >= 0 ? 1 : 0);
+  const int lane = threadIdx.x & 63;
+  int32_t gb, ge, ng, sz;
+  single_chunk(cnt, bt.chunk, &gb, &ge, &ng, &sz);
+  if (!ng) return;
+  load_sorted<C>(srt, item0 + gb, sz, lds, lane);
+  uint32_t fa[C], fb[C];
+  rank_cards<Q, kSkip, C>(free, lds, sz, fa, fb);
+  auto one_pod = [&](const GasRSingle& r, int32_t w) {
+    const int64_t pod = w & 0xFFFFFF;
+    uint32_t out = node_ok;
+    if (((w >> 24) & 0xF) == 1) {
+      uint32_t g[C];
+#pragma unroll
+      for (int jj = 0; jj < C; ++jj) g[jj] = r.g[jj];
+      const uint32_t m = (w & kBadPod) ? 0u : rmask<C>(fa, fb, g);
+      if constexpr (kBits) out = m ? node_ok : 0u;
+      else out = m ? (node_ok | (1u << 24) | (lowbit(m) >> 2)) : 0u;
+    }
+    put_result<kBits>(res, fit, pod, N, n, valid, out);
+  };
+  for (int32_t b0 = gb; b0 < ge; b0 += kPodBatch) {
+    const int32_t nb = __builtin_amdgcn_readfirstlane(min(kPodBatch, ge - b0));
+    constexpr int kWords = (int)(sizeof(GasRSingle) / 16);
+    constexpr int kIters = kPodBatch * kWords / 64;
+    const int4* src = reinterpret_cast<const int4*>(rs + b0);
+    int4 v[kIters];
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int32_t c = lane + it * 64;
+      v[it] = c < nb * kWords ? src[c] : int4{0, 0, 0, 0};
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    // pods in pairs: both records read (broadcast LDS reads) before the first one's tests
+    for (int32_t j = 0; j < nb; j += 2) {
+      const GasRSingle r0 = stage[j], r1 = stage[j + 1];
+      const int32_t w0 = __builtin_amdgcn_readfirstlane(r0.word);
+      const int32_t w1 = __builtin_amdgcn_readfirstlane(r1.word);
+      one_pod(r0, w0);
+      if (j + 1 < nb) one_pod(r1, w1);
+    }
+  }
+}
+
+template <int Q, bool kBits, int L = 0>
+__device__ __forceinline__ void rsingle_lists(const int64_t (&free)[kMaxCards][Q],
+                                              uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                              int32_t P, const GasRSingle* __restrict__ rs,
+                                              const int64_t* __restrict__ srt, int64_t item0,
+                                              const int32_t* __restrict__ counts,
+                                              const BlockTile& bt, int64_t* lds,
+                                              GasRSingle* stage, uint32_t* __restrict__ res,
+                                              uint64_t* __restrict__ fit) {
+  const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[L]);
+  rsingle_list<Q, L - 1, kBits>(free, node_ok, N, n, valid, rs + (int64_t)L * P, srt, item0, cnt,
+                                bt, lds, stage, res, fit);
+  if constexpr (L < Q)
+    rsingle_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, rs, srt, item0 + cnt, counts,
+                                   bt, lds, stage, res, fit);
+}
+
+template <int Q, bool kBits>
+__global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
+    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs, const int64_t* __restrict__ srt,
+    const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
+    uint64_t* __restrict__ fit) {
+  __shared__ int64_t lds[kTpb / 64][Q * kRankItems];   // sorted rows per wave
+  __shared__ GasRSingle stage[kTpb / 64][kPodBatch];  // a slice per wave
+  const BlockTile bt = block_tile(chunks);
+  // chunks past every list's end: nothing to load
+  int32_t most = 0;
+#pragma unroll
+  for (int l = 0; l <= Q; ++l) most = max(most, counts[l]);
+  if (bt.chunk * kRankMax >= __builtin_amdgcn_readfirstlane(most)) return;
+  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  int64_t free[kMaxCards][Q];
+  load_free_t<Q>(n, valid, N, free_t, free);
+  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  rsingle_lists<Q, kBits>(free, node_ok, N, n, valid, P, rs, srt, 0, counts, bt, lds[wave],
+                          stage[wave], res, fit);
+}
+
+// A row of packed ranks (byte j = kind j) checked at one card: x = the card's packed ranks
+// + 0x80 (the lane's table), every compared byte keeps bit 7.
+template <int C>
+__device__ __forceinline__ bool rpoint(uint32_t x, uint32_t gp) {
+  constexpr uint32_t kMc = C == 1 ? 0x80u : C == 2 ? 0x8080u : C == 3 ? 0x808080u : 0x80808080u;
+  return ((x - gp) & kMc) == kMc;
+}
+
+// Two- and three-selection pods in closed form (as closed_body) on ranks: masks of rows 0, 1, 3,
+// rows 2, 4, 5, 6 at the chosen cards from the lane's table of packed ranks.  Card positions
+// are bit positions 4c + 3 (0xFFFFFFFF: none), so min() picks the lower card and none loses.
+template <int C, int S>
+__device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint32_t (&fb)[C],
+                                           const GasRMulti& r, uint32_t w, const uint32_t* tab,
+                                           int lane, uint32_t node_ok) {
+  uint32_t g0[C], g1[C];
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    g0[j] = r.rep[0][j];
+    g1[j] = r.rep[1][j];
+  }
+  const uint32_t m0 = rmask<C>(fa, fb, g0);
+  const uint32_t m1 = (w & kSame01) ? m0 : rmask<C>(fa, fb, g1);
+  const uint32_t p0 = lowbit(m0);
+  const uint32_t x0 = tab[min(p0 >> 2, 7u) * 64 + lane];
+  const uint32_t u1 = lowbit(m1 & ~(1u << (p0 & 31u)));
+  const uint32_t p1 = rpoint<C>(x0, r.pk[0]) ? min(u1, p0) : u1;
+  uint32_t word = (p0 >> 2) | ((p1 >> 2) << 3);
+  uint32_t worst = max(p0, p1);
+  if constexpr (S == 3) {
+    uint32_t g3[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) g3[j] = r.rep[2][j];
+    const uint32_t m3 = (w & kSame03) ? m0 : (w & kSame13) ? m1 : rmask<C>(fa, fb, g3);
+    const uint32_t x1 = tab[min(p1 >> 2, 7u) * 64 + lane];
+    uint32_t touched;
+    if (p0 == p1) {
+      touched = rpoint<C>(x0, r.pk[3]) ? p0 : ~0u;
+    } else {
+      touched = min(rpoint<C>(x0, r.pk[1]) ? p0 : ~0u, rpoint<C>(x1, r.pk[2]) ? p1 : ~0u);
+    }
+    const uint32_t un = lowbit(m3 & ~(1u << (p0 & 31u)) & ~(1u << (p1 & 31u)));
+    const uint32_t p2 = min(un, touched);
+    word |= (p2 >> 2) << 6;
+    worst = max(worst, p2);
+  }
+  return worst < 32u ? (node_ok | ((uint32_t)S << 24) | (word & 0xFFFFFFu)) : 0u;
+}
+
+template <int Q, int SKIP, int S, bool kBits>
+__device__ __forceinline__ void rmulti_list(const int64_t (&free)[kMaxCards][Q], uint32_t node_ok,
+                                            int32_t N, int32_t n, bool valid,
+                                            const GasRMulti* __restrict__ rm,
+                                            const int32_t* __restrict__ rw,
+                                            const int64_t* __restrict__ srt, int64_t item0,
+                                            int32_t cnt, const BlockTile& bt, int64_t* lds,
+                                            GasRMulti* stage, uint32_t* tab,
+                                            uint32_t* __restrict__ res,
+                                            uint64_t* __restrict__ fit) {
+  constexpr int kSkip = Q == 1 ? -1 : SKIP;
+  constexpr int C = Q - (kSkip >= 0 ? 1 : 0);
+  constexpr int R = S == 2 ? 3 : 7;
+  const int lane = threadIdx.x & 63;
+  int32_t b, e, ng, sz;
+  chunk_groups(cnt, bt.chunks, bt.chunk, kRankMax / R, &b, &e, &ng, &sz);
+  for (int32_t gi = 0; gi < ng; ++gi) {
+    const int32_t gb = b + gi * sz, ge = min(e, gb + sz);
+    load_sorted<C>(srt, item0 + (int64_t)gb * R, (ge - gb) * R, lds, lane);
+    uint32_t fa[C], fb[C];
+    rank_cards<Q, kSkip, C>(free, lds, (ge - gb) * R, fa, fb);
+    // the lane's table: card k's packed ranks (byte j = kind j)
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k) {
+      uint32_t x = 0u;
+#pragma unroll
+      for (int j = 0; j < C; ++j)
+        x |= (((k & 1 ? fb[j] : fa[j]) >> (8 * (k >> 1))) & 0xFFu) << (8 * j);
+      tab[k * 64 + lane] = x;
+    }
+    for (int32_t b0 = gb; b0 < ge; b0 += kRankMB) {
+      const int32_t nb = min(kRankMB, ge - b0);
+      constexpr int kWords = (int)(sizeof(GasRMulti) / 16);
+      static_assert(kRankMB * kWords == 64, "one 16-B piece per lane");
+      const int4* src = reinterpret_cast<const int4*>(rm + b0);
+      const int4 v = lane < nb * kWords ? src[lane] : int4{0, 0, 0, 0};
+      const int32_t wd = lane < nb ? rw[b0 + lane] : 0;
+      __builtin_amdgcn_wave_barrier();
+      reinterpret_cast<int4*>(stage)[lane] = v;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      for (int32_t j = 0; j < nb; ++j) {
+        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(wd, j);
+        const int64_t pod = w & 0xFFFFFF;
+        uint32_t out = 0u;
+        if (!(w & kBadPod)) {
+          out = rclosed<C, S>(fa, fb, stage[j], w, tab, lane, node_ok);
+          if constexpr (kBits) out = out ? node_ok : 0u;
+        }
+        put_result<kBits>(res, fit, pod, N, n, valid, out);
+      }
+    }
+  }
+}
+
+template <int Q, bool kBits, int L = 0>
+__device__ __forceinline__ void rmulti_lists(const int64_t (&free)[kMaxCards][Q], uint32_t node_ok,
+                                             int32_t N, int32_t n, bool valid, int32_t P,
+                                             const GasRMulti* __restrict__ rm,
+                                             const int32_t* __restrict__ rw,
+                                             const int64_t* __restrict__ srt, int64_t item0,
+                                             const int32_t* __restrict__ counts,
+                                             const BlockTile& bt, int64_t* lds, GasRMulti* stage,
+                                             uint32_t* tab, uint32_t* __restrict__ res,
+                                             uint64_t* __restrict__ fit) {
+  // slot L: list L / 2, class L % 2 (S = 2 + L % 2); counts of the multi lists [l][kClasses]
+  constexpr int l = L / 2, S = 2 + L % 2;
+  const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[l * kClasses + L % 2]);
+  rmulti_list<Q, l - 1, S, kBits>(free, node_ok, N, n, valid, rm + (int64_t)L * P,
+                                  rw + (int64_t)L * P, srt, item0, cnt, bt, lds, stage, tab, res,
+                                  fit);
+  if constexpr (L + 1 < (Q + 1) * 2)
+    rmulti_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, rm, rw, srt,
+                                  item0 + (int64_t)cnt * (S == 2 ? 3 : 7), counts, bt, lds,
+                                  stage, tab, res, fit);
+}
+
+// Pods with several selections: the two- and three-selection lists on ranks, then the lists of
+// four to eight selections (multi_list, sequential on int64 free values).  The two phases use
+// the same LDS slice of the wave.
+template <int Q>
+struct MultiLds {
+  static constexpr int kC = Q > 1 ? Q - 1 : 1;
+  static constexpr size_t kRanked =
+      sizeof(int64_t) * Q * kRankItems + sizeof(GasRMulti) * kRankMB + sizeof(uint32_t) * kMaxCards * 64;
+  static constexpr size_t kSeq =
+      sizeof(GasSel) * kPacked * kMB + sizeof(int64_t) * kMaxCards * 64 * kC;
+  static constexpr size_t kBytes = kRanked > kSeq ? kRanked : kSeq;
+};
+
+template <int Q, bool kBits>
+__global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
+    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm, const int32_t* __restrict__ rw,
+    const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
+    const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
+    uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
+  __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kBytes / 16];
+  const BlockTile bt = block_tile(chunks);
+  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  int64_t free[kMaxCards][Q];
+  load_free_t<Q>(n, valid, N, free_t, free);
+  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* w = reinterpret_cast<char*>(smem[wave]);
+  int64_t* lds = reinterpret_cast<int64_t*>(w);
+  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w + sizeof(int64_t) * Q * kRankItems);
+  uint32_t* tab = reinterpret_cast<uint32_t*>(stage + kRankMB);
+  rmulti_lists<Q, kBits>(free, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
+                         tab, res, fit);
+  __builtin_amdgcn_wave_barrier();
+  GasSel* sstage = reinterpret_cast<GasSel*>(w);
+  int64_t* stab = reinterpret_cast<int64_t*>(sstage + kPacked * kMB);
+  multi_lists<Q, kBits, true>(free, sstage, stab, node_ok, N, n, valid, P, multi, sels, counts, bt,
+                              res, fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -1401,7 +1921,14 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_sels = al(sizeof(GasSel) * kPacked * (size_t)NL * kClasses * n_pods);
   const size_t b_pods = al(sizeof(int32_t) * (size_t)n_pods);
   constexpr size_t b_tail = ((1 + kClasses) * (PAS_GAS_MAX_RES + 1) + 1) * sizeof(int32_t);
-  const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_tail;
+  // ranked paths: pod records and sorted rows (items: <= P one-selection, <= 7P closed-form)
+  const size_t b_rs = al(sizeof(GasRSingle) * (size_t)NL * n_pods);
+  const size_t b_rm = al(sizeof(GasRMulti) * (size_t)NL * 2 * n_pods);
+  const size_t b_rw = al(sizeof(int32_t) * (size_t)NL * 2 * n_pods);
+  const size_t b_srs = al(sizeof(int64_t) * PAS_GAS_MAX_RES * (size_t)n_pods);
+  const size_t b_srm = al(sizeof(int64_t) * PAS_GAS_MAX_RES * 7 * (size_t)n_pods);
+  const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_rs + b_rm + b_rw + b_srs +
+                      b_srm + b_tail;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -1423,6 +1950,16 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   base += b_pods;
   int32_t* pod_steps = reinterpret_cast<int32_t*>(base);
   base += b_pods;
+  GasRSingle* rsingle = reinterpret_cast<GasRSingle*>(base);
+  base += b_rs;
+  GasRMulti* rmulti = reinterpret_cast<GasRMulti*>(base);
+  base += b_rm;
+  int32_t* rword = reinterpret_cast<int32_t*>(base);
+  base += b_rw;
+  int64_t* srt_s = reinterpret_cast<int64_t*>(base);
+  base += b_srs;
+  int64_t* srt_m = reinterpret_cast<int64_t*>(base);
+  base += b_srm;
   int32_t* counts = reinterpret_cast<int32_t*>(base);
   int32_t* n_big_pods = counts + (1 + kClasses) * (PAS_GAS_MAX_RES + 1);
   unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
@@ -1434,28 +1971,41 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   if (ctx->gas.derived_epoch != ctx->gas.epoch) {
     PAS_HIP(ctx, hipMemsetAsync(gflip, 0, 64, s));
     gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
-                                                             gflip, big_nodes, n_big_nodes);
+                                                             gflip, big_nodes, n_big_nodes,
+                                                             static_cast<int64_t*>(g.free_t));
     ctx->gas.derived_epoch = ctx->gas.epoch;
   }
   gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
       multi, sels, counts, big_pods, n_big_pods, pod_steps);
-  timing_end(ctx, s, &tl);
-  PAS_HIP(ctx, hipGetLastError());
-  // grids: (node block, pod chunk) pairs, ~4096 blocks; each kernel splits each of its
+  // grids: (node block, pod chunk) pairs, ~8192 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
   const int32_t nb_s = (N + kTpb - 1) / kTpb;
-  const int32_t ch_s = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_SINGLE + nb_s - 1) / nb_s));
+  const int32_t ch_s = (n_pods + kRankMax - 1) / kRankMax;  // fixed one-group chunks
   const int32_t ch_m = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_s - 1) / nb_s));
+  {
+    // one wave per (slot, chunk, group): groups per chunk <= ceil(ceil(P / chunks) / gs)
+    auto groups = [&](int32_t ch, int32_t gs) {
+      const int32_t per = (n_pods + ch - 1) / ch;
+      return (per + gs - 1) / gs;
+    };
+    const int32_t maxg = std::max(groups(ch_m, kRankMax / 3), groups(ch_m, kRankMax / 7));
+    const dim3 grid((unsigned)(std::max(ch_s, ch_m) * maxg), (unsigned)(NL * 3));
+    gas_rank_prep_kernel<<<grid, kRankPrepTpb, 0, s>>>(n_pods, Q, counts, ch_s, ch_m, maxg, single, multi,
+                                             sels, srt_s, srt_m, rsingle, rmulti, rword);
+  }
+  timing_end(ctx, s, &tl);
+  PAS_HIP(ctx, hipGetLastError());
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
-    gas_fit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                 \
-        N, K, n_pods, g.n_cards, g.cap, g.used, single, counts, ch_s, d_res, d_fit);           \
-    gas_fit_multi_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                  \
-        N, K, n_pods, g.n_cards, g.cap, g.used, multi, sels, counts + NL, ch_m, d_res, d_fit); \
+    gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, ch_s, d_res, d_fit);        \
+    gas_rfit_multi_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                 \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m, multi, sels, counts + NL,      \
+        ch_m, d_res, d_fit);                                                                   \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)

@@ -128,6 +128,7 @@ void free_gas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(g.cap));
   free_ptr(reinterpret_cast<void*&>(g.used));
   free_ptr(g.derived);
+  free_ptr(g.free_t);
   g = GasSnapshot{};
 }
 
@@ -557,6 +558,8 @@ static int gas_alloc(pas_ctx* ctx, int32_t n_nodes, int32_t max_cards, int32_t n
     PAS_HIP(ctx, hipMalloc(&g.used, sizeof(int64_t) * nn * (size_t)std::max(max_cards, 1) *
                                         (size_t)std::max(n_res, 1)));
     PAS_HIP(ctx, hipMalloc(&g.derived, 64 + sizeof(int32_t) * nn));
+    PAS_HIP(ctx, hipMalloc(&g.free_t, sizeof(int64_t) * PAS_GAS_PACKED *
+                                          (size_t)std::max(n_res, 1) * nn));
     g.n_nodes = n_nodes;
     g.max_cards = max_cards;
     g.n_res = n_res;

@@ -87,6 +87,9 @@ struct GasSnapshot {
   uint64_t epoch = 1;
   uint64_t derived_epoch = 0;
   void* derived = nullptr;  // gflip[4] u64 | n_big_nodes i32 (+pad) | big_nodes[N] i32
+  // card-major free values of the first 8 cards, free_t[k][q][n] (gas_fit.hip), derived
+  // with the above: the fit kernels' per-node loads are then coalesced
+  void* free_t = nullptr;
 };
 
 struct TimedLaunch {

@@ -28,7 +28,7 @@ for f in glob.glob(out + "/*_p*/**/*counter_collection.csv", recursive=True):
     tag = os.path.relpath(f, out).split("_p")[0]
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        if "gas_fit" not in n: continue
+        if "pas::" not in n or "gas_" not in n: continue
         k = n.split("(anonymous namespace)::")[1].split("(")[0]
         agg[(tag, k, r["Counter_Name"])].append(float(r["Counter_Value"]))
 for (t, k, c), v in sorted(agg.items()):

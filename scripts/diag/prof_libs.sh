@@ -16,7 +16,7 @@ for L in tree "$@"; do
 import csv, glob, sys
 for f in glob.glob(sys.argv[1] + "/**/*kernel_stats.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "gas_fit" in r["Name"]:
+        if "pas::" in r["Name"] and "gas_" in r["Name"]:
             n = r["Name"].split("(anonymous namespace)::")[-1].split("(")[0]
             print(f'{sys.argv[2]:24s} {n:40s} avg_us={float(r["AverageNs"])/1e3:9.1f} calls={r["Calls"]}')
 PY
