@@ -356,10 +356,13 @@ def bench_gas(args, world, rank):
                                 stream)
     req_t, mask_t = dev(batch.req), dev(batch.req_mask.view(np.int32))
     nc_t = dev(batch.n_containers)
-    res_t = torch.empty((P, N), dtype=torch.int32, device="cuda")
+    # result rows at a pitch of N rounded up to 32 words (pas_gas_fit_ld_device): every row
+    # starts on a 128-B line; --gas-pitch dense writes [P][N] rows
+    ld = N if args.gas_pitch == "dense" else (N + 31) // 32 * 32
+    res_t = torch.empty((P, ld), dtype=torch.int32, device="cuda")
 
     def step():
-        ctx.gas_fit_device(1, P, C, wl.I915, req_t, mask_t, nc_t, res_t, stream)
+        ctx.gas_fit_ld_device(1, P, C, wl.I915, req_t, mask_t, nc_t, res_t, ld, stream=stream)
 
     settle_steps = distrib.settle(step, args.settle, world=world)
     for _ in range(args.warmup):
@@ -373,6 +376,21 @@ def bench_gas(args, world, rank):
         step()
     ctx.set_timing(0)
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
+    # the same batch into dense [P][N] rows (pas_gas_fit_device), untimed extra steps
+    dense_ms = None
+    if ld != N:
+        dres_t = torch.empty((P, N), dtype=torch.int32, device="cuda")
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(3):
+            ctx.gas_fit_device(1, P, C, wl.I915, req_t, mask_t, nc_t, dres_t, stream)
+        a.record(stream)
+        for _ in range(args.steps):
+            ctx.gas_fit_device(1, P, C, wl.I915, req_t, mask_t, nc_t, dres_t, stream)
+        b.record(stream)
+        b.synchronize()
+        dense_ms = a.elapsed_time(b) / args.steps
+        assert torch.equal(dres_t, res_t[:, :N]), "dense and pitched results differ"
+        del dres_t
     alg_bytes = N * (8 * Q + 8 * K * Q + 4) + P * (8 * C * Q + 4 * C + 4) + 4 * P * N
     kernel_s = gpu["ms_per_step"] / 1e3
     achieved = alg_bytes / kernel_s / 1e9
@@ -383,12 +401,15 @@ def bench_gas(args, world, rank):
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C3)",
         "config": {"settle_steps": settle_steps, "workload": "gas_fit (BASELINE configs[2])", "pods_per_gpu": P, "nodes": N,
-                   "cards": K, "resources": Q,
-                   "fit_fraction": float((res_t.cpu().numpy().view(np.uint32) >> 31).mean())},
+                   "cards": K, "resources": Q, "result_row_pitch": ld,
+                   "dense_pitch_gpu_ms_per_step": dense_ms,
+                   "fit_fraction": float((res_t[:, :N].cpu().numpy().view(np.uint32) >> 31)
+                                         .mean())},
         "roofline": {"bound": "hbm",
-                     "kernel": "gas fit path: gas_prep_kernel, gas_fit_single_kernel, "
-                               "gas_fit_multi_kernel and gas_fit_generic_kernel (two HIP events "
-                               "on the launch stream around the timed steps)",
+                     "kernel": "gas fit path: gas_prep_kernel, gas_rank_prep_kernel, "
+                               "gas_rfit_single_kernel, gas_rfit_multi_kernel and "
+                               "gas_fit_generic_kernel (two HIP events on the launch stream "
+                               "around the timed steps)",
                      "fit_launches_ms": k_ms / max(k_n, 1),
                      "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
@@ -657,6 +678,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--gas-pitch", choices=["aligned", "dense"], default="aligned",
+                    help="GAS result rows: N rounded up to 32 words (default) or dense N")
     ap.add_argument("--workload", choices=["tas", "gas", "deschedule", "c5", "launch_check"],
                     default="tas")
     ap.add_argument("--pods", type=int, default=None)

@@ -340,6 +340,19 @@ int pas_gas_fit_ex_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t ma
                           pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
                           void* hip_stream);
 
+/* pas_gas_fit_ex_device with a result row pitch: the word of (pod p, node n) goes to
+ * d_res_out[p * ld_res + n], ld_res >= n_nodes (words n_nodes .. ld_res - 1 of a row are not
+ * written).  A pitch that is a multiple of 32 words starts every row on a 128-byte line: the
+ * fit kernels store a wave's 64 node words as one 256-byte piece of a row, and pieces that
+ * straddle lines (every other row of an odd-multiple-of-16 dense pitch, e.g. 50 000) are
+ * written ~25 % slower.  The selection side buffer is optional (d_side / d_side_count null,
+ * side_cap 0).  Same results as pas_gas_fit_ex_device otherwise (scheduler.go:449-482). */
+int pas_gas_fit_ld_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                          int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
+                          const int32_t* d_n_containers, uint32_t* d_res_out, int64_t ld_res,
+                          pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
+                          void* hip_stream);
+
 /* Pods of the last GAS fit call on this context with more than PAS_GAS_MAX_SELECTIONS
  * selections (their fitting words are PAS_GAS_SEL_LIMIT).  Waits for the call's stream. */
 int pas_gas_limit_count(pas_ctx* ctx, int64_t* n_pods_out);

@@ -374,7 +374,7 @@ __global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K,
       const int64_t f = (c > 0 && u >= 0) ? c - u : -1;
       m = f < m ? f : m;
     }
-    // the card-major copy (as load_free: -1 for cards the node does not have)
+    // the card-major copy (free_t, load_free_t: -1 for cards the node does not have)
     if (n < N)
       for (int k = 0; k < kMaxCards; ++k) {
         const int64_t u = k < nc ? used[((int64_t)n * K + k) * n_res + q] : -1;
@@ -395,25 +395,8 @@ __global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K,
 }
 
 // free[k][q] = cap[q] - used[k][q] if cap[q] > 0 and used[k][q] >= 0, else -1 (and -1 for
-// cards the node does not have).
-template <int Q>
-__device__ __forceinline__ void load_free(int32_t n, bool valid, int32_t ncard, int32_t K,
-                                          const int64_t* __restrict__ cap,
-                                          const int64_t* __restrict__ used,
-                                          int64_t (&free)[kMaxCards][Q]) {
-  int64_t cap_r[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) cap_r[q] = valid ? cap[(int64_t)n * Q + q] : 0;
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int64_t u = k < ncard ? used[((int64_t)n * K + k) * Q + q] : -1;
-      free[k][q] = (cap_r[q] > 0 && u >= 0) ? cap_r[q] - u : -1;
-    }
-}
-
-// The same from the card-major copy (GasSnapshot::free_t, one coalesced load per card and kind).
+// cards the node does not have), from the card-major copy (GasSnapshot::free_t, built by
+// gas_minfree_kernel; one coalesced load per card and kind).
 template <int Q>
 __device__ __forceinline__ void load_free_t(int32_t n, bool valid, int32_t N,
                                             const int64_t* __restrict__ free_t,
@@ -430,40 +413,6 @@ __device__ __forceinline__ void load_free_t(int32_t n, bool valid, int32_t N,
 
 typedef unsigned long long lane_mask;  // one bit per lane of the wave (ballot)
 
-// First card (lexicographic rank) passing checkResourceCapacity, or -1: cmp[q] <= free[k][q]
-// for every kind (cmp is INT64_MIN for kinds the container does not request).
-template <int Q, int SKIP>
-__device__ __forceinline__ int first_fit(const int64_t (&free)[kMaxCards][Q],
-                                         const int64_t (&cmp)[Q]) {
-  int chosen = -1;
-#pragma unroll
-  for (int k = kMaxCards - 1; k >= 0; --k) {  // first fit = lowest k
-    bool ok = true;
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (q != SKIP) ok &= cmp[q] <= free[k][q];  // lane masks and-ed in SALU
-    chosen = ok ? k : chosen;                    // one select per card
-  }
-  return chosen;
-}
-
-// Whether any card passes: the fit bit alone (bitmap outputs), no card order needed, so the
-// per-card lane masks are or-ed in SALU instead of selecting a card per lane.
-template <int Q, int SKIP>
-__device__ __forceinline__ bool any_fit(const int64_t (&free)[kMaxCards][Q],
-                                        const int64_t (&cmp)[Q]) {
-  bool any = false;
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k) {
-    bool ok = true;
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (q != SKIP) ok &= cmp[q] <= free[k][q];
-    any |= ok;
-  }
-  return any;
-}
-
 // One (pod, node) result: the packed word, or (kBits) the fit bit in the pod's row of a
 // node bitmap, written per 64-node word by lane 0 of the wave (waves cover aligned
 // 64-node ranges).
@@ -473,12 +422,16 @@ __device__ __forceinline__ bool any_fit(const int64_t (&free)[kMaxCards][Q],
 #ifndef PAS_GAS_STORE_AUX
 #define PAS_GAS_STORE_AUX 2  // result word store cache policy: nt (0: plain global store)
 #endif
+// The result words: word (p, n) at w[p * ld + n] (ld >= N; pas_gas_fit_ld_device).
+struct ResOut {
+  uint32_t* w;
+  int64_t ld;
+};
 template <bool kBits>
-__device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t* __restrict__ fit,
-                                           int64_t p, int32_t N, int32_t n, bool valid,
-                                           uint32_t out) {
+__device__ __forceinline__ void put_result(ResOut res, uint64_t* __restrict__ fit, int64_t p,
+                                           int32_t N, int32_t n, bool valid, uint32_t out) {
   if (PAS_GAS_ABLATE & 1) {
-    if (out == (uint32_t)p * 2654435761u + 0x7fu) res[n] = out;  // keeps the work alive
+    if (out == (uint32_t)p * 2654435761u + 0x7fu) res.w[n] = out;  // keeps the work alive
     return;
   }
   if (kBits) {
@@ -487,10 +440,10 @@ __device__ __forceinline__ void put_result(uint32_t* __restrict__ res, uint64_t*
   } else if (PAS_GAS_STORE_AUX) {
     // the pod's row as a buffer (lanes past N store nothing), with the store cache policy
     const __amdgpu_buffer_rsrc_t row =
-        __builtin_amdgcn_make_buffer_rsrc(res + p * N, 0, N * 4, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc(res.w + p * res.ld, 0, N * 4, 0x00020000);
     __builtin_amdgcn_raw_buffer_store_b32(out, row, n * 4, 0, PAS_GAS_STORE_AUX);
   } else if (valid) {
-    res[p * N + n] = out;
+    res.w[p * res.ld + n] = out;
   }
 }
 
@@ -517,108 +470,7 @@ __device__ __forceinline__ void list_share(const int32_t* count, const BlockTile
   *e = min(cnt, *b + per);
 }
 
-constexpr int kPodBatch = 64;  // single-selection pod records staged in LDS per round and wave
-
-// Pods with at most one selection, list `l` (kind SKIP = l - 1 dropped): a read-only first
-// fit per (pod, node lane).  Each wave stages the records of kPodBatch pods in its own LDS
-// slice (no block barrier) and reads them back with broadcast LDS reads: the compare values
-// stay in VGPRs, only the pod word goes to an SGPR.  (Vector loads of each record straight
-// from memory wait for the previous pod's result store: vmcnt counts stores and completes
-// in order.)
-template <int Q, int SKIP, bool kBits>
-__device__ __forceinline__ void single_list(const int64_t (&free)[kMaxCards][Q],
-                                            uint32_t node_ok, int32_t N, int32_t n, bool valid,
-                                            const GasSingle* __restrict__ single,
-                                            const int32_t* __restrict__ count, GasSingle* stage,
-                                            const BlockTile& bt, uint32_t* __restrict__ res,
-                                            uint64_t* __restrict__ fit) {
-  const int32_t lane = threadIdx.x & 63;
-  int32_t i0, i1;
-  list_share(count, bt, &i0, &i1);
-  for (int32_t b0 = i0; b0 < i1; b0 += kPodBatch) {
-    const int32_t nb = min(kPodBatch, i1 - b0);
-    constexpr int kWords = (int)(sizeof(GasSingle) / 16);
-    constexpr int kIters = kPodBatch * kWords / 64;
-    static_assert(kPodBatch * kWords % 64 == 0, "stage copy");
-    const int4* src = reinterpret_cast<const int4*>(single + b0);
-    int4 v[kIters];
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-      const int32_t c = lane + it * 64;
-      v[it] = c < nb * kWords ? src[c] : int4{0, 0, 0, 0};
-    }
-    __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    // broadcast LDS reads, the next pod's issued before this pod's compares
-    int64_t cmp[Q];
-    int32_t word;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) cmp[q] = q == SKIP ? 0 : stage[0].cmp[q];
-    word = stage[0].word;
-    for (int32_t j = 0; j < nb; ++j) {
-      const int32_t jn = min(j + 1, kPodBatch - 1);
-      int64_t ncmp[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) ncmp[q] = q == SKIP ? 0 : stage[jn].cmp[q];
-      const int32_t nword = stage[jn].word;
-      const int32_t w = __builtin_amdgcn_readfirstlane(word);
-      const int64_t pod = w & 0xFFFFFF;
-      uint32_t out = node_ok;
-      if (((w >> 24) & 0xF) == 1) {
-        if constexpr (kBits) {
-          out = (!(w & kBadPod) && any_fit<Q, SKIP>(free, cmp)) ? node_ok : 0u;
-        } else {
-          const int k = (w & kBadPod) ? -1 : first_fit<Q, SKIP>(free, cmp);
-          out = k >= 0 ? (node_ok | (1u << 24) | (uint32_t)k) : 0u;
-        }
-      }
-      put_result<kBits>(res, fit, pod, N, n, valid, out);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) cmp[q] = ncmp[q];
-      word = nword;
-    }
-  }
-}
-
-template <int Q, bool kBits, int L = 0>
-__device__ __forceinline__ void single_lists(const int64_t (&free)[kMaxCards][Q],
-                                             uint32_t node_ok, int32_t N, int32_t n, bool valid,
-                                             int32_t P, const GasSingle* __restrict__ single,
-                                             const int32_t* __restrict__ counts,
-                                             GasSingle* stage, const BlockTile& bt,
-                                             uint32_t* __restrict__ res,
-                                             uint64_t* __restrict__ fit) {
-  single_list<Q, L - 1, kBits>(free, node_ok, N, n, valid, single + (int64_t)L * P, counts + L,
-                               stage, bt, res, fit);
-  if constexpr (L < Q)
-    single_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, single, counts, stage, bt, res,
-                                  fit);
-}
-
-template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_fit_single_kernel(
-    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
-    const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
-    const GasSingle* __restrict__ single, const int32_t* __restrict__ counts, int32_t chunks,
-    uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
-  __shared__ GasSingle stage[kTpb / 64][kPodBatch];  // a slice per wave
-  const BlockTile bt = block_tile(chunks);
-  const int32_t n = bt.node_block * kTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
-  int64_t free[kMaxCards][Q];
-  load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
-  // FetchNode error / missing cards label -> errWontFit before any container (:282-298);
-  // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
-  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
-  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  single_lists<Q, kBits>(free, node_ok, N, n, valid, P, single, counts, stage[wave], bt, res,
-                         fit);
-}
+constexpr int kPodBatch = 64;  // one-selection pod records staged in LDS per round and wave
 
 // A group of cards of the untouched-card scan: bm * 2 + (1 if need[q] <= free[q] for the C
 // compared kinds), card by card from the highest, so bit k of the final mask is card k.
@@ -700,35 +552,9 @@ __device__ __forceinline__ uint32_t push2_c4(uint32_t bm, const int64_t (&n)[4],
       : "scc");
   return r;
 }
-// C = 2, two threshold rows A and B over the same 2 cards, their carry chains interleaved
-// (two independent dependence chains in one block)
-__device__ __forceinline__ void push2x2_c2(uint32_t& ba, uint32_t& bb, int64_t a0, int64_t a1,
-                                           int64_t b0, int64_t b1, int64_t x0, int64_t x1,
-                                           int64_t y0, int64_t y1) {
-  uint32_t ra, rb;
-  uint64_t m0, m1, m2, m3, m4, m5, m6, m7, co;
-  asm(PAS_CMP(m0, a0, x0) PAS_CMP(m1, a1, x1) PAS_CMP(m2, b0, x0) PAS_CMP(m3, b1, x1)
-      PAS_CMP(m4, a0, y0) PAS_CMP(m5, a1, y1) PAS_CMP(m6, b0, y0) PAS_CMP(m7, b1, y1)
-      PAS_AND(m0, m0, m1) PAS_AND(m2, m2, m3) PAS_AND(m4, m4, m5) PAS_AND(m6, m6, m7)
-      PAS_ADDC(ra, ia, m0) PAS_ADDC(rb, ib, m2) PAS_ADDC(ra, ra, m4) PAS_ADDC(rb, rb, m6)
-      : [ra] "=&v"(ra), [rb] "=&v"(rb), [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2),
-        [m3] "=&s"(m3), [m4] "=&s"(m4), [m5] "=&s"(m5), [m6] "=&s"(m6), [m7] "=&s"(m7),
-        [co] "=&s"(co)
-      : [a0] "v"(a0), [a1] "v"(a1), [b0] "v"(b0), [b1] "v"(b1), [x0] "v"(x0), [x1] "v"(x1),
-        [y0] "v"(y0), [y1] "v"(y1), [ia] "v"(ba), [ib] "v"(bb)
-      : "scc");
-  ba = ra;
-  bb = rb;
-}
 #undef PAS_CMP
 #undef PAS_AND
 #undef PAS_ADDC
-
-// Two fit masks at once (rows a and b), interleaved where a two-row block exists (C = 2).
-template <int C>
-__device__ __forceinline__ void fit_mask2(const int64_t (&a)[C], const int64_t (&b)[C],
-                                          const int64_t (&fr)[kMaxCards][C], uint64_t live,
-                                          uint32_t* ma, uint32_t* mb);
 
 // Bit mask of the cards k (bit k) with need[j] <= fr[k][j] for all C compared kinds.
 template <int C>
@@ -772,30 +598,6 @@ __device__ __forceinline__ uint32_t fit_mask(const int64_t (&need)[C],
 
 constexpr int kMB = 2;  // multi-selection pods staged in LDS per round and wave (LDS: 4 workgroups per CU)
 constexpr int kRowChunks = kPacked * (int)sizeof(GasSel) / 16;  // 16-B chunks per row
-// the 16-B piece of a row whose first dword is GasThresholds::over
-constexpr int kOverPiece =
-    (kThRow * (int)sizeof(GasSel) + (int)offsetof(GasThresholds, over)) / 16;
-static_assert((kThRow * sizeof(GasSel) + offsetof(GasThresholds, over)) % 16 == 0, "over");
-
-// Fit mask of the compared kinds (all but SKIP) of a threshold row: bit k = card k's snapshot
-// free passes every compared threshold.
-template <int C>
-__device__ __forceinline__ void fit_mask2(const int64_t (&a)[C], const int64_t (&b)[C],
-                                          const int64_t (&fr)[kMaxCards][C], uint64_t live,
-                                          uint32_t* ma, uint32_t* mb) {
-  if constexpr (C == 2) {
-    uint32_t x = 0u, y = 0u;
-#pragma unroll
-    for (int k = kMaxCards - 1; k > 0; k -= 2)
-      push2x2_c2(x, y, a[0], a[1], b[0], b[1], fr[k][0], fr[k][1], fr[k - 1][0], fr[k - 1][1]);
-    *ma = x;
-    *mb = y;
-  } else {
-    *ma = fit_mask<C>(a, fr, live);
-    *mb = fit_mask<C>(b, fr, live);
-  }
-}
-
 template <int Q, int SKIP>
 __device__ __forceinline__ uint32_t th_mask(const int64_t (&free)[kMaxCards][Q], const int64_t* th,
                                             uint64_t live) {
@@ -814,80 +616,7 @@ __device__ __forceinline__ uint32_t th_mask(const int64_t (&free)[kMaxCards][Q],
   return fit_mask<kC>(need, fr, live);
 }
 
-template <int Q, int SKIP>
-__device__ __forceinline__ void th_mask2(const int64_t (&free)[kMaxCards][Q], const int64_t* ta,
-                                         const int64_t* tb, uint64_t live, uint32_t* ma,
-                                         uint32_t* mb) {
-  constexpr int kSkip = Q == 1 ? -1 : SKIP;
-  constexpr int kC = Q - (kSkip >= 0 ? 1 : 0);
-  int64_t a[kC], b[kC];
-  int64_t fr[kMaxCards][kC];
-#pragma unroll
-  for (int q = 0, j = 0; q < Q; ++q)
-    if (q != kSkip) {
-      a[j] = ta[q];
-      b[j++] = tb[q];
-    }
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0, j = 0; q < Q; ++q)
-      if (q != kSkip) fr[k][j++] = free[k][q];
-  fit_mask2<kC>(a, b, fr, live, ma, mb);
-}
-
 __device__ __forceinline__ uint32_t lowest(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : 8u; }
-__device__ __forceinline__ uint32_t bit(uint32_t m, uint32_t k) { return (m >> k) & 1u; }
-
-// A pod with 2 or 3 selections, in closed form.  Selection t takes the first card whose free
-// covers its need plus the takes already on that card (addRM, resource_map.go:38-53); which
-// earlier takes those are depends only on the earlier choices, so every combination is one
-// threshold row of the snapshot free values (GasThresholds) and each row is one fit mask:
-//   c0 = lowest(m0)
-//   c1 = min(lowest(m1 without c0), c0 if m2 has c0)
-//   c2 = min(lowest(m3 without c0, c1),
-//            c0 == c1 ? (c0 if m6 has c0) : min(c0 if m4 has c0, c1 if m5 has c1))
-// The masks are independent of each other (no per-lane state, no dependent chain).
-template <int Q, int SKIP>
-__device__ __forceinline__ uint32_t multi_closed(const int64_t (&free)[kMaxCards][Q],
-                                                 const GasThresholds& t, int32_t S,
-                                                 uint64_t live, uint32_t node_ok) {
-  // every row read before the masks (one LDS round trip), masks without branches: an
-  // overflowing threshold's mask is computed and cleared
-  const int32_t over = __builtin_amdgcn_readfirstlane(t.over);
-  const int rows = S == 3 ? 7 : 3;
-  int64_t th[7][Q];
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) th[j][q] = j < 3 || S == 3 ? t.th[j][q] : 0;
-  uint32_t m[7];
-  th_mask2<Q, SKIP>(free, th[0], th[1], live, &m[0], &m[1]);
-  m[2] = th_mask<Q, SKIP>(free, th[2], live);
-  if (rows == 7) {
-    th_mask2<Q, SKIP>(free, th[3], th[4], live, &m[3], &m[4]);
-    th_mask2<Q, SKIP>(free, th[5], th[6], live, &m[5], &m[6]);
-  } else {
-    m[3] = m[4] = m[5] = m[6] = 0u;
-  }
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-    if ((over >> j) & 1) m[j] = 0u;  // an overflowing threshold passes no card
-  const uint32_t c0 = lowest(m[0]);
-  const uint32_t c1 = min(lowest(m[1] & ~(1u << c0)), bit(m[2], c0) ? c0 : 8u);
-  uint32_t word = c0 | (c1 << 3);
-  bool fits = c0 < 8u && c1 < 8u;
-  if (S == 3) {
-    const uint32_t untouched = lowest(m[3] & ~(1u << c0) & ~(1u << c1));
-    const uint32_t touched =
-        c0 == c1 ? (bit(m[6], c0) ? c0 : 8u)
-                 : min(bit(m[4], c0) ? c0 : 8u, bit(m[5], c1) ? c1 : 8u);
-    const uint32_t c2 = min(untouched, touched);
-    fits = fits && c2 < 8u;
-    word |= c2 << 6;
-  }
-  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
-}
 
 // Lane-private copy of the node's free values of the compared kinds (all but SKIP) in LDS,
 // [card][lane][kind], so that a lane can read its chosen card's values back with one LDS read
@@ -908,97 +637,6 @@ __device__ __forceinline__ void fill_tab(const int64_t (&free)[kMaxCards][Q], co
 #pragma unroll
     for (int q = 0, j = 0; q < Q; ++q)
       if (q != SKIP) tab.at(k, lane)[j++] = free[k][q];
-}
-
-// threshold row th (all Q kinds, SKIP dropped) against a gathered card's free values
-template <int Q, int SKIP, int kC>
-__device__ __forceinline__ bool th_fits(const int64_t* th, const int64_t (&g)[kC]) {
-  bool ok = true;
-#pragma unroll
-  for (int q = 0, j = 0; q < Q; ++q)
-    if (q != SKIP) ok &= th[q] <= g[j++];
-  return ok;
-}
-
-// multi_closed with the rows that only matter at an already chosen card (2, 4, 5, 6) checked
-// at that card alone, on its free values read back from the lane's LDS copy: S = 2 computes
-// two fit masks instead of three, S = 3 three instead of seven.
-// kOvf: some threshold of the pod overflows (over bits 0-6).  Such pods are rare, so the
-// common instantiation drops every overflow test.
-// kSame: 1 / 0 = the first two selections ask the same / not (one mask or two), -1 = read it
-// from over bit 8 (the rare overflow instantiation).
-template <int Q, int SKIP, int kC, int S, bool kOvf, int kSame>
-__device__ __forceinline__ uint32_t closed_body(const int64_t (&free)[kMaxCards][Q],
-                                                const GasThresholds& t, int32_t over,
-                                                uint64_t live, uint32_t node_ok,
-                                                const FreeTab<kC>& tab, int lane) {
-  auto ov = [&](int bit) { return kOvf && (over & bit) != 0; };
-  int64_t th[7][Q];
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) th[j][q] = j < 3 || S == 3 ? t.th[j][q] : 0;
-  uint32_t m0, m1, m3 = 0u;
-  if (kSame == 1 || (kSame < 0 && (over & (1 << 8)))) {  // the first two ask the same: one mask
-    m0 = th_mask<Q, SKIP>(free, th[0], live);
-    m1 = m0;
-  } else {
-    th_mask2<Q, SKIP>(free, th[0], th[1], live, &m0, &m1);
-  }
-  if (S == 3) {
-    if (over & (1 << 9)) m3 = m0;
-    else if (over & (1 << 10)) m3 = m1;
-    else m3 = th_mask<Q, SKIP>(free, th[3], live);
-  }
-  if (ov(1)) m0 = 0u;  // an overflowing threshold passes no card
-  if (ov(2)) m1 = 0u;
-  if (ov(8)) m3 = 0u;
-  // card indices with "none" = 8: bit 8 as a sentinel under every 8-card mask, so the
-  // lowest set bit needs no zero test; 8 fails every `< 8` below and clears only bit 8
-  const uint32_t c0 = (uint32_t)__builtin_ctz(m0 | 0x100u);
-  int64_t g0[kC];
-  {
-    const int64_t* p = tab.at(min(c0, 7u), lane);
-#pragma unroll
-    for (int j = 0; j < kC; ++j) g0[j] = p[j];
-  }
-  const bool b2 = !ov(4) && th_fits<Q, SKIP, kC>(th[2], g0);
-  const uint32_t u1 = (uint32_t)__builtin_ctz((m1 & ~(1u << c0)) | 0x100u);
-  const uint32_t c1 = b2 ? min(u1, c0) : u1;
-  uint32_t word = c0 | (c1 << 3);
-  uint32_t any = c0 | c1;  // >= 8 when a selection found no card
-  if (S == 3) {
-    int64_t g1[kC];
-    const int64_t* p = tab.at(min(c1, 7u), lane);
-#pragma unroll
-    for (int j = 0; j < kC; ++j) g1[j] = p[j];
-    uint32_t touched;
-    if (c0 == c1) {
-      touched = (!ov(64) && th_fits<Q, SKIP, kC>(th[6], g0)) ? c0 : 8u;
-    } else {
-      const uint32_t t4 = (!ov(16) && th_fits<Q, SKIP, kC>(th[4], g0)) ? c0 : 8u;
-      const uint32_t t5 = (!ov(32) && th_fits<Q, SKIP, kC>(th[5], g1)) ? c1 : 8u;
-      touched = min(t4, t5);
-    }
-    const uint32_t untouched =
-        (uint32_t)__builtin_ctz((m3 & ~(1u << c0) & ~(1u << c1)) | 0x100u);
-    const uint32_t c2 = min(untouched, touched);
-    any |= c2;
-    word |= c2 << 6;
-  }
-  return any < 8u ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
-}
-
-template <int Q, int SKIP, int kC, int S>
-__device__ __forceinline__ uint32_t multi_closed_g(const int64_t (&free)[kMaxCards][Q],
-                                                   const GasThresholds& t, int32_t over,
-                                                   uint64_t live, uint32_t node_ok,
-                                                   const FreeTab<kC>& tab, int lane) {
-  if (over & 0x7F)
-    return closed_body<Q, SKIP, kC, S, true, -1>(free, t, over, live, node_ok, tab, lane);
-  if (over & (1 << 8))
-    return closed_body<Q, SKIP, kC, S, false, 1>(free, t, over, live, node_ok, tab, lane);
-  return closed_body<Q, SKIP, kC, S, false, 0>(free, t, over, live, node_ok, tab, lane);
 }
 
 // A pod with 4 to 8 selections: the selections in order on a working copy of the free values
@@ -1116,18 +754,18 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
   return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
 }
 
-// Pods with several selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
+// Pods of 4 to 8 selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
 // the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
 // reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
 // waiting for its copy does not hold up the other waves of the block.
-template <int Q, int SKIP, int kCls, bool kBits>
+template <int Q, int SKIP, bool kBits>
 __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
                                            int64_t* tab_base, uint32_t node_ok,
                                            int32_t N, int32_t n, bool valid,
                                            const int32_t* __restrict__ list,
                                            const GasSel* __restrict__ sels,
                                            const int32_t* __restrict__ count, const BlockTile& bt,
-                                           uint32_t* __restrict__ res,
+                                           ResOut res,
                                            uint64_t* __restrict__ fit) {
   const int32_t lane = threadIdx.x & 63;
   const uint64_t live = __ballot(valid && node_ok != 0u);
@@ -1161,9 +799,9 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
     for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
     // for the sequential class: which selections repeat the previous one, for the whole batch
     // in one ballot (lane l holds 16-B piece l % 4 of selection (l % 32) / 4 of row l / 32)
-    uint64_t same_m = 0;
-    if constexpr (kCls == 2) {
-      static_assert(kIters == 1 && kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "pieces");
+    static_assert(kIters == 1 && kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "pieces");
+    uint64_t same_m;
+    {
       const int4 u = v[0];
       const int ux = __shfl_up(u.x, 4, 64), uy = __shfl_up(u.y, 4, 64);
       const int uz = __shfl_up(u.z, 4, 64), uw = __shfl_up(u.w, 4, 64);
@@ -1172,10 +810,8 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    // the batch's pod words and threshold flags straight from the staging registers (lane j:
-    // pod j's word; the flags word sits in piece kOverPiece of its row), not read back from LDS
-    static_assert(kIters == 1, "one staging register per lane");
-    const int32_t wcur = wd, vcur = v[0].x;
+    // the batch's pod words straight from the staging register (lane j: pod j's word)
+    const int32_t wcur = wd;
     load_batch(b0 + kMB);
     for (int32_t j = 0; j < nb; ++j) {
       const int32_t pw = __builtin_amdgcn_readlane(wcur, j);
@@ -1184,15 +820,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
       const GasSel* rec = stage + j * kPacked;
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
-        const GasThresholds& th = *reinterpret_cast<const GasThresholds*>(rec + kThRow);
-        if constexpr (kCls < 2) {  // S = 2 or 3: closed form
-          if constexpr (kGather)
-            out = multi_closed_g<Q, SKIP, kC, 2 + kCls>(
-                free, th, __builtin_amdgcn_readlane(vcur, j * kRowChunks + kOverPiece), live,
-                node_ok, tab, lane);
-          else
-            out = multi_closed<Q, SKIP>(free, th, 2 + kCls, live, node_ok);
-        } else if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
+        if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
           if constexpr (kGather)
             out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane,
                                          (uint32_t)(same_m >> (32 * j)));
@@ -1205,46 +833,20 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
   }
 }
 
-template <int Q, bool kBits, bool kSeqOnly, int L = 0>
-__device__ __forceinline__ void multi_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                            int64_t* tab, uint32_t node_ok,
-                                            int32_t N,
-                                            int32_t n, bool valid, int32_t P,
-                                            const int32_t* __restrict__ multi,
-                                            const GasSel* __restrict__ sels,
-                                            const int32_t* __restrict__ counts,
-                                            const BlockTile& bt, uint32_t* __restrict__ res,
-                                            uint64_t* __restrict__ fit) {
-  if constexpr (!kSeqOnly || L % kClasses == 2)
-    multi_list<Q, L / kClasses - 1, L % kClasses, kBits>(
-        free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
-        sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
-  if constexpr (L + 1 < (Q + 1) * kClasses)
-    multi_lists<Q, kBits, kSeqOnly, L + 1>(free, stage, tab, node_ok, N, n, valid, P, multi, sels,
-                                 counts, bt, res, fit);
-}
-
-template <int Q, bool kBits, bool kSeqOnly>
-__global__ __launch_bounds__(kTpb) void gas_fit_multi_kernel(
-    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
-    const int64_t* __restrict__ cap, const int64_t* __restrict__ used,
-    const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
-    const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
-    uint64_t* __restrict__ fit) {
-  __shared__ GasSel stage[kTpb / 64][kPacked * kMB];  // a slice per wave
-  constexpr int kC = Q > 1 ? Q - 1 : 1;
-  __shared__ int64_t tab[kTpb / 64][kMaxCards * 64 * kC];  // FreeTab per wave
-  const BlockTile bt = block_tile(chunks);
-  const int32_t n = bt.node_block * kTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
-  int64_t free[kMaxCards][Q];
-  load_free<Q>(n, valid, min(nc, K), K, cap, used, free);
-  // nodes with more than 8 cards are left to gas_fit_generic_kernel (0 here)
-  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
-  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  multi_lists<Q, kBits, kSeqOnly>(free, stage[wave], tab[wave], node_ok, N, n, valid, P,
-                                  multi, sels, counts, bt, res, fit);
+// The lists of pods with 4 to 8 selections (class 2 of each kind-skip list).
+template <int Q, bool kBits, int l = 0>
+__device__ __forceinline__ void seq_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
+                                          int64_t* tab, uint32_t node_ok, int32_t N, int32_t n,
+                                          bool valid, int32_t P, const int32_t* __restrict__ multi,
+                                          const GasSel* __restrict__ sels,
+                                          const int32_t* __restrict__ counts, const BlockTile& bt,
+                                          ResOut res, uint64_t* __restrict__ fit) {
+  constexpr int L = l * kClasses + 2;
+  multi_list<Q, l - 1, kBits>(free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
+                              sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
+  if constexpr (l < Q)
+    seq_lists<Q, kBits, l + 1>(free, stage, tab, node_ok, N, n, valid, P, multi, sels, counts, bt,
+                               res, fit);
 }
 
 // ---------------------------------------------------------------------------- ranked fit
@@ -1287,63 +889,22 @@ struct alignas(16) GasRMulti {
 constexpr uint32_t kSame01 = 1u << 28, kSame03 = 1u << 29, kSame13 = 1u << 31;
 
 __device__ __forceinline__ int32_t rank_rows(int32_t cls) { return cls == 0 ? 1 : cls == 1 ? 3 : 7; }
+__device__ __forceinline__ int32_t rank_gs(int32_t cls) { return kRankMax / rank_rows(cls); }
 
-// The chunk [b, e) of a list of cnt entries (the split of list_share) and its ng groups of
-// sz (the last one possibly shorter) <= gs pods.
-__device__ __forceinline__ void chunk_groups(int32_t cnt, int32_t chunks, int32_t chunk,
-                                             int32_t gs, int32_t* b, int32_t* e, int32_t* ng,
-                                             int32_t* sz) {
-  const int32_t per = (cnt + chunks - 1) / chunks;
-  *b = min(cnt, chunk * per);
-  *e = min(cnt, *b + per);
-  *ng = (*e - *b + gs - 1) / gs;
-  *sz = *ng > 0 ? (*e - *b + *ng - 1) / *ng : 0;
-}
-
-// The one-selection lists are cut into fixed chunks of kRankMax pods, one group each (a block
-// of the fit kernel ranks its nodes once); the grid covers ceil(P / kRankMax) chunks.
-__device__ __forceinline__ void single_chunk(int32_t cnt, int32_t chunk, int32_t* b, int32_t* e,
-                                             int32_t* ng, int32_t* sz) {
-  *b = min(cnt, chunk * kRankMax);
-  *e = min(cnt, *b + kRankMax);
-  *ng = *e > *b ? 1 : 0;
-  *sz = *e - *b;
-}
-
-// One block per (list slot, chunk, group), a thread per (item, kind).  Slots: [0, NL) the
-// one-selection lists; NL + 2 l + c list l's two- (c = 0) and three-selection (c = 1) pods.  A
-// group's items are its pods' rows (pod-major).  Per compared kind: an item's rank =
-// #{items below it} (+ #{equal items before it} for its sorted position), written as the
-// sorted row (srt_*[item][kind j]) and as the item's rank in its pod's record.  Items of a
-// slot sit after those of the slots before it, so a group's sorted rows are contiguous.
-constexpr int kRankPrepTpb = kRankItems * PAS_GAS_MAX_RES;
-__global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
-    int32_t P, int32_t Q, const int32_t* __restrict__ counts, int32_t ch_s, int32_t ch_m,
-    int32_t maxg, const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
+__device__ __forceinline__ void rank_group(
+    int32_t P, int32_t Q, const int32_t* __restrict__ counts, int32_t slot, int32_t gi,
+    const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
-    GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti,
-    int32_t* __restrict__ rword) {
-  __shared__ int64_t v[PAS_GAS_MAX_RES][kRankItems];
-  __shared__ uint32_t pks[kRankItems];
+    GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti, int32_t* __restrict__ rword,
+    int64_t (*v)[kRankItems], uint32_t* pks) {
   const int32_t NL = Q + 1;
-  const int32_t slot = blockIdx.y;
   const bool one = slot < NL;
   const int32_t l = one ? slot : (slot - NL) >> 1;
   const int32_t cls = one ? 0 : 1 + ((slot - NL) & 1);
   const int32_t R = rank_rows(cls);
-  const int32_t chunks = one ? ch_s : ch_m;
-  const int32_t chunk = blockIdx.x / maxg, gi = blockIdx.x % maxg;
-  if (chunk >= chunks) return;
   const int32_t ml = l * kClasses + (cls - 1);  // multi list (cls > 0)
   const int32_t cnt = counts[one ? l : NL + ml];
-  int32_t b, e, ng, sz;
-  if (one) {
-    single_chunk(cnt, chunk, &b, &e, &ng, &sz);
-  } else {
-    chunk_groups(cnt, chunks, chunk, kRankMax / R, &b, &e, &ng, &sz);
-  }
-  if (gi >= ng) return;
-  const int32_t gb = b + gi * sz, ge = min(e, gb + sz);
+  const int32_t gb = gi * rank_gs(cls), ge = min(cnt, gb + rank_gs(cls));
   const int32_t n = (ge - gb) * R;
   int64_t base = 0;
   if (one) {
@@ -1409,6 +970,57 @@ __global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
   }
 }
 
+
+// Each ranked list is cut into fixed groups of gs = 127 / rows pods: group g holds list
+// positions [g gs, min(cnt, (g + 1) gs)).  A one-selection chunk of the fit kernel is one group
+// (the grid covers ceil(P / 127) chunks); a multi-selection chunk takes ceil(G / chunks) whole
+// groups of each list (G groups), so every block ranks its nodes once per full group.
+__device__ __forceinline__ void chunk_groups(int32_t cnt, int32_t chunks, int32_t chunk,
+                                             int32_t gs, int32_t* g0, int32_t* g1) {
+  const int32_t G = (cnt + gs - 1) / gs;
+  const int32_t gpc = (G + chunks - 1) / chunks;
+  *g0 = min(G, chunk * gpc);
+  *g1 = min(G, *g0 + gpc);
+}
+
+// One block per non-empty group (a persistent loop over the groups of every list slot), a
+// thread per (item, kind).  Slots: [0, NL) the one-selection lists; NL + 2 l + c list l's
+// two- (c = 0) and three-selection (c = 1) pods.  A group's items are its pods' rows
+// (pod-major).  Per compared kind: an item's rank = #{items below it} (+ #{equal items before
+// it} for its sorted position), written as the sorted row (srt_*[item][kind j]) and as the
+// item's rank in its pod's record.  Items of a slot sit after those of the slots before it,
+// so a group's sorted rows are contiguous.
+constexpr int kRankPrepTpb = kRankItems * PAS_GAS_MAX_RES;
+constexpr int kRankPrepBlocks = 1024;
+__global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
+    int32_t P, int32_t Q, const int32_t* __restrict__ counts,
+    const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
+    const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
+    GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti,
+    int32_t* __restrict__ rword) {
+  __shared__ int64_t v[PAS_GAS_MAX_RES][kRankItems];
+  __shared__ uint32_t pks[kRankItems];
+  const int32_t NL = Q + 1, slots = NL * 3;
+  auto slot_count = [&](int32_t slot) {
+    return slot < NL ? counts[slot]
+                     : counts[NL + ((slot - NL) >> 1) * kClasses + ((slot - NL) & 1)];
+  };
+  for (int32_t w = blockIdx.x;; w += gridDim.x) {
+    // the group: w-th over the slots' groups in slot order
+    int32_t slot = 0, gi = w;
+    for (; slot < slots; ++slot) {
+      const int32_t G = (slot_count(slot) + rank_gs(slot < NL ? 0 : 1 + ((slot - NL) & 1)) - 1) /
+                        rank_gs(slot < NL ? 0 : 1 + ((slot - NL) & 1));
+      if (gi < G) break;
+      gi -= G;
+    }
+    if (slot >= slots) return;
+    __syncthreads();  // the previous group's reads of v / pks are done
+    rank_group(P, Q, counts, slot, gi, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword,
+               v, pks);
+  }
+}
+
 // The group's sorted rows of the C compared kinds into the wave's LDS slice [C][128]
 // (positions past the group's items: INT64_MAX).
 template <int C>
@@ -1432,24 +1044,57 @@ __device__ __forceinline__ void load_sorted(const int64_t* __restrict__ srt, int
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
+// Four upper-bound levels at once: pos[k] = 2 pos[k] + (x[k] <= f[k]).  The compares go first
+// (each writes a lane mask), then the adds with the masks as carry-in, each mask read three
+// instructions after its compare (the VALU SGPR-write -> mask-read hazard needs two).
+__device__ __forceinline__ void rank_level4(uint32_t& p0, uint32_t& p1, uint32_t& p2, uint32_t& p3,
+                                            int64_t x0, int64_t x1, int64_t x2, int64_t x3,
+                                            int64_t f0, int64_t f1, int64_t f2, int64_t f3) {
+  uint64_t m0, m1, m2, m3, co;
+  asm("v_cmp_le_i64_e64 %[m0], %[x0], %[f0]\n\t"
+      "v_cmp_le_i64_e64 %[m1], %[x1], %[f1]\n\t"
+      "v_cmp_le_i64_e64 %[m2], %[x2], %[f2]\n\t"
+      "v_cmp_le_i64_e64 %[m3], %[x3], %[f3]\n\t"
+      "v_addc_co_u32_e64 %[p0], %[co], %[p0], %[p0], %[m0]\n\t"
+      "v_addc_co_u32_e64 %[p1], %[co], %[p1], %[p1], %[m1]\n\t"
+      "v_addc_co_u32_e64 %[p2], %[co], %[p2], %[p2], %[m2]\n\t"
+      "v_addc_co_u32_e64 %[p3], %[co], %[p3], %[p3], %[m3]"
+      : [p0] "+v"(p0), [p1] "+v"(p1), [p2] "+v"(p2), [p3] "+v"(p3), [m0] "=&s"(m0),
+        [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [co] "=&s"(co)
+      : [x0] "v"(x0), [x1] "v"(x1), [x2] "v"(x2), [x3] "v"(x3), [f0] "v"(f0), [f1] "v"(f1),
+        [f2] "v"(f2), [f3] "v"(f3));
+}
+
 // The node's cards ranked against the group: fa[j] = bytes rank + 0x80 of cards 0, 2, 4, 6
-// (kind j), fb[j] of cards 1, 3, 5, 7.  rank = #{group thresholds <= free} (upper bound in
-// the sorted row; at most n, the padding is INT64_MAX).
+// (kind j), fb[j] of cards 1, 3, 5, 7.  rank = #{group thresholds <= free}, the upper bound in
+// the sorted row found bit by bit: level L probes entry (pos << (7 - L)) + 2^(6 - L) - 1 and
+// appends the outcome (an address, a compare and an add-with-carry per level; entry 127 is
+// padding and never probed; at most n, the padding is INT64_MAX).  The 8 cards of a kind
+// go level by level together (8 LDS reads in flight).
 template <int Q, int SKIP, int C>
 __device__ __forceinline__ void rank_cards(const int64_t (&free)[kMaxCards][Q], const int64_t* lds,
                                            int32_t n, uint32_t (&fa)[C], uint32_t (&fb)[C]) {
 #pragma unroll
   for (int q = 0, j = 0; q < Q; ++q) {
     if (q == SKIP) continue;
+    uint32_t pos[kMaxCards];
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k) pos[k] = 0u;
+    const int64_t* row = lds + j * kRankItems;
+#pragma unroll
+    for (int sh = 6; sh >= 0; --sh) {
+      int64_t x[kMaxCards];
+#pragma unroll
+      for (int k = 0; k < kMaxCards; ++k) x[k] = row[(pos[k] << (sh + 1)) + (1 << sh) - 1];
+      rank_level4(pos[0], pos[1], pos[2], pos[3], x[0], x[1], x[2], x[3], free[0][q], free[1][q],
+                  free[2][q], free[3][q]);
+      rank_level4(pos[4], pos[5], pos[6], pos[7], x[4], x[5], x[6], x[7], free[4][q], free[5][q],
+                  free[6][q], free[7][q]);
+    }
     uint32_t a = 0u, b = 0u;
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) {
-      const int64_t f = free[k][q];
-      int32_t pos = 0;
-#pragma unroll
-      for (int s = kRankItems / 2; s >= 1; s >>= 1)
-        pos = lds[j * kRankItems + pos + s - 1] <= f ? pos + s : pos;
-      const uint32_t r = (uint32_t)min(pos, n) + 0x80u;
+      const uint32_t r = min(pos[k], (uint32_t)n) + 0x80u;
       if (k & 1) b |= r << (8 * (k >> 1));
       else a |= r << (8 * (k >> 1));
     }
@@ -1481,17 +1126,17 @@ __device__ __forceinline__ void rsingle_list(const int64_t (&free)[kMaxCards][Q]
                                              const GasRSingle* __restrict__ rs,
                                              const int64_t* __restrict__ srt, int64_t item0,
                                              int32_t cnt, const BlockTile& bt, int64_t* lds,
-                                             GasRSingle* stage, uint32_t* __restrict__ res,
+                                             GasRSingle* stage, ResOut res,
                                              uint64_t* __restrict__ fit) {
   constexpr int kSkip = Q == 1 ? -1 : SKIP;
   constexpr int C = Q - (kSkip >= 0 ? 1 : 0);
   const int lane = threadIdx.x & 63;
-  int32_t gb, ge, ng, sz;
-  single_chunk(cnt, bt.chunk, &gb, &ge, &ng, &sz);
-  if (!ng) return;
-  load_sorted<C>(srt, item0 + gb, sz, lds, lane);
+  // this chunk's group (one-selection lists: chunk = group)
+  const int32_t gb = min(cnt, bt.chunk * kRankMax), ge = min(cnt, gb + kRankMax);
+  if (gb >= ge) return;
+  load_sorted<C>(srt, item0 + gb, ge - gb, lds, lane);
   uint32_t fa[C], fb[C];
-  rank_cards<Q, kSkip, C>(free, lds, sz, fa, fb);
+  rank_cards<Q, kSkip, C>(free, lds, ge - gb, fa, fb);
   auto one_pod = [&](const GasRSingle& r, int32_t w) {
     const int64_t pod = w & 0xFFFFFF;
     uint32_t out = node_ok;
@@ -1540,7 +1185,7 @@ __device__ __forceinline__ void rsingle_lists(const int64_t (&free)[kMaxCards][Q
                                               const int64_t* __restrict__ srt, int64_t item0,
                                               const int32_t* __restrict__ counts,
                                               const BlockTile& bt, int64_t* lds,
-                                              GasRSingle* stage, uint32_t* __restrict__ res,
+                                              GasRSingle* stage, ResOut res,
                                               uint64_t* __restrict__ fit) {
   const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[L]);
   rsingle_list<Q, L - 1, kBits>(free, node_ok, N, n, valid, rs + (int64_t)L * P, srt, item0, cnt,
@@ -1554,7 +1199,7 @@ template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs, const int64_t* __restrict__ srt,
-    const int32_t* __restrict__ counts, int32_t chunks, uint32_t* __restrict__ res,
+    const int32_t* __restrict__ counts, int32_t chunks, ResOut res,
     uint64_t* __restrict__ fit) {
   __shared__ int64_t lds[kTpb / 64][Q * kRankItems];   // sorted rows per wave
   __shared__ GasRSingle stage[kTpb / 64][kPodBatch];  // a slice per wave
@@ -1632,16 +1277,17 @@ __device__ __forceinline__ void rmulti_list(const int64_t (&free)[kMaxCards][Q],
                                             const int64_t* __restrict__ srt, int64_t item0,
                                             int32_t cnt, const BlockTile& bt, int64_t* lds,
                                             GasRMulti* stage, uint32_t* tab,
-                                            uint32_t* __restrict__ res,
+                                            ResOut res,
                                             uint64_t* __restrict__ fit) {
   constexpr int kSkip = Q == 1 ? -1 : SKIP;
   constexpr int C = Q - (kSkip >= 0 ? 1 : 0);
   constexpr int R = S == 2 ? 3 : 7;
   const int lane = threadIdx.x & 63;
-  int32_t b, e, ng, sz;
-  chunk_groups(cnt, bt.chunks, bt.chunk, kRankMax / R, &b, &e, &ng, &sz);
-  for (int32_t gi = 0; gi < ng; ++gi) {
-    const int32_t gb = b + gi * sz, ge = min(e, gb + sz);
+  constexpr int32_t gs = kRankMax / R;
+  int32_t g0, g1;
+  chunk_groups(cnt, bt.chunks, bt.chunk, gs, &g0, &g1);
+  for (int32_t gi = g0; gi < g1; ++gi) {
+    const int32_t gb = gi * gs, ge = min(cnt, gb + gs);
     load_sorted<C>(srt, item0 + (int64_t)gb * R, (ge - gb) * R, lds, lane);
     uint32_t fa[C], fb[C];
     rank_cards<Q, kSkip, C>(free, lds, (ge - gb) * R, fa, fb);
@@ -1688,7 +1334,7 @@ __device__ __forceinline__ void rmulti_lists(const int64_t (&free)[kMaxCards][Q]
                                              const int64_t* __restrict__ srt, int64_t item0,
                                              const int32_t* __restrict__ counts,
                                              const BlockTile& bt, int64_t* lds, GasRMulti* stage,
-                                             uint32_t* tab, uint32_t* __restrict__ res,
+                                             uint32_t* tab, ResOut res,
                                              uint64_t* __restrict__ fit) {
   // slot L: list L / 2, class L % 2 (S = 2 + L % 2); counts of the multi lists [l][kClasses]
   constexpr int l = L / 2, S = 2 + L % 2;
@@ -1721,7 +1367,7 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm, const int32_t* __restrict__ rw,
     const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
-    uint32_t* __restrict__ res, uint64_t* __restrict__ fit) {
+    ResOut res, uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kBytes / 16];
   const BlockTile bt = block_tile(chunks);
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
@@ -1740,8 +1386,8 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
   __builtin_amdgcn_wave_barrier();
   GasSel* sstage = reinterpret_cast<GasSel*>(w);
   int64_t* stab = reinterpret_cast<int64_t*>(sstage + kPacked * kMB);
-  multi_lists<Q, kBits, true>(free, sstage, stab, node_ok, N, n, valid, P, multi, sels, counts, bt,
-                              res, fit);
+  seq_lists<Q, kBits>(free, sstage, stab, node_ok, N, n, valid, P, multi, sels, counts, bt, res,
+                      fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -1771,6 +1417,7 @@ struct GenericArgs {
   const int32_t* pod_steps;
   int32_t n_pods;
   uint32_t* res;
+  int64_t ld;  // result row pitch
   uint64_t* fit;
   pas_gas_selection* side;
   int64_t side_cap;
@@ -1863,7 +1510,7 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
                    (n >> 6),
                1ull << (n & 63));
   } else {
-    a.res[(int64_t)p * a.N + n] = word;
+    a.res[(int64_t)p * a.ld + n] = word;
   }
 }
 
@@ -1893,7 +1540,7 @@ __global__ __launch_bounds__(64) void gas_fit_generic_kernel(GenericArgs a) {
 
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
-                   const int32_t* d_n_containers, uint32_t* d_res, uint64_t* d_fit,
+                   const int32_t* d_n_containers, uint32_t* d_res, int64_t ld_res, uint64_t* d_fit,
                    pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
                    hipStream_t s) {
   const GasSnapshot& g = ctx->gas;
@@ -1983,17 +1630,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const int32_t nb_s = (N + kTpb - 1) / kTpb;
   const int32_t ch_s = (n_pods + kRankMax - 1) / kRankMax;  // fixed one-group chunks
   const int32_t ch_m = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_s - 1) / nb_s));
-  {
-    // one wave per (slot, chunk, group): groups per chunk <= ceil(ceil(P / chunks) / gs)
-    auto groups = [&](int32_t ch, int32_t gs) {
-      const int32_t per = (n_pods + ch - 1) / ch;
-      return (per + gs - 1) / gs;
-    };
-    const int32_t maxg = std::max(groups(ch_m, kRankMax / 3), groups(ch_m, kRankMax / 7));
-    const dim3 grid((unsigned)(std::max(ch_s, ch_m) * maxg), (unsigned)(NL * 3));
-    gas_rank_prep_kernel<<<grid, kRankPrepTpb, 0, s>>>(n_pods, Q, counts, ch_s, ch_m, maxg, single, multi,
-                                             sels, srt_s, srt_m, rsingle, rmulti, rword);
-  }
+  gas_rank_prep_kernel<<<kRankPrepBlocks, kRankPrepTpb, 0, s>>>(
+      n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
@@ -2002,10 +1640,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
     gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                \
-        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, ch_s, d_res, d_fit);        \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, ch_s, ResOut{d_res, ld_res}, d_fit);        \
     gas_rfit_multi_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                 \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m, multi, sels, counts + NL,      \
-        ch_m, d_res, d_fit);                                                                   \
+        ch_m, ResOut{d_res, ld_res}, d_fit);                                                                   \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
@@ -2033,6 +1671,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   ga.pod_steps = pod_steps;
   ga.n_pods = n_pods;
   ga.res = d_res;
+  ga.ld = ld_res;
   ga.fit = d_fit;
   ga.side = d_side;
   ga.side_cap = d_side ? side_cap : 0;

@@ -920,7 +920,7 @@ static int gas_fit_host(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_
     PAS_HIP(ctx, hipMemcpyAsync(d_mask, req_mask, b_mask, hipMemcpyHostToDevice, s));
   }
   PAS_HIP(ctx, hipMemcpyAsync(d_nc, n_containers, b_nc, hipMemcpyHostToDevice, s));
-  rc = gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_mask, d_nc, d_res,
+  rc = gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_mask, d_nc, d_res, N,
                       nullptr, side_cap > 0 ? d_side : nullptr, side_cap,
                       side_count ? d_count : nullptr, s);
   if (rc) return rc;
@@ -960,21 +960,24 @@ static int gas_fit_device_common(pas_ctx* ctx, uint64_t gen, int32_t n_pods,
                                  int32_t max_containers, int32_t i915_index,
                                  const int64_t* d_req, const uint32_t* d_req_mask,
                                  const int32_t* d_n_containers, uint32_t* d_res_out,
-                                 uint64_t* d_fit_out, pas_gas_selection* d_side, int64_t side_cap,
-                                 int64_t* d_side_count, void* hip_stream, const char* fn) {
+                                 int64_t ld_res, uint64_t* d_fit_out, pas_gas_selection* d_side,
+                                 int64_t side_cap, int64_t* d_side_count, void* hip_stream,
+                                 const char* fn) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_gas_gen(ctx, gen);
   if (rc) return rc;
+  if (ld_res < 0) ld_res = ctx->gas.n_nodes;  // dense rows
   if (n_pods < 0 || max_containers < 0 || i915_index >= ctx->gas.n_res || i915_index < -1 ||
-      side_cap < 0)
+      side_cap < 0 || ld_res < ctx->gas.n_nodes)
     return set_error(ctx, PAS_EINVAL, std::string(fn) + ": bad shape");
   if (n_pods > 0 && (!d_n_containers || (!d_res_out && !d_fit_out) ||
                      (max_containers > 0 && (!d_req || !d_req_mask)) || (side_cap > 0 && !d_side)))
     return set_error(ctx, PAS_EINVAL, std::string(fn) + ": null input");
   if ((rc = activate(ctx))) return rc;
   return gas_fit_launch(ctx, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                        d_n_containers, d_res_out, d_fit_out, side_cap > 0 ? d_side : nullptr,
-                        side_cap, d_side_count, pick_stream(ctx, hip_stream));
+                        d_n_containers, d_res_out, ld_res, d_fit_out,
+                        side_cap > 0 ? d_side : nullptr, side_cap, d_side_count,
+                        pick_stream(ctx, hip_stream));
 }
 
 int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
@@ -983,7 +986,7 @@ int pas_gas_fit_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_c
   if (ctx && !d_res_out && n_pods > 0)
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_device: null input");
   return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                               d_n_containers, d_res_out, nullptr, nullptr, 0, nullptr,
+                               d_n_containers, d_res_out, -1, nullptr, nullptr, 0, nullptr,
                                hip_stream, "pas_gas_fit_device");
 }
 
@@ -995,8 +998,21 @@ int pas_gas_fit_ex_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t ma
   if (ctx && ((!d_res_out && n_pods > 0) || !d_side_count))
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_ex_device: null input");
   return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                               d_n_containers, d_res_out, nullptr, d_side, side_cap,
+                               d_n_containers, d_res_out, -1, nullptr, d_side, side_cap,
                                d_side_count, hip_stream, "pas_gas_fit_ex_device");
+}
+
+int pas_gas_fit_ld_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
+                          int32_t i915_index, const int64_t* d_req, const uint32_t* d_req_mask,
+                          const int32_t* d_n_containers, uint32_t* d_res_out, int64_t ld_res,
+                          pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
+                          void* hip_stream) {
+  if (ctx && !d_res_out && n_pods > 0)
+    return set_error(ctx, PAS_EINVAL, "pas_gas_fit_ld_device: null input");
+  if (ctx && ld_res < 0) return set_error(ctx, PAS_EINVAL, "pas_gas_fit_ld_device: ld_res < 0");
+  return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
+                               d_n_containers, d_res_out, ld_res, nullptr, d_side, side_cap,
+                               d_side_count, hip_stream, "pas_gas_fit_ld_device");
 }
 
 int pas_gas_limit_count(pas_ctx* ctx, int64_t* n_pods_out) {
@@ -1023,7 +1039,7 @@ int pas_gas_fit_bitmap_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_
   if (n_pods > 0 && !d_fit_out)
     return set_error(ctx, PAS_EINVAL, "pas_gas_fit_bitmap_device: null input");
   return gas_fit_device_common(ctx, gen, n_pods, max_containers, i915_index, d_req, d_req_mask,
-                               d_n_containers, nullptr, d_fit_out, nullptr, 0, nullptr,
+                               d_n_containers, nullptr, -1, d_fit_out, nullptr, 0, nullptr,
                                hip_stream, "pas_gas_fit_bitmap_device");
 }
 

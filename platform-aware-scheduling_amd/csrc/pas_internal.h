@@ -170,9 +170,9 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
                           const int32_t* d_rule_off, uint64_t* d_viol, hipStream_t s);
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
-                   const int32_t* d_n_containers, uint32_t* d_res, uint64_t* d_fit,
-                   pas_gas_selection* d_side, int64_t side_cap, int64_t* d_side_count,
-                   hipStream_t s);
+                   const int32_t* d_n_containers, uint32_t* d_res, int64_t ld_res,
+                   uint64_t* d_fit, pas_gas_selection* d_side, int64_t side_cap,
+                   int64_t* d_side_count, hipStream_t s);
 int tas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rule* d_rules,
                     const int32_t* d_rule_off, const pas_rule* d_prio, const uint64_t* d_cand,
                     int32_t k, int32_t node_base, int64_t* d_key, int32_t* d_node,

@@ -156,6 +156,10 @@ SIGNATURES = {
         c_int,
         [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, _P, c_int64, _P, _P],
     ),
+    "pas_gas_fit_ld_device": (
+        c_int,
+        [_P, c_uint64, c_int32, c_int32, c_int32, _P, _P, _P, _P, c_int64, _P, c_int64, _P, _P],
+    ),
     "pas_gas_limit_count": (c_int, [_P, POINTER(c_int64)]),
     "pas_gas_fit_bitmap_device": (
         c_int,

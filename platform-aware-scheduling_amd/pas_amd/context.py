@@ -463,6 +463,19 @@ class Context:
                                         _dptr(res_t), _stream(stream))
         self._check(rc, "pas_gas_fit_device")
 
+    def gas_fit_ld_device(self, gen: int, n_pods: int, max_containers: int, i915_index: int,
+                          req_t, mask_t, ncont_t, res_t, ld_res: int, side_t=None,
+                          side_cap: int = 0, count_t=None, stream=None):
+        """pas_gas_fit_ld_device: words of (pod p, node n) at res_t.view(-1)[p * ld_res + n]."""
+        rc = self._l.pas_gas_fit_ld_device(self._h, gen, n_pods, max_containers, i915_index,
+                                           _dptr(req_t), _dptr(mask_t), _dptr(ncont_t),
+                                           _dptr(res_t), ld_res,
+                                           _dptr(side_t) if side_t is not None else None,
+                                           side_cap,
+                                           _dptr(count_t) if count_t is not None else None,
+                                           _stream(stream))
+        self._check(rc, "pas_gas_fit_ld_device")
+
     def gas_fit_bitmap_device(self, gen: int, n_pods: int, max_containers: int, i915_index: int,
                               req_t, mask_t, ncont_t, fit_t, stream=None):
         """GAS fit verdicts as node bitmaps fit_t[n_pods][W64] (pas_gas_fit_bitmap_device)."""

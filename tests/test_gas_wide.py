@@ -205,3 +205,48 @@ def test_selection_sum_past_int64(ctx, oracle):
     np.testing.assert_array_equal(ctx.gas_fit(gen, req, mask, two, 0), want)
     res, st = ctx.gas_bind(gen, gen + 1, [0], [0], req, mask, two, 0)
     assert res[0] == 0 and st[0] == _lib.PAS_GAS_WONT_FIT
+
+
+@pytest.mark.parametrize("extra", [0, 7, 48])
+def test_result_row_pitch(ctx, oracle, extra):
+    # pas_gas_fit_ld_device: rows at a pitch ld >= N (here N + extra, and N rounded up to 32
+    # words) hold the dense words; the padding is not written.  Wide nodes (generic kernel),
+    # pods past 8 selections (generic) and the ranked fast kernels all honour the pitch.
+    rng = np.random.default_rng(11 + extra)
+    n_cards, cap, used, req, mask, ncont = random_wide(rng, 1000, 12, 3, 200, 3, 12)
+    want, w_sel, _ = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0, selections=True)
+    gen = _upload(ctx, n_cards, cap, used)
+    dev = torch.device("cuda", 0)
+    p, c, q = req.shape
+    n = len(n_cards)
+    ld = n + extra if extra else (n + 31) // 32 * 32 + 32
+    req_t = torch.from_numpy(req).to(dev)
+    mask_t = torch.from_numpy(mask.view(np.int32)).to(dev)
+    ncont_t = torch.from_numpy(ncont).to(dev)
+    res_t = torch.full((p, ld), -0x21524111, dtype=torch.int32, device=dev)  # 0xDEADBEEF
+    cap_side = 1 << 16
+    side_t = torch.zeros((cap_side, _lib.GAS_SELECTION_DTYPE.itemsize), dtype=torch.uint8,
+                         device=dev)
+    count_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream()
+    ctx.gas_fit_ld_device(gen, p, c, 0, req_t, mask_t, ncont_t, res_t, ld, side_t, cap_side,
+                          count_t, stream)
+    torch.cuda.synchronize()
+    got = res_t.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[:, :n], want)
+    assert (got[:, n:] == 0xDEADBEEF).all()
+    ext = np.argwhere((want >> 24) & 15 == oracle.SEL_EXTENDED)
+    count = int(count_t.item())
+    assert count == len(ext)
+    side = side_t[:count].cpu().numpy().view(_lib.GAS_SELECTION_DTYPE).reshape(-1)
+    side = side[np.lexsort((side["node"], side["pod"]))]
+    np.testing.assert_array_equal(side["card"], w_sel[ext[:, 0], ext[:, 1]])
+    # no side buffer
+    res_t.fill_(-0x21524111)
+    ctx.gas_fit_ld_device(gen, p, c, 0, req_t, mask_t, ncont_t, res_t, ld, stream=stream)
+    torch.cuda.synchronize()
+    got = res_t.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[:, :n], want)
+    assert (got[:, n:] == 0xDEADBEEF).all()
+    with pytest.raises(pas_amd.PasError):
+        ctx.gas_fit_ld_device(gen, p, c, 0, req_t, mask_t, ncont_t, res_t, n - 1, stream=stream)
