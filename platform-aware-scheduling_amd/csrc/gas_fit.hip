@@ -16,22 +16,25 @@
 // means need > INT64_MAX - used >= free.  Taking a card (addRM) is free -= need.  A
 // negative need on a requested kind fails every card (:343-347).
 //
-// The pod loop is wave-uniform: pod records sit in SGPRs, so each card check is one 64-bit
-// compare against an SGPR.  The prep kernel splits the batch: pods with at most one card
-// selection (the common case: one container, one i915) go to a kernel that only reads free;
-// pods with several selections go to a kernel that takes cards in a working copy
-// (per-card lane-masked updates), so the first kernel keeps a small register footprint.
+// The pod loop is wave-uniform (a lane per node, the pod's values broadcast).  The prep
+// kernel files each pod under a list by selection count: one selection (the common case), two,
+// three, four to eight (more: the generic kernel), and by the kind it may skip (below).
+// Launches per fit: gas_prep_kernel (lists), gas_rank_prep_kernel (rank groups, below),
+// gas_rfit_single_kernel (one-selection pods), gas_rfit_multi_kernel (several selections:
+// two and three in closed form, four to eight in order), gas_fit_generic_kernel (shapes past
+// 8 cards or 8 selections).
+//
+// Rank compression (the ranked fit section): every "need <= free" compare of a group of at
+// most 127 thresholds becomes a compare of 7-bit ranks, four cards of one kind per 32-bit
+// subtraction, exactly.
 //
 // Kind skipping (exact, decided per pod before the fit kernels): gmin[q] = the minimum of
 // free[k][q] over every card of every labelled node of the snapshot (gas_minfree_kernel).
-// When a single-selection pod's need of kind q is <= gmin[q], no check of kind q can fail
-// anywhere, so its compares are dropped: the prep kernel files the pod under list 1 + q (the
-// lowest such kind) or list 0, and the single kernel instantiates one body per list, so the
-// skip costs nothing per (pod, node).  The last kind the selection requests stays compared,
-// so cards a node does not have (free -1 everywhere) still fail.  In the C3 mix the i915
-// kind (1 per selection against >= 30 free) goes: single kernel 502 -> 381 us.  The same
-// for multi-selection pods (bound = need plus the takes before it) measured 1587 -> 1609 us,
-// so that kernel keeps every kind: it is not bound by its compares.
+// When a pod's total take of kind q is <= gmin[q], no check of kind q can fail anywhere, so
+// its compares are dropped: the prep kernel files the pod under list 1 + q (the lowest such
+// kind) or list 0, and the fit kernels instantiate one body per list.  The last kind a
+// selection requests stays compared, so cards a node does not have (free -1) still fail.  In
+// the C3 mix the i915 kind (1 per selection against >= 30 free) goes.
 #include <hip/hip_runtime.h>
 
 #include "gas_runs.h"
@@ -114,6 +117,14 @@ __device__ __forceinline__ ContainerReq load_container(int64_t i, int32_t n_res,
   return c;
 }
 
+// v / ni truncated toward zero (Go's int64 division), ni > 1: 32-bit unsigned division when
+// both fit (the common case), else the 64-bit one.
+__device__ __forceinline__ int64_t per_gpu(int64_t v, int64_t ni) {
+  if (v >= 0 && v <= (int64_t)UINT32_MAX && ni <= (int64_t)UINT32_MAX)
+    return (int64_t)((uint32_t)v / (uint32_t)ni);
+  return v / ni;
+}
+
 __device__ GasStep container_step(const ContainerReq& cr, int32_t n_res, int32_t i915) {
   const uint32_t m = cr.m;
   const int64_t(&rv)[PAS_GAS_MAX_RES] = cr.rv;
@@ -129,7 +140,7 @@ __device__ GasStep container_step(const ContainerReq& cr, int32_t n_res, int32_t
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
     const bool has = q < n_res && ((m >> q) & 1u);
     int64_t v = has ? rv[q] : 0;
-    if (ni > 1) v /= ni;
+    if (ni > 1) v = per_gpu(v, ni);
     if (has && v < 0) g.bad = 1;
     g.take[q] = v;
     g.cmp[q] = has ? v : INT64_MIN;
@@ -142,14 +153,14 @@ __device__ GasStep container_step(const ContainerReq& cr, int32_t n_res, int32_t
 // holds), else 0.  The last kind the selection requests is kept: cards a node does not have
 // read free = -1 and must keep failing.  A bad selection fails in any list.
 __device__ __forceinline__ int32_t skip_list(int32_t n_res, const int64_t (&cmp)[PAS_GAS_MAX_RES],
-                                             uint32_t kinds,
-                                             const unsigned long long* __restrict__ gflip) {
-  for (int q = 0; q < n_res; ++q) {
-    if (!((kinds >> q) & 1u) || kinds == (1u << q)) continue;
-    const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
-    if (cmp[q] <= gmin) return 1 + q;
+                                             uint32_t kinds, const int64_t (&gmin)[PAS_GAS_MAX_RES]) {
+  int32_t l = 0;
+#pragma unroll
+  for (int q = PAS_GAS_MAX_RES - 1; q >= 0; --q) {  // the lowest such kind wins
+    if (q >= n_res || !((kinds >> q) & 1u) || kinds == (1u << q)) continue;
+    if (cmp[q] <= gmin[q]) l = 1 + q;
   }
-  return 0;
+  return l;
 }
 
 // A slot in list `list` for each active lane: one atomic per distinct list in the wave (lanes
@@ -189,7 +200,7 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
 // and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
 // go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
 // PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
-__global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
+__global__ __launch_bounds__(kPrepTpb) void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
                                 int32_t i915, const int64_t* __restrict__ req,
                                 const uint32_t* __restrict__ mask,
                                 const int32_t* __restrict__ n_containers,
@@ -210,21 +221,30 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
 #pragma unroll
     for (int c = 0; c < kPre; ++c) pre[c] = load_container(row + min(c, nc - 1), n_res, req, mask);
   }
-  auto container = [&](int32_t c) {
-    ContainerReq cr = pre[0];
+  // their steps, once; both passes below run unrolled over them (a runtime container index
+  // into these arrays would put them in scratch memory), then over containers past them
+  GasStep pst[kPre];
 #pragma unroll
-    for (int k = 1; k < kPre; ++k) cr = c == k ? pre[k] : cr;
-    if (c >= kPre) cr = load_container(row + c, n_res, req, mask);
-    return container_step(cr, n_res, i915);
+  for (int c = 0; c < kPre; ++c) pst[c] = container_step(pre[c], n_res, i915);
+  auto each_container = [&](auto&& fn) {
+#pragma unroll
+    for (int c = 0; c < kPre; ++c)
+      if (c < nc) fn(pst[c]);
+    for (int32_t c = kPre; c < nc; ++c)
+      fn(container_step(load_container(row + c, n_res, req, mask), n_res, i915));
   };
+  // the kind minima (kept flipped in gflip, gas_minfree_kernel)
+  int64_t gmin[PAS_GAS_MAX_RES];
+#pragma unroll
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q)
+    gmin[q] = q < n_res ? (int64_t)((unsigned long long)INT64_MAX - gflip[q]) : INT64_MAX;
   int32_t steps = 0;
   uint32_t kinds = 0;
   uint32_t skip_ok = (1u << n_res) - 1u, skip_req = 0;  // multi_skip_list
   int64_t cum[PAS_GAS_MAX_RES] = {};                     // the pod's total take per kind
   GasSingle one = {};
   int32_t one_bad = 0;
-  for (int32_t c = 0; c < nc; ++c) {
-    const GasStep g = container(c);
+  each_container([&](const GasStep& g) {
     if (g.num_i915 > 0) {
       if (steps == 0) {
 #pragma unroll
@@ -235,23 +255,24 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
       steps = min(steps + g.num_i915, PAS_GAS_MAX_SELECTIONS + 1);
       const uint32_t gk = (uint32_t)g.kinds;
       skip_req |= gk;
-      for (int q = 0; q < n_res; ++q) {
-        if (!((gk >> q) & 1u)) continue;
-        // saturating: a total past INT64_MAX only has to exceed every gmin
+#pragma unroll
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+        if (q >= n_res || !((gk >> q) & 1u)) continue;
+        // num_i915 takes, saturating: a total past INT64_MAX only has to exceed every gmin
         const int64_t add = g.take[q] > 0 ? g.take[q] : 0;
-        for (int32_t r = 0; r < g.num_i915; ++r)
-          cum[q] = cum[q] > INT64_MAX - add ? INT64_MAX : cum[q] + add;
+        int64_t prod;
+        const bool ovf = __builtin_mul_overflow(add, (int64_t)g.num_i915, &prod);
+        cum[q] = (ovf || prod > INT64_MAX - cum[q]) ? INT64_MAX : cum[q] + prod;
         if (gk == (1u << q)) skip_ok &= ~(1u << q);
       }
     }
-  }
-  for (int q = 0; q < n_res; ++q) {
-    const int64_t gmin = (int64_t)((unsigned long long)INT64_MAX - gflip[q]);
-    if (cum[q] > gmin) skip_ok &= ~(1u << q);
-  }
+  });
+#pragma unroll
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q)
+    if (q < n_res && cum[q] > gmin[q]) skip_ok &= ~(1u << q);
   pod_steps[p] = steps;
   const bool one_sel = steps <= 1;
-  const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gflip) : 0)
+  const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gmin) : 0)
                             : multi_skip_list(n_res, skip_ok, skip_req);
   const int32_t nl = n_res + 1;
   const int32_t ml = l * kClasses + (steps == 2 ? 0 : steps == 3 ? 1 : 2);  // multi list
@@ -275,22 +296,20 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
   int64_t take0[PAS_GAS_MAX_RES], take1[PAS_GAS_MAX_RES];
 #pragma unroll
   for (int q = 0; q < PAS_GAS_MAX_RES; ++q) cmp0[q] = cmp1[q] = cmp2[q] = take0[q] = take1[q] = 0;
-  for (int32_t c = 0; c < nc; ++c) {
-    const GasStep g = container(c);
+  each_container([&](const GasStep& g) {
     bad |= g.num_i915 > 0 ? g.bad : 0;
-    for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
+    // selections k .. k + num_i915 - 1 all carry this container's step
+    const bool s0 = k <= 0 && 0 < k + g.num_i915, s1 = k <= 1 && 1 < k + g.num_i915;
+    const bool s2 = k <= 2 && 2 < k + g.num_i915;
 #pragma unroll
-      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
-        if (k == 0) {
-          cmp0[q] = g.cmp[q];
-          take0[q] = g.take[q];
-        } else if (k == 1) {
-          cmp1[q] = g.cmp[q];
-          take1[q] = g.take[q];
-        } else if (k == 2) {
-          cmp2[q] = g.cmp[q];
-        }
-      }
+    for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+      cmp0[q] = s0 ? g.cmp[q] : cmp0[q];
+      take0[q] = s0 ? g.take[q] : take0[q];
+      cmp1[q] = s1 ? g.cmp[q] : cmp1[q];
+      take1[q] = s1 ? g.take[q] : take1[q];
+      cmp2[q] = s2 ? g.cmp[q] : cmp2[q];
+    }
+    for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
       GasSel e = {};
 #pragma unroll
       for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
@@ -299,53 +318,62 @@ __global__ void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t 
       }
       out[k] = e;
     }
-  }
+  });
   if (steps <= 3) {
     // thresholds: need plus the takes of a subset of the earlier selections (cards taken
     // from by exactly those selections); unrequested kinds stay INT64_MIN
     //   row 0: c0   1: c1   2: c1 + t0   3: c2   4: c2 + t0   5: c2 + t1   6: c2 + t0 + t1
-    GasThresholds t = {};
-    auto add = [](int64_t v, int64_t d, bool* o) {
+    // written straight to the row (a local GasThresholds would live in scratch memory)
+    GasThresholds* t = reinterpret_cast<GasThresholds*>(out + kThRow);
+    auto add = [](int64_t v, int64_t d, bool& o) {
       int64_t r;
-      if (__builtin_add_overflow(v, d, &r)) *o = true;
+      const bool f = __builtin_add_overflow(v, d, &r);
+      o = o || f;
       return r;
     };
+    int32_t over = 0;
+    int64_t th[7][PAS_GAS_MAX_RES];
 #pragma unroll
     for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
       bool o2 = false, o4 = false, o5 = false, o6 = false;
-      t.th[0][q] = cmp0[q];
-      t.th[1][q] = cmp1[q];
-      t.th[2][q] = cmp1[q] == INT64_MIN ? cmp1[q] : add(cmp1[q], take0[q], &o2);
-      t.th[3][q] = cmp2[q];
-      t.th[4][q] = cmp2[q] == INT64_MIN ? cmp2[q] : add(cmp2[q], take0[q], &o4);
-      t.th[5][q] = cmp2[q] == INT64_MIN ? cmp2[q] : add(cmp2[q], take1[q], &o5);
+      th[0][q] = cmp0[q];
+      th[1][q] = cmp1[q];
+      th[2][q] = cmp1[q] == INT64_MIN ? cmp1[q] : add(cmp1[q], take0[q], o2);
+      th[3][q] = cmp2[q];
+      th[4][q] = cmp2[q] == INT64_MIN ? cmp2[q] : add(cmp2[q], take0[q], o4);
+      th[5][q] = cmp2[q] == INT64_MIN ? cmp2[q] : add(cmp2[q], take1[q], o5);
       if (cmp2[q] == INT64_MIN) {
-        t.th[6][q] = cmp2[q];
+        th[6][q] = cmp2[q];
       } else {
-        const int64_t v = add(cmp2[q], take0[q], &o6);
-        t.th[6][q] = o6 ? v : add(v, take1[q], &o6);
+        const int64_t v = add(cmp2[q], take0[q], o6);
+        th[6][q] = o6 ? v : add(v, take1[q], o6);
       }
-      t.over |= (o2 ? 4 : 0) | (o4 ? 16 : 0) | (o5 ? 32 : 0) | (o6 ? 64 : 0);
+      over |= (o2 ? 4 : 0) | (o4 ? 16 : 0) | (o5 ? 32 : 0) | (o6 ? 64 : 0);
     }
     if (steps == 2) {  // rows 3..6 unused
 #pragma unroll
-      for (int j = 3; j < 7; ++j)
+      for (int jj = 3; jj < 7; ++jj)
 #pragma unroll
-        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) t.th[j][q] = 0;
-      t.over &= 7;
+        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) th[jj][q] = 0;
+      over &= 7;
     }
     // full-mask rows (0, 1, 3: a selection's own need) that repeat an earlier one (the
     // selections of one container are identical): bit 8 row 1 == row 0, bit 9 row 3 == row 0,
-    // bit 10 row 3 == row 1 — the kernel copies the mask instead of computing it
+    // bit 10 row 3 == row 1 (the ranked kernel reuses the mask)
     auto same = [&](int a, int b) {
       bool eq = true;
-      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) eq = eq && t.th[a][q] == t.th[b][q];
+#pragma unroll
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) eq = eq && th[a][q] == th[b][q];
       return eq;
     };
-    if (same(1, 0)) t.over |= 1 << 8;
-    if (steps == 3 && same(3, 0)) t.over |= 1 << 9;
-    if (steps == 3 && same(3, 1)) t.over |= 1 << 10;
-    *reinterpret_cast<GasThresholds*>(out + kThRow) = t;
+    if (same(1, 0)) over |= 1 << 8;
+    if (steps == 3 && same(3, 0)) over |= 1 << 9;
+    if (steps == 3 && same(3, 1)) over |= 1 << 10;
+#pragma unroll
+    for (int jj = 0; jj < 7; ++jj)
+#pragma unroll
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) t->th[jj][q] = th[jj][q];
+    t->over = over;
   }
   multi[(int64_t)ml * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
 }
@@ -618,237 +646,6 @@ __device__ __forceinline__ uint32_t th_mask(const int64_t (&free)[kMaxCards][Q],
 
 __device__ __forceinline__ uint32_t lowest(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : 8u; }
 
-// Lane-private copy of the node's free values of the compared kinds (all but SKIP) in LDS,
-// [card][lane][kind], so that a lane can read its chosen card's values back with one LDS read
-// (registers cannot be indexed per lane).
-template <int kC>
-struct FreeTab {
-  int64_t* base;  // this wave's table: kMaxCards * 64 * kC
-  __device__ __forceinline__ int64_t* at(uint32_t card, int lane) const {
-    return base + ((int64_t)card * 64 + lane) * kC;
-  }
-};
-
-template <int Q, int SKIP, int kC>
-__device__ __forceinline__ void fill_tab(const int64_t (&free)[kMaxCards][Q], const FreeTab<kC>& tab,
-                                         int lane) {
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0, j = 0; q < Q; ++q)
-      if (q != SKIP) tab.at(k, lane)[j++] = free[k][q];
-}
-
-// A pod with 4 to 8 selections: the selections in order on a working copy of the free values
-// (registers), each a fit mask on the copy; the chosen card's copy drops by the take, updated
-// under the lanes that chose it (one branch per card some lane chose).
-template <int Q, int SKIP>
-__device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards][Q],
-                                                const GasSel* rec, int32_t S, uint64_t live,
-                                                uint32_t node_ok) {
-  typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
-  int64_t w[kMaxCards][Q];
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
-  bool fits = true;
-  uint32_t word = 0u;
-  for (int32_t t = 0; t < S; ++t) {
-    int64_t cmp[Q], neg[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const v2i64 ct = *reinterpret_cast<const v2i64*>(rec[t].ct[q]);
-      cmp[q] = ct.x;
-      neg[q] = ct.y;
-    }
-    const uint32_t c = lowest(th_mask<Q, SKIP>(w, cmp, live));
-    fits = fits && c < 8u;
-    if (!__ballot(fits)) break;
-#pragma unroll
-    for (int kk = 0; kk < kMaxCards; ++kk)
-      if (__ballot(c == (uint32_t)kk) && c == (uint32_t)kk)
-#pragma unroll
-        for (int q = 0; q < Q; ++q) w[kk][q] += neg[q];
-    word |= (c & 7u) << (3 * t);
-  }
-  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
-}
-
-// A pod with several selections, in order: selection t takes the first card (lexicographic)
-// whose current free covers its need (getCardsForContainerGPURequest, scheduler.go:200-257;
-// addRM after each take).  A card no earlier selection of the pod took from still has its
-// snapshot free, so the candidates are the fit mask of the need on the snapshot (free only
-// falls: a card outside the mask cannot pass); among them a card an earlier selection s took
-// from passes only if its current free cur[s] covers the need.  So
-//   c_t = lowest(mask(need_t) without {c_s : s < t, need_t > cur[s]})
-// and the take lowers cur of every s with c_s = c_t (a card first taken reads its snapshot
-// free from the lane's LDS copy).  Registers only, unrolled over t; a selection whose need
-// equals the previous one's reuses its mask (the selections of one container are identical).
-
-template <int Q, int SKIP, int kC>
-__device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q],
-                                              const GasSel* rec, int32_t S, uint64_t live,
-                                              uint32_t node_ok, const FreeTab<kC>& tab,
-                                              int lane, uint32_t same_row) {
-  typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
-  int64_t fr[kMaxCards][kC];
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0, j = 0; q < Q; ++q)
-      if (q != SKIP) fr[k][j++] = free[k][q];
-  int64_t cur[kPacked][kC];
-  uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot (0: stale)
-  uint32_t word = 0u, m = 0u;
-  bool fits = true;
-#pragma unroll
-  for (int t = 0; t < kPacked; ++t) {
-    if (t >= S) break;
-    int64_t need[kC], neg[kC];
-#pragma unroll
-    for (int q = 0, j = 0; q < Q; ++q)
-      if (q != SKIP) {
-        const v2i64 ct = *reinterpret_cast<const v2i64*>(rec[t].ct[q]);
-        need[j] = ct.x;
-        neg[j++] = ct.y;
-      }
-    // same_row: nibble t all ones = selection t's record equals selection t - 1's
-    const bool same = t > 0 && ((same_row >> (4 * t)) & 0xFu) == 0xFu;
-    if (!same) m = fit_mask<kC>(need, fr, live);
-    uint32_t bad = 0u;
-#pragma unroll
-    for (int s2 = 0; s2 < t; ++s2) {
-      bool ok = true;
-#pragma unroll
-      for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[s2][j];
-      bad |= ok ? 0u : cb[s2];
-    }
-    const uint32_t c = lowest(m & ~bad);
-    fits = fits && c < 8u;
-    if (!__ballot(fits)) break;
-    int64_t g[kC];
-    {
-      const int64_t* p = tab.at(min(c, 7u), lane);
-#pragma unroll
-      for (int j = 0; j < kC; ++j) g[j] = p[j];
-    }
-    // one valid entry per card: the newest take's; the entry it replaces is marked stale
-    // (no card bit) instead of being rewritten
-    const uint32_t bc = 1u << c;  // c = 8 (no card): bit 8, outside every 8-card mask
-#pragma unroll
-    for (int s2 = 0; s2 < t; ++s2) {
-      const bool e = cb[s2] == bc;
-#pragma unroll
-      for (int j = 0; j < kC; ++j) g[j] = e ? cur[s2][j] : g[j];
-      cb[s2] = e ? 0u : cb[s2];
-    }
-#pragma unroll
-    for (int j = 0; j < kC; ++j) {
-      g[j] += neg[j];
-      cur[t][j] = g[j];
-    }
-    cb[t] = bc;
-    word |= (c & 7u) << (3 * t);
-  }
-  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
-}
-
-// Pods of 4 to 8 selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
-// the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
-// reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
-// waiting for its copy does not hold up the other waves of the block.
-template <int Q, int SKIP, bool kBits>
-__device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                           int64_t* tab_base, uint32_t node_ok,
-                                           int32_t N, int32_t n, bool valid,
-                                           const int32_t* __restrict__ list,
-                                           const GasSel* __restrict__ sels,
-                                           const int32_t* __restrict__ count, const BlockTile& bt,
-                                           ResOut res,
-                                           uint64_t* __restrict__ fit) {
-  const int32_t lane = threadIdx.x & 63;
-  const uint64_t live = __ballot(valid && node_ok != 0u);
-  int32_t i0, i1;
-  list_share(count, bt, &i0, &i1);
-  // lists with a skipped kind read chosen cards back from the lane's LDS copy (kC = Q - 1)
-  constexpr bool kGather = Q > 1 && SKIP >= 0;
-  constexpr int kC = Q > 1 ? Q - 1 : 1;
-  const FreeTab<kC> tab{tab_base};
-  if (kGather && i0 < i1) fill_tab<Q, SKIP, kC>(free, tab, lane);
-  // a batch's rows are loaded one batch ahead: every load of the next batch is in flight
-  // while this batch's pods are evaluated (rows past the batch: zeros, not read)
-  constexpr int kIters = kMB * kRowChunks / 64;
-  int4 v[kIters];
-  int32_t wd = 0;
-  auto load_batch = [&](int32_t b0) {
-    const int32_t nb = max(0, min(kMB, i1 - b0));
-    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) {
-      const int32_t c = lane + it * 64;
-      v[it] = c < nb * kRowChunks ? src[c] : int4{0, 0, 0, 0};
-    }
-    wd = lane < nb ? list[b0 + lane] : 0;
-  };
-  if (i0 < i1) load_batch(i0);
-  for (int32_t b0 = i0; b0 < i1; b0 += kMB) {
-    const int32_t nb = min(kMB, i1 - b0);
-    __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
-#pragma unroll
-    for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
-    // for the sequential class: which selections repeat the previous one, for the whole batch
-    // in one ballot (lane l holds 16-B piece l % 4 of selection (l % 32) / 4 of row l / 32)
-    static_assert(kIters == 1 && kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "pieces");
-    uint64_t same_m;
-    {
-      const int4 u = v[0];
-      const int ux = __shfl_up(u.x, 4, 64), uy = __shfl_up(u.y, 4, 64);
-      const int uz = __shfl_up(u.z, 4, 64), uw = __shfl_up(u.w, 4, 64);
-      same_m = __ballot((lane & 31) >= 4 && u.x == ux && u.y == uy && u.z == uz && u.w == uw);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    // the batch's pod words straight from the staging register (lane j: pod j's word)
-    const int32_t wcur = wd;
-    load_batch(b0 + kMB);
-    for (int32_t j = 0; j < nb; ++j) {
-      const int32_t pw = __builtin_amdgcn_readlane(wcur, j);
-      const int32_t pod = pw & 0xFFFFFF;
-      const int32_t S = (pw >> 24) & 0xF;
-      const GasSel* rec = stage + j * kPacked;
-      uint32_t out = 0u;
-      if (!(pw & kBadPod)) {
-        if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
-          if constexpr (kGather)
-            out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane,
-                                         (uint32_t)(same_m >> (32 * j)));
-          else
-            out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
-        }
-      }
-      put_result<kBits>(res, fit, pod, N, n, valid, out);
-    }
-  }
-}
-
-// The lists of pods with 4 to 8 selections (class 2 of each kind-skip list).
-template <int Q, bool kBits, int l = 0>
-__device__ __forceinline__ void seq_lists(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
-                                          int64_t* tab, uint32_t node_ok, int32_t N, int32_t n,
-                                          bool valid, int32_t P, const int32_t* __restrict__ multi,
-                                          const GasSel* __restrict__ sels,
-                                          const int32_t* __restrict__ counts, const BlockTile& bt,
-                                          ResOut res, uint64_t* __restrict__ fit) {
-  constexpr int L = l * kClasses + 2;
-  multi_list<Q, l - 1, kBits>(free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
-                              sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
-  if constexpr (l < Q)
-    seq_lists<Q, kBits, l + 1>(free, stage, tab, node_ok, N, n, valid, P, multi, sels, counts, bt,
-                               res, fit);
-}
-
 // ---------------------------------------------------------------------------- ranked fit
 //
 // Rank compression (exact).  Every compare of the one-selection and closed-form paths is
@@ -885,24 +682,32 @@ struct alignas(16) GasRMulti {
   uint32_t rep[3][PAS_GAS_MAX_RES];
   uint32_t pk[4];
 };
+// A four-to-eight-selection pod's ranks: selection t's need per compared kind, replicated.
+struct alignas(16) GasRSeq {
+  uint32_t rep[kPacked][PAS_GAS_MAX_RES];
+};
 // rword flags (free bits of a multi-list word): the full-mask rows that repeat an earlier one
 constexpr uint32_t kSame01 = 1u << 28, kSame03 = 1u << 29, kSame13 = 1u << 31;
 
-__device__ __forceinline__ int32_t rank_rows(int32_t cls) { return cls == 0 ? 1 : cls == 1 ? 3 : 7; }
+// rows per pod of a slot class: 0 one selection, 1 two, 2 three, 3 four to eight (a row per
+// selection, rows past S hold INT64_MIN)
+__device__ __forceinline__ int32_t rank_rows(int32_t cls) {
+  return cls == 0 ? 1 : cls == 1 ? 3 : cls == 2 ? 7 : kPacked;
+}
 __device__ __forceinline__ int32_t rank_gs(int32_t cls) { return kRankMax / rank_rows(cls); }
 
 __device__ __forceinline__ void rank_group(
-    int32_t P, int32_t Q, const int32_t* __restrict__ counts, int32_t slot, int32_t gi,
+    int32_t P, int32_t Q, const int32_t* counts, int32_t slot, int32_t gi,
     const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
     GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti, int32_t* __restrict__ rword,
-    int64_t (*v)[kRankItems], uint32_t* pks) {
+    GasRSeq* __restrict__ rseq, int64_t (*v)[kRankItems], uint32_t* pks) {
   const int32_t NL = Q + 1;
-  const bool one = slot < NL;
-  const int32_t l = one ? slot : (slot - NL) >> 1;
-  const int32_t cls = one ? 0 : 1 + ((slot - NL) & 1);
+  const bool one = slot < NL, seq = slot >= 3 * NL;
+  const int32_t l = one ? slot : seq ? slot - 3 * NL : (slot - NL) >> 1;
+  const int32_t cls = one ? 0 : seq ? 3 : 1 + ((slot - NL) & 1);
   const int32_t R = rank_rows(cls);
-  const int32_t ml = l * kClasses + (cls - 1);  // multi list (cls > 0)
+  const int32_t ml = l * kClasses + (cls - 1 < 2 ? cls - 1 : 2);  // multi list (cls > 0)
   const int32_t cnt = counts[one ? l : NL + ml];
   const int32_t gb = gi * rank_gs(cls), ge = min(cnt, gb + rank_gs(cls));
   const int32_t n = (ge - gb) * R;
@@ -910,8 +715,12 @@ __device__ __forceinline__ void rank_group(
   if (one) {
     for (int32_t s = 0; s < l; ++s) base += counts[s];
   } else {
-    for (int32_t s = 0; s < slot - NL; ++s)
+    // two- and three-selection slots in slot order, then the sequential ones
+    const int32_t pairs = seq ? 2 * NL : slot - NL;
+    for (int32_t s = 0; s < pairs; ++s)
       base += (int64_t)counts[NL + (s >> 1) * kClasses + (s & 1)] * rank_rows(1 + (s & 1));
+    if (seq)  // list 0's sequential pods are not ranked (no groups, no rows)
+      for (int32_t s = 1; s < l; ++s) base += (int64_t)counts[NL + s * kClasses + 2] * kPacked;
   }
   base += (int64_t)gb * R;
   int64_t* srt = one ? srt_s : srt_m;
@@ -921,12 +730,21 @@ __device__ __forceinline__ void rank_group(
   const int32_t j = q - (skip >= 0 && q > skip ? 1 : 0);  // compared-kind index
   const bool live = kind && i < n;
   const int32_t pos = gb + (i < n ? i / R : 0), row = i < n ? i % R : 0;
-  const GasThresholds* th = one ? nullptr
-                                : reinterpret_cast<const GasThresholds*>(
-                                      sels + ((int64_t)ml * P + pos) * kPacked + kThRow);
+  const GasThresholds* th = one || seq ? nullptr
+                                      : reinterpret_cast<const GasThresholds*>(
+                                            sels + ((int64_t)ml * P + pos) * kPacked + kThRow);
   // values padded with INT64_MAX (never below an item; equal only to items past the padding)
   int64_t y = INT64_MAX;
-  if (live) y = one ? single[(int64_t)l * P + pos].cmp[q] : th->th[row][q];
+  if (live) {
+    if (one) {
+      y = single[(int64_t)l * P + pos].cmp[q];
+    } else if (seq) {  // selection `row` of the pod (INT64_MIN past its S)
+      const int32_t S = (multi[(int64_t)ml * P + pos] >> 24) & 0xF;
+      y = row < S ? sels[((int64_t)ml * P + pos) * kPacked + row].ct[q][0] : INT64_MIN;
+    } else {
+      y = th->th[row][q];
+    }
+  }
   v[q][i] = y;
   if (q == 0) pks[i] = 0u;
   __syncthreads();
@@ -943,10 +761,12 @@ __device__ __forceinline__ void rank_group(
       }
     }
     srt[(base + less + eqb) * PAS_GAS_MAX_RES + j] = y;
-    const uint32_t over = one ? 0u : (uint32_t)th->over;
+    const uint32_t over = one || seq ? 0u : (uint32_t)th->over;
     g = ((over >> row) & 1u) ? 0x80u : (uint32_t)(less + 1);
     if (one) {
       rsingle[(int64_t)l * P + pos].g[j] = g * 0x01010101u;
+    } else if (seq) {
+      rseq[(int64_t)l * P + pos].rep[row][j] = g * 0x01010101u;
     } else if (row == 0 || row == 1 || row == 3) {
       rmulti[(int64_t)(l * 2 + cls - 1) * P + pos].rep[row == 3 ? 2 : row][j] = g * 0x01010101u;
     } else {
@@ -955,7 +775,7 @@ __device__ __forceinline__ void rank_group(
   }
   __syncthreads();
   // one thread per item: the packed rows and the pod word
-  if (threadIdx.x >= kRankItems || i >= n) return;
+  if (threadIdx.x >= kRankItems || i >= n || seq) return;
   if (one) {
     rsingle[(int64_t)l * P + pos].word = single[(int64_t)l * P + pos].word;
     return;
@@ -991,33 +811,47 @@ __device__ __forceinline__ void chunk_groups(int32_t cnt, int32_t chunks, int32_
 // item's rank in its pod's record.  Items of a slot sit after those of the slots before it,
 // so a group's sorted rows are contiguous.
 constexpr int kRankPrepTpb = kRankItems * PAS_GAS_MAX_RES;
-constexpr int kRankPrepBlocks = 1024;
+constexpr int kRankPrepBlocks = 256;  // one per CU: a group per block at a time
 __global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
-    int32_t P, int32_t Q, const int32_t* __restrict__ counts,
+    int32_t P, int32_t Q, const int32_t* counts,
     const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
     GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti,
-    int32_t* __restrict__ rword) {
+    int32_t* __restrict__ rword, GasRSeq* __restrict__ rseq) {
   __shared__ int64_t v[PAS_GAS_MAX_RES][kRankItems];
   __shared__ uint32_t pks[kRankItems];
-  const int32_t NL = Q + 1, slots = NL * 3;
-  auto slot_count = [&](int32_t slot) {
-    return slot < NL ? counts[slot]
-                     : counts[NL + ((slot - NL) >> 1) * kClasses + ((slot - NL) & 1)];
+  __shared__ int32_t cnt_s[(1 + kClasses) * (PAS_GAS_MAX_RES + 1)];
+  const int32_t NL = Q + 1, slots = NL * 4;
+  // the list counts, loaded once (a slot scan of dependent global loads costs a round trip each)
+  if (threadIdx.x < (1 + kClasses) * NL) cnt_s[threadIdx.x] = counts[threadIdx.x];
+  __syncthreads();
+  counts = cnt_s;
+  // slots: one-selection lists, two/three-selection pairs, sequential lists (list 0's
+  // sequential pods, with no kind skipped, are evaluated on 64-bit values: no groups)
+  auto slot_groups = [&](int32_t slot) {
+    int32_t cnt, cls;
+    if (slot < NL) {
+      cnt = counts[slot], cls = 0;
+    } else if (slot < 3 * NL) {
+      cnt = counts[NL + ((slot - NL) >> 1) * kClasses + ((slot - NL) & 1)];
+      cls = 1 + ((slot - NL) & 1);
+    } else {
+      cnt = slot == 3 * NL ? 0 : counts[NL + (slot - 3 * NL) * kClasses + 2], cls = 3;
+    }
+    return (cnt + rank_gs(cls) - 1) / rank_gs(cls);
   };
   for (int32_t w = blockIdx.x;; w += gridDim.x) {
     // the group: w-th over the slots' groups in slot order
     int32_t slot = 0, gi = w;
     for (; slot < slots; ++slot) {
-      const int32_t G = (slot_count(slot) + rank_gs(slot < NL ? 0 : 1 + ((slot - NL) & 1)) - 1) /
-                        rank_gs(slot < NL ? 0 : 1 + ((slot - NL) & 1));
+      const int32_t G = slot_groups(slot);
       if (gi < G) break;
       gi -= G;
     }
     if (slot >= slots) return;
     __syncthreads();  // the previous group's reads of v / pks are done
     rank_group(P, Q, counts, slot, gi, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword,
-               v, pks);
+               rseq, v, pks);
   }
 }
 
@@ -1119,6 +953,350 @@ __device__ __forceinline__ uint32_t rmask(const uint32_t (&fa)[C], const uint32_
 
 // lowest set bit, 0xFFFFFFFF for none (v_ffbl_b32)
 __device__ __forceinline__ uint32_t lowbit(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : ~0u; }
+
+// Lane-private copy of the node's free values of the compared kinds (all but SKIP) in LDS,
+// [card][lane][kind], so that a lane can read its chosen card's values back with one LDS read
+// (registers cannot be indexed per lane).
+template <int kC>
+struct FreeTab {
+  int64_t* base;  // this wave's table: kMaxCards * 64 * kC
+  __device__ __forceinline__ int64_t* at(uint32_t card, int lane) const {
+    return base + ((int64_t)card * 64 + lane) * kC;
+  }
+};
+
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ void fill_tab(const int64_t (&free)[kMaxCards][Q], const FreeTab<kC>& tab,
+                                         int lane) {
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != SKIP) tab.at(k, lane)[j++] = free[k][q];
+}
+
+// A pod with 4 to 8 selections: the selections in order on a working copy of the free values
+// (registers), each a fit mask on the copy; the chosen card's copy drops by the take, updated
+// under the lanes that chose it (one branch per card some lane chose).
+template <int Q, int SKIP>
+__device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards][Q],
+                                                const GasSel* rec, int32_t S, uint64_t live,
+                                                uint32_t node_ok) {
+  typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+  int64_t w[kMaxCards][Q];
+#pragma unroll
+  for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
+  bool fits = true;
+  uint32_t word = 0u;
+  for (int32_t t = 0; t < S; ++t) {
+    int64_t cmp[Q], neg[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const v2i64 ct = *reinterpret_cast<const v2i64*>(rec[t].ct[q]);
+      cmp[q] = ct.x;
+      neg[q] = ct.y;
+    }
+    const uint32_t c = lowest(th_mask<Q, SKIP>(w, cmp, live));
+    fits = fits && c < 8u;
+    if (!__ballot(fits)) break;
+#pragma unroll
+    for (int kk = 0; kk < kMaxCards; ++kk)
+      if (__ballot(c == (uint32_t)kk) && c == (uint32_t)kk)
+#pragma unroll
+        for (int q = 0; q < Q; ++q) w[kk][q] += neg[q];
+    word |= (c & 7u) << (3 * t);
+  }
+  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
+// A pod with several selections, in order: selection t takes the first card (lexicographic)
+// whose current free covers its need (getCardsForContainerGPURequest, scheduler.go:200-257;
+// addRM after each take).  A card no earlier selection of the pod took from still has its
+// snapshot free, so the candidates are the fit mask of the need on the snapshot (free only
+// falls: a card outside the mask cannot pass); among them a card an earlier selection s took
+// from passes only if its current free cur[s] covers the need.  So
+//   c_t = lowest(mask(need_t) without {c_s : s < t, need_t > cur[s]})
+// and the take lowers cur of every s with c_s = c_t (a card first taken reads its snapshot
+// free from the lane's LDS copy).  Registers only, unrolled over t; a selection whose need
+// equals the previous one's reuses its mask (the selections of one container are identical).
+
+// kRanked: the fit masks from the group ranks (rk: selection t's ranks per compared kind,
+// replicated; fa / fb the node's card ranks) instead of 64-bit compares; card k is then bit
+// 4k + 3 of a mask (rmask), else bit k.
+template <int Q, int SKIP, int kC, bool kRanked = false>
+__device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q],
+                                              const GasSel* rec, int32_t S, uint64_t live,
+                                              uint32_t node_ok, const FreeTab<kC>& tab,
+                                              int lane, uint32_t same_row,
+                                              const uint32_t* rk = nullptr,
+                                              const uint32_t* fa = nullptr,
+                                              const uint32_t* fb = nullptr) {
+  typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+  int64_t fr[kMaxCards][kC];
+  if constexpr (!kRanked) {
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k)
+#pragma unroll
+      for (int q = 0, j = 0; q < Q; ++q)
+        if (q != SKIP) fr[k][j++] = free[k][q];
+  }
+  int64_t cur[kPacked][kC];
+  uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot (0: stale)
+  uint32_t word = 0u, m = 0u;
+  bool fits = true;
+#pragma unroll
+  for (int t = 0; t < kPacked; ++t) {
+    if (t >= S) break;
+    int64_t need[kC], neg[kC];
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != SKIP) {
+        const v2i64 ct = *reinterpret_cast<const v2i64*>(rec[t].ct[q]);
+        need[j] = ct.x;
+        neg[j++] = ct.y;
+      }
+    // same_row: nibble t all ones = selection t's record equals selection t - 1's
+    const bool same = t > 0 && ((same_row >> (4 * t)) & 0xFu) == 0xFu;
+    if (!same) {
+      if constexpr (kRanked) {
+        uint32_t ga[kC], gfa[kC], gfb[kC];
+#pragma unroll
+        for (int j = 0; j < kC; ++j) {
+          ga[j] = rk[t * PAS_GAS_MAX_RES + j];
+          gfa[j] = fa[j];
+          gfb[j] = fb[j];
+        }
+        m = rmask<kC>(gfa, gfb, ga);
+      } else {
+        m = fit_mask<kC>(need, fr, live);
+      }
+    }
+    uint32_t bad = 0u;
+#pragma unroll
+    for (int s2 = 0; s2 < t; ++s2) {
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[s2][j];
+      bad |= ok ? 0u : cb[s2];
+    }
+    // the chosen card, and its bit in the mask layout (a failed lane's later choices are
+    // garbage: its word is 0 whatever they are)
+    uint32_t c, bc;
+    if constexpr (kRanked) {
+      const uint32_t pb = lowbit(m & ~bad);
+      c = pb >> 2;
+      bc = 1u << (pb & 31u);
+    } else {
+      c = lowest(m & ~bad);
+      bc = 1u << c;  // c = 8 (no card): bit 8, outside every 8-card mask
+    }
+    fits = fits && c < 8u;
+    if (!__ballot(fits)) break;
+    int64_t g[kC];
+    {
+      const int64_t* p = tab.at(min(c, 7u), lane);
+#pragma unroll
+      for (int j = 0; j < kC; ++j) g[j] = p[j];
+    }
+    // one valid entry per card: the newest take's; the entry it replaces is marked stale
+    // (no card bit) instead of being rewritten
+#pragma unroll
+    for (int s2 = 0; s2 < t; ++s2) {
+      const bool e = cb[s2] == bc;
+#pragma unroll
+      for (int j = 0; j < kC; ++j) g[j] = e ? cur[s2][j] : g[j];
+      cb[s2] = e ? 0u : cb[s2];
+    }
+#pragma unroll
+    for (int j = 0; j < kC; ++j) {
+      g[j] += neg[j];
+      cur[t][j] = g[j];
+    }
+    cb[t] = bc;
+    word |= (c & 7u) << (3 * t);
+  }
+  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+}
+
+// Pods of 4 to 8 selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
+// the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
+// reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
+// waiting for its copy does not hold up the other waves of the block.
+template <int Q, int SKIP, bool kBits>
+__device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
+                                           int64_t* tab_base, uint32_t node_ok,
+                                           int32_t N, int32_t n, bool valid,
+                                           const int32_t* __restrict__ list,
+                                           const GasSel* __restrict__ sels,
+                                           const int32_t* __restrict__ count, const BlockTile& bt,
+                                           ResOut res,
+                                           uint64_t* __restrict__ fit) {
+  const int32_t lane = threadIdx.x & 63;
+  const uint64_t live = __ballot(valid && node_ok != 0u);
+  int32_t i0, i1;
+  list_share(count, bt, &i0, &i1);
+  // lists with a skipped kind read chosen cards back from the lane's LDS copy (kC = Q - 1)
+  constexpr bool kGather = Q > 1 && SKIP >= 0;
+  constexpr int kC = Q > 1 ? Q - 1 : 1;
+  const FreeTab<kC> tab{tab_base};
+  if (kGather && i0 < i1) fill_tab<Q, SKIP, kC>(free, tab, lane);
+  // a batch's rows are loaded one batch ahead: every load of the next batch is in flight
+  // while this batch's pods are evaluated (rows past the batch: zeros, not read)
+  constexpr int kIters = kMB * kRowChunks / 64;
+  int4 v[kIters];
+  int32_t wd = 0;
+  auto load_batch = [&](int32_t b0) {
+    const int32_t nb = max(0, min(kMB, i1 - b0));
+    const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const int32_t c = lane + it * 64;
+      v[it] = c < nb * kRowChunks ? src[c] : int4{0, 0, 0, 0};
+    }
+    wd = lane < nb ? list[b0 + lane] : 0;
+  };
+  if (i0 < i1) load_batch(i0);
+  for (int32_t b0 = i0; b0 < i1; b0 += kMB) {
+    const int32_t nb = min(kMB, i1 - b0);
+    __builtin_amdgcn_wave_barrier();  // the previous batch's stage reads are done
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) reinterpret_cast<int4*>(stage)[lane + it * 64] = v[it];
+    // for the sequential class: which selections repeat the previous one, for the whole batch
+    // in one ballot (lane l holds 16-B piece l % 4 of selection (l % 32) / 4 of row l / 32)
+    static_assert(kIters == 1 && kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "pieces");
+    uint64_t same_m;
+    {
+      const int4 u = v[0];
+      const int ux = __shfl_up(u.x, 4, 64), uy = __shfl_up(u.y, 4, 64);
+      const int uz = __shfl_up(u.z, 4, 64), uw = __shfl_up(u.w, 4, 64);
+      same_m = __ballot((lane & 31) >= 4 && u.x == ux && u.y == uy && u.z == uz && u.w == uw);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    // the batch's pod words straight from the staging register (lane j: pod j's word)
+    const int32_t wcur = wd;
+    load_batch(b0 + kMB);
+    for (int32_t j = 0; j < nb; ++j) {
+      const int32_t pw = __builtin_amdgcn_readlane(wcur, j);
+      const int32_t pod = pw & 0xFFFFFF;
+      const int32_t S = (pw >> 24) & 0xF;
+      const GasSel* rec = stage + j * kPacked;
+      uint32_t out = 0u;
+      if (!(pw & kBadPod)) {
+        if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
+          if constexpr (kGather)
+            out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane,
+                                         (uint32_t)(same_m >> (32 * j)));
+          else
+            out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
+        }
+      }
+      put_result<kBits>(res, fit, pod, N, n, valid, out);
+    }
+  }
+}
+
+// Pods of 4 to 8 selections of a list with a skipped kind, with fit masks from group ranks
+// (multi_seq<..., true>): the list is cut into groups of 15 pods (8 rows each), a chunk takes
+// whole groups; per group the node's cards are ranked once, then batches of kMB pods (their
+// 64-bit rows for the current-free checks and their rank rows) are staged as in multi_list.
+// LDS: the FreeTab copy, then the sorted rows of the ranking, overlaid by the batch stage.
+template <int Q, int SKIP, bool kBits>
+__device__ __forceinline__ void rseq_list(const int64_t (&free)[kMaxCards][Q], char* wlds,
+                                          uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                          const int32_t* __restrict__ list,
+                                          const GasSel* __restrict__ sels,
+                                          const GasRSeq* __restrict__ rq,
+                                          const int64_t* __restrict__ srt, int64_t item0,
+                                          int32_t cnt, const BlockTile& bt, ResOut res,
+                                          uint64_t* __restrict__ fit) {
+  constexpr int kC = Q - 1;
+  const int32_t lane = threadIdx.x & 63;
+  const FreeTab<kC> tab{reinterpret_cast<int64_t*>(wlds)};
+  char* over = wlds + sizeof(int64_t) * kMaxCards * 64 * kC;
+  int64_t* lds = reinterpret_cast<int64_t*>(over);
+  GasSel* stage = reinterpret_cast<GasSel*>(over);
+  GasRSeq* rstage = reinterpret_cast<GasRSeq*>(stage + kMB * kPacked);
+  constexpr int32_t gs = kRankMax / kPacked;
+  int32_t g0, g1;
+  chunk_groups(cnt, bt.chunks, bt.chunk, gs, &g0, &g1);
+  if (g0 < g1) fill_tab<Q, SKIP, kC>(free, tab, lane);
+  static_assert(kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "one 16-B piece per lane");
+  static_assert(kMB * sizeof(GasRSeq) / 16 <= 64, "rank rows");
+  constexpr int kRWords = (int)(sizeof(GasRSeq) / 16);
+  for (int32_t gi = g0; gi < g1; ++gi) {
+    const int32_t gb = gi * gs, ge = min(cnt, gb + gs);
+    load_sorted<kC>(srt, item0 + (int64_t)gb * kPacked, (ge - gb) * kPacked, lds, lane);
+    uint32_t fa[kC], fb[kC];
+    rank_cards<Q, SKIP, kC>(free, lds, (ge - gb) * kPacked, fa, fb);
+    for (int32_t b0 = gb; b0 < ge; b0 += kMB) {
+      const int32_t nb = min(kMB, ge - b0);
+      const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
+      const int4 v = lane < nb * kRowChunks ? src[lane] : int4{0, 0, 0, 0};
+      const int4* rsrc = reinterpret_cast<const int4*>(rq + b0);
+      const int4 rv = lane < nb * kRWords ? rsrc[lane] : int4{0, 0, 0, 0};
+      const int32_t wd = lane < nb ? list[b0 + lane] : 0;
+      __builtin_amdgcn_wave_barrier();  // the previous batch's (or the ranking's) reads are done
+      reinterpret_cast<int4*>(stage)[lane] = v;
+      if (lane < kMB * kRWords) reinterpret_cast<int4*>(rstage)[lane] = rv;
+      uint64_t same_m;  // selections repeating the previous one (as multi_list)
+      {
+        const int ux = __shfl_up(v.x, 4, 64), uy = __shfl_up(v.y, 4, 64);
+        const int uz = __shfl_up(v.z, 4, 64), uw = __shfl_up(v.w, 4, 64);
+        same_m = __ballot((lane & 31) >= 4 && v.x == ux && v.y == uy && v.z == uz && v.w == uw);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      for (int32_t j = 0; j < nb; ++j) {
+        const int32_t pw = __builtin_amdgcn_readlane(wd, j);
+        const int32_t pod = pw & 0xFFFFFF;
+        const int32_t S = (pw >> 24) & 0xF;
+        uint32_t out = 0u;
+        if (!(pw & kBadPod) && S <= kPacked)  // more: the generic kernel's, 0 here
+          out = multi_seq<Q, SKIP, kC, true>(free, stage + j * kPacked, S, 0, node_ok, tab, lane,
+                                             (uint32_t)(same_m >> (32 * j)),
+                                             &rstage[j].rep[0][0], fa, fb);
+        put_result<kBits>(res, fit, pod, N, n, valid, out);
+      }
+    }
+  }
+}
+
+// The lists of pods with 4 to 8 selections (class 2 of each kind-skip list): ranked where a
+// kind is skipped (rseq_list), else on 64-bit values (multi_list).  item0: the first sorted
+// row of list 1's groups (after the two- and three-selection lists' rows).
+template <int Q, bool kBits, int l = 0>
+__device__ __forceinline__ void seq_lists(const int64_t (&free)[kMaxCards][Q], char* wlds,
+                                          uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                          int32_t P, const int32_t* __restrict__ multi,
+                                          const GasSel* __restrict__ sels,
+                                          const GasRSeq* __restrict__ rq,
+                                          const int64_t* __restrict__ srt, int64_t item0,
+                                          const int32_t* __restrict__ counts, const BlockTile& bt,
+                                          ResOut res, uint64_t* __restrict__ fit) {
+  constexpr int L = l * kClasses + 2;
+  int32_t cnt = 0;
+  if constexpr (l == 0 || Q == 1) {
+    GasSel* stage = reinterpret_cast<GasSel*>(wlds);
+    int64_t* tab = reinterpret_cast<int64_t*>(stage + kPacked * kMB);
+    multi_list<Q, l - 1, kBits>(free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
+                                sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
+  } else {
+    cnt = __builtin_amdgcn_readfirstlane(counts[L]);
+    rseq_list<Q, l - 1, kBits>(free, wlds, node_ok, N, n, valid, multi + (int64_t)L * P,
+                               sels + (int64_t)L * P * kPacked, rq + (int64_t)l * P, srt, item0,
+                               cnt, bt, res, fit);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (l < Q)
+    seq_lists<Q, kBits, l + 1>(free, wlds, node_ok, N, n, valid, P, multi, sels, rq, srt,
+                               item0 + (int64_t)cnt * kPacked, counts, bt, res, fit);
+}
+
 
 template <int Q, int SKIP, bool kBits>
 __device__ __forceinline__ void rsingle_list(const int64_t (&free)[kMaxCards][Q],
@@ -1356,15 +1534,19 @@ struct MultiLds {
   static constexpr int kC = Q > 1 ? Q - 1 : 1;
   static constexpr size_t kRanked =
       sizeof(int64_t) * Q * kRankItems + sizeof(GasRMulti) * kRankMB + sizeof(uint32_t) * kMaxCards * 64;
-  static constexpr size_t kSeq =
-      sizeof(GasSel) * kPacked * kMB + sizeof(int64_t) * kMaxCards * 64 * kC;
+  static constexpr size_t kSeqOver = sizeof(int64_t) * kC * kRankItems >
+                                             sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB
+                                         ? sizeof(int64_t) * kC * kRankItems
+                                         : sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB;
+  static constexpr size_t kSeq = sizeof(int64_t) * kMaxCards * 64 * kC + kSeqOver;
   static constexpr size_t kBytes = kRanked > kSeq ? kRanked : kSeq;
 };
 
 template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
-    const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm, const int32_t* __restrict__ rw,
+    const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
+    const int32_t* __restrict__ rw, const GasRSeq* __restrict__ rq,
     const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
     ResOut res, uint64_t* __restrict__ fit) {
@@ -1384,10 +1566,13 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
   rmulti_lists<Q, kBits>(free, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
                          tab, res, fit);
   __builtin_amdgcn_wave_barrier();
-  GasSel* sstage = reinterpret_cast<GasSel*>(w);
-  int64_t* stab = reinterpret_cast<int64_t*>(sstage + kPacked * kMB);
-  seq_lists<Q, kBits>(free, sstage, stab, node_ok, N, n, valid, P, multi, sels, counts, bt, res,
-                      fit);
+  // the sequential lists' sorted rows follow every two- and three-selection list's rows
+  int64_t item_seq = 0;
+#pragma unroll
+  for (int l = 0; l <= Q; ++l)
+    item_seq += (int64_t)counts[l * kClasses] * 3 + (int64_t)counts[l * kClasses + 1] * 7;
+  seq_lists<Q, kBits>(free, w, node_ok, N, n, valid, P, multi, sels, rq, srt,
+                      __builtin_amdgcn_readfirstlane(item_seq), counts, bt, res, fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -1573,9 +1758,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_rm = al(sizeof(GasRMulti) * (size_t)NL * 2 * n_pods);
   const size_t b_rw = al(sizeof(int32_t) * (size_t)NL * 2 * n_pods);
   const size_t b_srs = al(sizeof(int64_t) * PAS_GAS_MAX_RES * (size_t)n_pods);
-  const size_t b_srm = al(sizeof(int64_t) * PAS_GAS_MAX_RES * 7 * (size_t)n_pods);
+  const size_t b_srm = al(sizeof(int64_t) * PAS_GAS_MAX_RES * kPacked * (size_t)n_pods);
+  const size_t b_rq = al(sizeof(GasRSeq) * (size_t)NL * n_pods);
   const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_rs + b_rm + b_rw + b_srs +
-                      b_srm + b_tail;
+                      b_srm + b_rq + b_tail;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -1607,6 +1793,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   base += b_srs;
   int64_t* srt_m = reinterpret_cast<int64_t*>(base);
   base += b_srm;
+  GasRSeq* rseq = reinterpret_cast<GasRSeq*>(base);
+  base += b_rq;
   int32_t* counts = reinterpret_cast<int32_t*>(base);
   int32_t* n_big_pods = counts + (1 + kClasses) * (PAS_GAS_MAX_RES + 1);
   unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
@@ -1631,7 +1819,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const int32_t ch_s = (n_pods + kRankMax - 1) / kRankMax;  // fixed one-group chunks
   const int32_t ch_m = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_s - 1) / nb_s));
   gas_rank_prep_kernel<<<kRankPrepBlocks, kRankPrepTpb, 0, s>>>(
-      n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword);
+      n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword, rseq);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
@@ -1642,7 +1830,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, ch_s, ResOut{d_res, ld_res}, d_fit);        \
     gas_rfit_multi_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                 \
-        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m, multi, sels, counts + NL,      \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, rseq, srt_m, multi, sels, counts + NL,      \
         ch_m, ResOut{d_res, ld_res}, d_fit);                                                                   \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
