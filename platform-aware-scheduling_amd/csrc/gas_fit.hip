@@ -208,8 +208,19 @@ __global__ __launch_bounds__(kPrepTpb) void gas_prep_kernel(int32_t n_pods, int3
                                 GasSingle* __restrict__ single, int32_t* __restrict__ multi,
                                 GasSel* __restrict__ sels, int32_t* __restrict__ counts,
                                 int32_t* __restrict__ big_pods, int32_t* __restrict__ n_big_pods,
-                                int32_t* __restrict__ pod_steps) {
+                                int32_t* __restrict__ pod_steps, int32_t* __restrict__ counts_next,
+                                int32_t n_counts, int64_t* __restrict__ limit_count,
+                                int64_t* __restrict__ side_count) {
   const int32_t p = blockIdx.x * kPrepTpb + threadIdx.x;
+  // block 0 zeroes the next fit's counts and this fit's generic-kernel counters (read after
+  // this kernel in stream order), in place of fill launches
+  if (blockIdx.x == 0) {
+    for (int32_t i = threadIdx.x; i < n_counts; i += kPrepTpb) counts_next[i] = 0;
+    if (threadIdx.x == 0) {
+      *limit_count = 0;
+      if (side_count) *side_count = 0;
+    }
+  }
   if (p >= n_pods) return;
   const int32_t nc = min(max(n_containers[p], 0), max_containers);
   const int64_t row = (int64_t)p * max_containers;
@@ -1730,13 +1741,17 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
                    hipStream_t s) {
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
+  constexpr int32_t kCounts = (1 + kClasses) * (PAS_GAS_MAX_RES + 1) + 1;  // lists + generic pods
   if (!ctx->gas_limit) {
     PAS_HIP(ctx, hipMalloc(&ctx->gas_limit, sizeof(int64_t)));
     PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_limit_ev, hipEventDisableTiming));
+    PAS_HIP(ctx, hipMalloc(&ctx->gas_counts, 2 * kCounts * sizeof(int32_t)));
+    PAS_HIP(ctx, hipMemsetAsync(ctx->gas_counts, 0, 2 * kCounts * sizeof(int32_t), s));
+    ctx->gas_counts_set = 0;
   }
-  PAS_HIP(ctx, hipMemsetAsync(ctx->gas_limit, 0, sizeof(int64_t), s));
-  if (d_side_count) PAS_HIP(ctx, hipMemsetAsync(d_side_count, 0, sizeof(int64_t), s));
   if (N == 0 || n_pods == 0) {
+    PAS_HIP(ctx, hipMemsetAsync(ctx->gas_limit, 0, sizeof(int64_t), s));
+    if (d_side_count) PAS_HIP(ctx, hipMemsetAsync(d_side_count, 0, sizeof(int64_t), s));
     PAS_HIP(ctx, hipEventRecord(ctx->gas_limit_ev, s));
     return PAS_OK;
   }
@@ -1752,7 +1767,6 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_multi = al(sizeof(int32_t) * (size_t)NL * kClasses * n_pods);
   const size_t b_sels = al(sizeof(GasSel) * kPacked * (size_t)NL * kClasses * n_pods);
   const size_t b_pods = al(sizeof(int32_t) * (size_t)n_pods);
-  constexpr size_t b_tail = ((1 + kClasses) * (PAS_GAS_MAX_RES + 1) + 1) * sizeof(int32_t);
   // ranked paths: pod records and sorted rows (items: <= P one-selection, <= 7P closed-form)
   const size_t b_rs = al(sizeof(GasRSingle) * (size_t)NL * n_pods);
   const size_t b_rm = al(sizeof(GasRMulti) * (size_t)NL * 2 * n_pods);
@@ -1761,7 +1775,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_srm = al(sizeof(int64_t) * PAS_GAS_MAX_RES * kPacked * (size_t)n_pods);
   const size_t b_rq = al(sizeof(GasRSeq) * (size_t)NL * n_pods);
   const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_rs + b_rm + b_rw + b_srs +
-                      b_srm + b_rq + b_tail;
+                      b_srm + b_rq;
   if (need > ctx->aux_bytes) {
     if (ctx->aux) {
       PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -1795,14 +1809,16 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   base += b_srm;
   GasRSeq* rseq = reinterpret_cast<GasRSeq*>(base);
   base += b_rq;
-  int32_t* counts = reinterpret_cast<int32_t*>(base);
+  // this fit's list counts (zeroed by the previous fit's prep kernel, or at allocation) and
+  // the other set, which this fit's prep kernel zeroes for the next one
+  int32_t* counts = ctx->gas_counts + kCounts * ctx->gas_counts_set;
+  int32_t* counts_next = ctx->gas_counts + kCounts * (1 - ctx->gas_counts_set);
   int32_t* n_big_pods = counts + (1 + kClasses) * (PAS_GAS_MAX_RES + 1);
   unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
   int32_t* n_big_nodes = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
   int32_t* big_nodes = reinterpret_cast<int32_t*>(static_cast<char*>(g.derived) + 64);
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
-  PAS_HIP(ctx, hipMemsetAsync(counts, 0, b_tail, s));
   if (ctx->gas.derived_epoch != ctx->gas.epoch) {
     PAS_HIP(ctx, hipMemsetAsync(gflip, 0, 64, s));
     gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
@@ -1812,7 +1828,9 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   }
   gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
-      multi, sels, counts, big_pods, n_big_pods, pod_steps);
+      multi, sels, counts, big_pods, n_big_pods, pod_steps, counts_next, kCounts, ctx->gas_limit,
+      d_side_count);
+  ctx->gas_counts_set = 1 - ctx->gas_counts_set;
   // grids: (node block, pod chunk) pairs, ~8192 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
   const int32_t nb_s = (N + kTpb - 1) / kTpb;

@@ -197,6 +197,7 @@ void pas_destroy(pas_ctx* ctx) {
   if (ctx->merge_buf) (void)hipFree(ctx->merge_buf);
   if (ctx->label_part) (void)hipFree(ctx->label_part);
   if (ctx->gas_limit) (void)hipFree(ctx->gas_limit);
+  if (ctx->gas_counts) (void)hipFree(ctx->gas_counts);
   if (ctx->tas_gpass) (void)hipFree(ctx->tas_gpass);
   if (ctx->gas_limit_ev) (void)hipEventDestroy(ctx->gas_limit_ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);

@@ -119,6 +119,10 @@ struct pas_ctx {
   void* merge_buf = nullptr;  // ping-pong rows of the full-list merge (tas_list_merge.hip)
   size_t merge_bytes = 0;
   int64_t* gas_limit = nullptr;     // pods of the last GAS fit past PAS_GAS_MAX_SELECTIONS
+  // the GAS fit's list counts, two sets: a fit uses one (zero) and its prep kernel zeroes the
+  // other for the next fit (no fill launch per fit); gas_counts_set = the set of the next fit
+  int32_t* gas_counts = nullptr;
+  int gas_counts_set = 0;
   hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
