@@ -744,14 +744,20 @@ __device__ __forceinline__ void rank_group(
   const GasThresholds* th = one || seq ? nullptr
                                       : reinterpret_cast<const GasThresholds*>(
                                             sels + ((int64_t)ml * P + pos) * kPacked + kThRow);
-  // values padded with INT64_MAX (never below an item; equal only to items past the padding)
+  // every global load of the group up front (one round trip): the value (padded with
+  // INT64_MAX: never below an item, equal only to items past the padding), the pod word, the
+  // threshold flags, the one-selection word
+  const bool item = i < n;
+  const int32_t mword = !one && item ? multi[(int64_t)ml * P + pos] : 0;
+  const uint32_t over = !one && !seq && item ? (uint32_t)th->over : 0u;
+  const int32_t sword = one && item && q == 0 ? single[(int64_t)l * P + pos].word : 0;
   int64_t y = INT64_MAX;
   if (live) {
     if (one) {
       y = single[(int64_t)l * P + pos].cmp[q];
-    } else if (seq) {  // selection `row` of the pod (INT64_MIN past its S)
-      const int32_t S = (multi[(int64_t)ml * P + pos] >> 24) & 0xF;
-      y = row < S ? sels[((int64_t)ml * P + pos) * kPacked + row].ct[q][0] : INT64_MIN;
+    } else if (seq) {  // selection `row` of the pod, loaded unconditionally (INT64_MIN past S)
+      const int64_t x = sels[((int64_t)ml * P + pos) * kPacked + row].ct[q][0];
+      y = row < ((mword >> 24) & 0xF) ? x : INT64_MIN;
     } else {
       y = th->th[row][q];
     }
@@ -772,7 +778,6 @@ __device__ __forceinline__ void rank_group(
       }
     }
     srt[(base + less + eqb) * PAS_GAS_MAX_RES + j] = y;
-    const uint32_t over = one || seq ? 0u : (uint32_t)th->over;
     g = ((over >> row) & 1u) ? 0x80u : (uint32_t)(less + 1);
     if (one) {
       rsingle[(int64_t)l * P + pos].g[j] = g * 0x01010101u;
@@ -788,17 +793,15 @@ __device__ __forceinline__ void rank_group(
   // one thread per item: the packed rows and the pod word
   if (threadIdx.x >= kRankItems || i >= n || seq) return;
   if (one) {
-    rsingle[(int64_t)l * P + pos].word = single[(int64_t)l * P + pos].word;
+    rsingle[(int64_t)l * P + pos].word = sword;
     return;
   }
   const int64_t mp = (int64_t)(l * 2 + cls - 1) * P + pos;
   if (row == 2 || row >= 4) rmulti[mp].pk[row == 2 ? 0 : row - 3] = pks[i];
-  if (row == 0) {
-    const uint32_t o = (uint32_t)th->over;
-    rword[mp] = (int32_t)((uint32_t)multi[(int64_t)ml * P + pos] |
-                          (((o >> 8) & 1u) ? kSame01 : 0u) | (((o >> 9) & 1u) ? kSame03 : 0u) |
-                          (((o >> 10) & 1u) ? kSame13 : 0u));
-  }
+  if (row == 0)
+    rword[mp] = (int32_t)((uint32_t)mword | (((over >> 8) & 1u) ? kSame01 : 0u) |
+                          (((over >> 9) & 1u) ? kSame03 : 0u) |
+                          (((over >> 10) & 1u) ? kSame13 : 0u));
 }
 
 
