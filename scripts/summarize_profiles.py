@@ -20,8 +20,8 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles")
 TAS_PATH = ("tas_prep_kernel", "tas_eval_kernel")
-GAS_PATH = ("gas_minfree_kernel", "gas_prep_kernel", "gas_fit_single_kernel",
-            "gas_fit_multi_kernel", "gas_fit_generic_kernel")
+GAS_PATH = ("gas_minfree_kernel", "gas_prep_kernel", "gas_rank_prep_kernel",
+            "gas_rfit_single_kernel", "gas_rfit_multi_kernel", "gas_fit_generic_kernel")
 
 
 def short(name):
@@ -90,7 +90,7 @@ def main():
         elif w == "gas":
             # per step: gas_minfree_kernel runs once per snapshot change, not per fit
             calls = {r["kernel"]: r["calls"] for r in rows}
-            per = max(calls.get("gas_fit_single_kernel", 1), 1)
+            per = max(calls.get("gas_rfit_single_kernel", 1), 1)
             wt = {k: min(calls.get(k, per) / per, 1.0) for k in GAS_PATH}
             traffic["gas_fit_kernel"] = round(sum(hbm(k) * wt[k] for k in GAS_PATH))
             traffic["gas_fit_by_kernel"] = {k: round(hbm(k)) for k in GAS_PATH}
