@@ -952,6 +952,47 @@ __device__ __forceinline__ void rank_cards(const int64_t (&free)[kMaxCards][Q], 
   }
 }
 
+// rank_cards with the free values read from the card-major copy one kind at a time (8 values
+// live instead of 8 Q).
+template <int Q, int SKIP, int C>
+__device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t, int32_t n_node,
+                                             bool valid, int32_t N, const int64_t* lds,
+                                             int32_t n, uint32_t (&fa)[C], uint32_t (&fb)[C]) {
+  const int32_t nn = valid ? n_node : 0;
+#pragma unroll
+  for (int q = 0, j = 0; q < Q; ++q) {
+    if (q == SKIP) continue;
+    int64_t f[kMaxCards];
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k) {
+      const int64_t x = free_t[((int64_t)k * Q + q) * N + nn];
+      f[k] = valid ? x : -1;
+    }
+    uint32_t pos[kMaxCards];
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k) pos[k] = 0u;
+    const int64_t* row = lds + j * kRankItems;
+#pragma unroll
+    for (int sh = 6; sh >= 0; --sh) {
+      int64_t x[kMaxCards];
+#pragma unroll
+      for (int k = 0; k < kMaxCards; ++k) x[k] = row[(pos[k] << (sh + 1)) + (1 << sh) - 1];
+      rank_level4(pos[0], pos[1], pos[2], pos[3], x[0], x[1], x[2], x[3], f[0], f[1], f[2], f[3]);
+      rank_level4(pos[4], pos[5], pos[6], pos[7], x[4], x[5], x[6], x[7], f[4], f[5], f[6], f[7]);
+    }
+    uint32_t a = 0u, b = 0u;
+#pragma unroll
+    for (int k = 0; k < kMaxCards; ++k) {
+      const uint32_t r = min(pos[k], (uint32_t)n) + 0x80u;
+      if (k & 1) b |= r << (8 * (k >> 1));
+      else a |= r << (8 * (k >> 1));
+    }
+    fa[j] = a;
+    fb[j] = b;
+    ++j;
+  }
+}
+
 // Card mask of a row of replicated ranks g[j]: card k passes <=> bit 4k + 3.
 template <int C>
 __device__ __forceinline__ uint32_t rmask(const uint32_t (&fa)[C], const uint32_t (&fb)[C],
@@ -1313,7 +1354,7 @@ __device__ __forceinline__ void seq_lists(const int64_t (&free)[kMaxCards][Q], c
 
 
 template <int Q, int SKIP, bool kBits>
-__device__ __forceinline__ void rsingle_list(const int64_t (&free)[kMaxCards][Q],
+__device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
                                              uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                              const GasRSingle* __restrict__ rs,
                                              const int64_t* __restrict__ srt, int64_t item0,
@@ -1326,9 +1367,10 @@ __device__ __forceinline__ void rsingle_list(const int64_t (&free)[kMaxCards][Q]
   // this chunk's group (one-selection lists: chunk = group)
   const int32_t gb = min(cnt, bt.chunk * kRankMax), ge = min(cnt, gb + kRankMax);
   if (gb >= ge) return;
-  load_sorted<C>(srt, item0 + gb, ge - gb, lds, lane);
   uint32_t fa[C], fb[C];
-  rank_cards<Q, kSkip, C>(free, lds, ge - gb, fa, fb);
+  // the node's free values only while ranking, one kind at a time (registers for the pod loop)
+  load_sorted<C>(srt, item0 + gb, ge - gb, lds, lane);
+  rank_cards_t<Q, kSkip, C>(free_t, n, valid, N, lds, ge - gb, fa, fb);
   auto one_pod = [&](const GasRSingle& r, int32_t w) {
     const int64_t pod = w & 0xFFFFFF;
     uint32_t out = node_ok;
@@ -1371,7 +1413,7 @@ __device__ __forceinline__ void rsingle_list(const int64_t (&free)[kMaxCards][Q]
 }
 
 template <int Q, bool kBits, int L = 0>
-__device__ __forceinline__ void rsingle_lists(const int64_t (&free)[kMaxCards][Q],
+__device__ __forceinline__ void rsingle_lists(const int64_t* __restrict__ free_t,
                                               uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                               int32_t P, const GasRSingle* __restrict__ rs,
                                               const int64_t* __restrict__ srt, int64_t item0,
@@ -1380,10 +1422,10 @@ __device__ __forceinline__ void rsingle_lists(const int64_t (&free)[kMaxCards][Q
                                               GasRSingle* stage, ResOut res,
                                               uint64_t* __restrict__ fit) {
   const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[L]);
-  rsingle_list<Q, L - 1, kBits>(free, node_ok, N, n, valid, rs + (int64_t)L * P, srt, item0, cnt,
-                                bt, lds, stage, res, fit);
+  rsingle_list<Q, L - 1, kBits>(free_t, node_ok, N, n, valid, rs + (int64_t)L * P, srt, item0,
+                                cnt, bt, lds, stage, res, fit);
   if constexpr (L < Q)
-    rsingle_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, rs, srt, item0 + cnt, counts,
+    rsingle_lists<Q, kBits, L + 1>(free_t, node_ok, N, n, valid, P, rs, srt, item0 + cnt, counts,
                                    bt, lds, stage, res, fit);
 }
 
@@ -1404,11 +1446,9 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
-  int64_t free[kMaxCards][Q];
-  load_free_t<Q>(n, valid, N, free_t, free);
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  rsingle_lists<Q, kBits>(free, node_ok, N, n, valid, P, rs, srt, 0, counts, bt, lds[wave],
+  rsingle_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rs, srt, 0, counts, bt, lds[wave],
                           stage[wave], res, fit);
 }
 
