@@ -75,7 +75,7 @@ struct alignas(16) GasSel {
   int64_t ct[PAS_GAS_MAX_RES][2];
 };
 // A pod with 2 or 3 selections is resolved in closed form from threshold compares on the
-// snapshot free values (see multi_closed): threshold j per kind, in compare form (INT64_MIN
+// snapshot free values (see rclosed): threshold j per kind, in compare form (INT64_MIN
 // for kinds the selection does not request).  The 7 thresholds of a 3-selection pod:
 //   0: n0   1: n1   2: n1 + t0   3: n2   4: n2 + t0   5: n2 + t1   6: n2 + t0 + t1
 // (n = the selection's need, t = an earlier selection's take); a 2-selection pod uses 0-2.
@@ -1460,9 +1460,18 @@ __device__ __forceinline__ bool rpoint(uint32_t x, uint32_t gp) {
   return ((x - gp) & kMc) == kMc;
 }
 
-// Two- and three-selection pods in closed form (as closed_body) on ranks: masks of rows 0, 1, 3,
-// rows 2, 4, 5, 6 at the chosen cards from the lane's table of packed ranks.  Card positions
-// are bit positions 4c + 3 (0xFFFFFFFF: none), so min() picks the lower card and none loses.
+// Two- and three-selection pods in closed form on ranks.  Selection t takes the first card
+// whose free covers its need plus the takes already on that card (getCardsForContainerGPU-
+// Request, scheduler.go:200-257; addRM, resource_map.go:38-53); which earlier takes those are
+// depends only on the earlier choices, so every combination is one threshold row
+// (GasThresholds):
+//   c0 = lowest(m0)
+//   c1 = min(lowest(m1 without c0), c0 if row 2 fits at c0)
+//   c2 = min(lowest(m3 without c0, c1),
+//            c0 == c1 ? (c0 if row 6 fits at c0) : min(c0 if row 4 fits at c0, c1 if row 5 at c1))
+// Masks of rows 0, 1, 3 from the group ranks; rows 2, 4, 5, 6 checked at the chosen card on
+// its packed ranks from the lane's table.  Card positions are bit positions 4c + 3
+// (0xFFFFFFFF: none), so min() picks the lower card and none loses.
 template <int C, int S>
 __device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint32_t (&fb)[C],
                                            const GasRMulti& r, uint32_t w, const uint32_t* tab,
