@@ -1797,8 +1797,15 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   if (!ctx->gas_limit) {
     PAS_HIP(ctx, hipMalloc(&ctx->gas_limit, sizeof(int64_t)));
     PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_limit_ev, hipEventDisableTiming));
-    PAS_HIP(ctx, hipMalloc(&ctx->gas_counts, 2 * kCounts * sizeof(int32_t)));
-    PAS_HIP(ctx, hipMemsetAsync(ctx->gas_counts, 0, 2 * kCounts * sizeof(int32_t), s));
+  }
+  if (!ctx->gas_counts) {  // both sets zero before their first use
+    int32_t* c = nullptr;
+    PAS_HIP(ctx, hipMalloc(&c, 2 * kCounts * sizeof(int32_t)));
+    if (hipMemsetAsync(c, 0, 2 * kCounts * sizeof(int32_t), s) != hipSuccess) {
+      (void)hipFree(c);
+      return set_error(ctx, PAS_EDEVICE, "pas_gas_fit: counts init failed");
+    }
+    ctx->gas_counts = c;
     ctx->gas_counts_set = 0;
   }
   if (N == 0 || n_pods == 0) {
