@@ -1099,7 +1099,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
   }
   int64_t cur[kPacked][kC];
   uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot (0: stale)
-  uint32_t word = 0u, m = 0u;
+  uint32_t word = 0u, m = 0u, bad_prev = 0u;
   bool fits = true;
 #pragma unroll
   for (int t = 0; t < kPacked; ++t) {
@@ -1129,13 +1129,24 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
       }
     }
     uint32_t bad = 0u;
-#pragma unroll
-    for (int s2 = 0; s2 < t; ++s2) {
+    if (same) {
+      // the need of step t - 1: the entries before t - 1 that are still valid are unchanged
+      // since then (a take only adds an entry and marks the card's older one stale, and the
+      // card taken was not in the old set), so only entry t - 1 is new
       bool ok = true;
 #pragma unroll
-      for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[s2][j];
-      bad |= ok ? 0u : cb[s2];
+      for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[t > 0 ? t - 1 : 0][j];
+      bad = bad_prev | (ok ? 0u : cb[t > 0 ? t - 1 : 0]);
+    } else {
+#pragma unroll
+      for (int s2 = 0; s2 < t; ++s2) {
+        bool ok = true;
+#pragma unroll
+        for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[s2][j];
+        bad |= ok ? 0u : cb[s2];
+      }
     }
+    bad_prev = bad;
     // the chosen card, and its bit in the mask layout (a failed lane's later choices are
     // garbage: its word is 0 whatever they are)
     uint32_t c, bc;
