@@ -1522,7 +1522,7 @@ __device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint3
 }
 
 template <int Q, int SKIP, int S, bool kBits>
-__device__ __forceinline__ void rmulti_list(const int64_t (&free)[kMaxCards][Q], uint32_t node_ok,
+__device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, uint32_t node_ok,
                                             int32_t N, int32_t n, bool valid,
                                             const GasRMulti* __restrict__ rm,
                                             const int32_t* __restrict__ rw,
@@ -1542,7 +1542,7 @@ __device__ __forceinline__ void rmulti_list(const int64_t (&free)[kMaxCards][Q],
     const int32_t gb = gi * gs, ge = min(cnt, gb + gs);
     load_sorted<C>(srt, item0 + (int64_t)gb * R, (ge - gb) * R, lds, lane);
     uint32_t fa[C], fb[C];
-    rank_cards<Q, kSkip, C>(free, lds, (ge - gb) * R, fa, fb);
+    rank_cards_t<Q, kSkip, C>(free_t, n, valid, N, lds, (ge - gb) * R, fa, fb);
     // the lane's table: card k's packed ranks (byte j = kind j)
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) {
@@ -1579,7 +1579,7 @@ __device__ __forceinline__ void rmulti_list(const int64_t (&free)[kMaxCards][Q],
 }
 
 template <int Q, bool kBits, int L = 0>
-__device__ __forceinline__ void rmulti_lists(const int64_t (&free)[kMaxCards][Q], uint32_t node_ok,
+__device__ __forceinline__ void rmulti_lists(const int64_t* __restrict__ free_t, uint32_t node_ok,
                                              int32_t N, int32_t n, bool valid, int32_t P,
                                              const GasRMulti* __restrict__ rm,
                                              const int32_t* __restrict__ rw,
@@ -1591,18 +1591,19 @@ __device__ __forceinline__ void rmulti_lists(const int64_t (&free)[kMaxCards][Q]
   // slot L: list L / 2, class L % 2 (S = 2 + L % 2); counts of the multi lists [l][kClasses]
   constexpr int l = L / 2, S = 2 + L % 2;
   const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[l * kClasses + L % 2]);
-  rmulti_list<Q, l - 1, S, kBits>(free, node_ok, N, n, valid, rm + (int64_t)L * P,
+  rmulti_list<Q, l - 1, S, kBits>(free_t, node_ok, N, n, valid, rm + (int64_t)L * P,
                                   rw + (int64_t)L * P, srt, item0, cnt, bt, lds, stage, tab, res,
                                   fit);
   if constexpr (L + 1 < (Q + 1) * 2)
-    rmulti_lists<Q, kBits, L + 1>(free, node_ok, N, n, valid, P, rm, rw, srt,
+    rmulti_lists<Q, kBits, L + 1>(free_t, node_ok, N, n, valid, P, rm, rw, srt,
                                   item0 + (int64_t)cnt * (S == 2 ? 3 : 7), counts, bt, lds,
                                   stage, tab, res, fit);
 }
 
-// Pods with several selections: the two- and three-selection lists on ranks, then the lists of
-// four to eight selections (multi_list, sequential on int64 free values).  The two phases use
-// the same LDS slice of the wave.
+// Pods with several selections, two kernels so that each gets the registers of its own phase:
+// the two- and three-selection lists on ranks (ranked straight from free_t, no register copy of
+// the node's free values: 8 waves per SIMD instead of the sequential phase's 4), then the lists
+// of four to eight selections (sequential, with the node's free values in registers).
 template <int Q>
 struct MultiLds {
   static constexpr int kC = Q > 1 ? Q - 1 : 1;
@@ -1613,18 +1614,37 @@ struct MultiLds {
                                          ? sizeof(int64_t) * kC * kRankItems
                                          : sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB;
   static constexpr size_t kSeq = sizeof(int64_t) * kMaxCards * 64 * kC + kSeqOver;
-  static constexpr size_t kBytes = kRanked > kSeq ? kRanked : kSeq;
 };
 
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
+__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(5))) void gas_rfit_closed_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
-    const int32_t* __restrict__ rw, const GasRSeq* __restrict__ rq,
+    const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
+    const int32_t* __restrict__ counts, int32_t chunks, ResOut res, uint64_t* __restrict__ fit) {
+  __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kRanked / 16];
+  const BlockTile bt = block_tile(chunks);
+  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* w = reinterpret_cast<char*>(smem[wave]);
+  int64_t* lds = reinterpret_cast<int64_t*>(w);
+  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w + sizeof(int64_t) * Q * kRankItems);
+  uint32_t* tab = reinterpret_cast<uint32_t*>(stage + kRankMB);
+  rmulti_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
+                         tab, res, fit);
+}
+
+template <int Q, bool kBits>
+__global__ __launch_bounds__(kTpb) void gas_rfit_seq_kernel(
+    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
     const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
     ResOut res, uint64_t* __restrict__ fit) {
-  __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kBytes / 16];
+  __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kSeq / 16];
   const BlockTile bt = block_tile(chunks);
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
@@ -1633,20 +1653,14 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_multi_kernel(
   load_free_t<Q>(n, valid, N, free_t, free);
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char* w = reinterpret_cast<char*>(smem[wave]);
-  int64_t* lds = reinterpret_cast<int64_t*>(w);
-  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w + sizeof(int64_t) * Q * kRankItems);
-  uint32_t* tab = reinterpret_cast<uint32_t*>(stage + kRankMB);
-  rmulti_lists<Q, kBits>(free, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
-                         tab, res, fit);
-  __builtin_amdgcn_wave_barrier();
   // the sequential lists' sorted rows follow every two- and three-selection list's rows
   int64_t item_seq = 0;
 #pragma unroll
   for (int l = 0; l <= Q; ++l)
     item_seq += (int64_t)counts[l * kClasses] * 3 + (int64_t)counts[l * kClasses + 1] * 7;
-  seq_lists<Q, kBits>(free, w, node_ok, N, n, valid, P, multi, sels, rq, srt,
-                      __builtin_amdgcn_readfirstlane(item_seq), counts, bt, res, fit);
+  seq_lists<Q, kBits>(free, reinterpret_cast<char*>(smem[wave]), node_ok, N, n, valid, P, multi,
+                      sels, rq, srt, __builtin_amdgcn_readfirstlane(item_seq), counts, bt, res,
+                      fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -1917,9 +1931,12 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   case QQ * 2 + B:                                                                             \
     gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, ch_s, ResOut{d_res, ld_res}, d_fit);        \
-    gas_rfit_multi_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                 \
-        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, rseq, srt_m, multi, sels, counts + NL,      \
-        ch_m, ResOut{d_res, ld_res}, d_fit);                                                                   \
+    gas_rfit_closed_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
+        counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
+    gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                   \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,     \
+        counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
