@@ -407,8 +407,9 @@ def bench_gas(args, world, rank):
                                          .mean())},
         "roofline": {"bound": "hbm",
                      "kernel": "gas fit path: gas_prep_kernel, gas_rank_prep_kernel, "
-                               "gas_rfit_single_kernel, gas_rfit_multi_kernel and "
-                               "gas_fit_generic_kernel (two HIP events on the launch stream "
+                               "gas_rfit_single_kernel, gas_rfit_closed_kernel, "
+                               "gas_rfit_seq_kernel and gas_fit_generic_kernel (two HIP "
+                               "events on the launch stream "
                                "around the timed steps)",
                      "fit_launches_ms": k_ms / max(k_n, 1),
                      "achieved": achieved,

@@ -20,9 +20,9 @@
 // kernel files each pod under a list by selection count: one selection (the common case), two,
 // three, four to eight (more: the generic kernel), and by the kind it may skip (below).
 // Launches per fit: gas_prep_kernel (lists), gas_rank_prep_kernel (rank groups, below),
-// gas_rfit_single_kernel (one-selection pods), gas_rfit_multi_kernel (several selections:
-// two and three in closed form, four to eight in order), gas_fit_generic_kernel (shapes past
-// 8 cards or 8 selections).
+// gas_rfit_single_kernel (one-selection pods), gas_rfit_closed_kernel (two and three
+// selections in closed form), gas_rfit_seq_kernel (four to eight in order),
+// gas_fit_generic_kernel (shapes past 8 cards or 8 selections).
 //
 // Rank compression (the ranked fit section): every "need <= free" compare of a group of at
 // most 127 thresholds becomes a compare of 7-bit ranks, four cards of one kind per 32-bit

@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "profiles")
 TAS_PATH = ("tas_prep_kernel", "tas_eval_kernel")
 GAS_PATH = ("gas_minfree_kernel", "gas_prep_kernel", "gas_rank_prep_kernel",
-            "gas_rfit_single_kernel", "gas_rfit_multi_kernel", "gas_fit_generic_kernel")
+            "gas_rfit_single_kernel", "gas_rfit_closed_kernel", "gas_rfit_seq_kernel",
+            "gas_fit_generic_kernel")
 
 
 def short(name):
