@@ -1833,6 +1833,12 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     ctx->gas_counts = c;
     ctx->gas_counts_set = 0;
   }
+  // A fit on another stream than the previous one: order it after that fit, whose prep
+  // kernel zeroed this fit's list counts and whose kernels may still read the shared aux
+  // scratch (gas_limit_ev is recorded on every exit after a prep launch).
+  if (ctx->gas_have_last && ctx->gas_last_stream != s)
+    PAS_HIP(ctx, hipStreamWaitEvent(s, ctx->gas_limit_ev, 0));
+  if (Q < 1 || Q > PAS_GAS_MAX_RES) return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   if (N == 0 || n_pods == 0) {
     PAS_HIP(ctx, hipMemsetAsync(ctx->gas_limit, 0, sizeof(int64_t), s));
     if (d_side_count) PAS_HIP(ctx, hipMemsetAsync(d_side_count, 0, sizeof(int64_t), s));
@@ -1914,7 +1920,17 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
       multi, sels, counts, big_pods, n_big_pods, pod_steps, counts_next, kCounts, ctx->gas_limit,
       d_side_count);
+  PAS_HIP(ctx, hipGetLastError());
+  // the prep kernel ran: the other set is zeroed (on s) for the next fit, and every exit from
+  // here records gas_limit_ev on s for a next fit on another stream to wait on
   ctx->gas_counts_set = 1 - ctx->gas_counts_set;
+  ctx->gas_last_stream = s;
+  ctx->gas_have_last = true;
+  struct RecordOnExit {
+    hipEvent_t e;
+    hipStream_t s;
+    ~RecordOnExit() { (void)hipEventRecord(e, s); }
+  } done{ctx->gas_limit_ev, s};
   // grids: (node block, pod chunk) pairs, ~8192 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
   const int32_t nb_s = (N + kTpb - 1) / kTpb;
@@ -1979,7 +1995,6 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     gas_fit_generic_kernel<PAS_GAS_MAX_CARDS><<<kGenericBlocks, 64, 0, s>>>(ga);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
-  PAS_HIP(ctx, hipEventRecord(ctx->gas_limit_ev, s));
   return PAS_OK;
 }
 

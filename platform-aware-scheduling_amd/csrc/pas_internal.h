@@ -123,6 +123,8 @@ struct pas_ctx {
   // other for the next fit (no fill launch per fit); gas_counts_set = the set of the next fit
   int32_t* gas_counts = nullptr;
   int gas_counts_set = 0;
+  hipStream_t gas_last_stream = nullptr;  // stream of the last fit that launched its prep
+  bool gas_have_last = false;             // (the null stream is a valid one)
   hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)

@@ -171,6 +171,16 @@ __global__ void list_len_kernel(int32_t n_pods, Runs in, int32_t n_runs, int64_t
   out_len[p] = (int32_t)total;
 }
 
+// One shard: its run already is the cluster's list; copy the node ids, sentinels as -1.
+__global__ void single_run_kernel(int32_t n_pods, const int32_t* __restrict__ node, int64_t w,
+                                  int32_t* __restrict__ out_node, int64_t out_pitch) {
+  const int64_t t = (int64_t)blockIdx.x * kTpb + threadIdx.x;
+  if (t >= (int64_t)n_pods * w) return;
+  const int64_t p = t / w, i = t - p * w;
+  const int32_t n = node[t];
+  out_node[p * out_pitch + i] = n != kNodeNone ? n : -1;
+}
+
 }  // namespace
 
 int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t width,
@@ -186,6 +196,13 @@ int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t wi
   list_len_kernel<<<(n_pods + kTpb - 1) / kTpb, kTpb, 0, s>>>(n_pods, in, n_shards, width,
                                                              d_out_len);
   PAS_HIP(ctx, hipGetLastError());
+  if (rounds == 0) {  // one shard: no merge, no scratch
+    const int64_t n = (int64_t)n_pods * width;
+    single_run_kernel<<<(unsigned)((n + kTpb - 1) / kTpb), kTpb, 0, s>>>(n_pods, d_nodes, width,
+                                                                        d_out_node, out_ld);
+    PAS_HIP(ctx, hipGetLastError());
+    return PAS_OK;
+  }
   // the tile cuts of a round, then ping-pong rows [P][sp * width] for the rounds before the
   // last.  A round has n_pairs * (tiles + 1) <= sp * width / kTile + 2 * n_pairs cuts per pod.
   int64_t* key_buf[2] = {nullptr, nullptr};
@@ -224,8 +241,6 @@ int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t wi
     PAS_HIP(ctx, hipGetLastError());
     return PAS_OK;
   };
-  if (rounds == 0)  // one shard: its list is the cluster's; the pair (run 0, an empty run)
-    return round(in, width, 1, nullptr, d_out_node, out_ld);
   for (int32_t r = 0; r < rounds; ++r) {
     const int64_t w = (int64_t)width << r;
     const int32_t n_pairs = (int32_t)(sp >> (r + 1));

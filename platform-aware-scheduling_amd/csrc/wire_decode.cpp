@@ -608,16 +608,17 @@ class WorkerPool {
     } catch (...) {
       return false;
     }
+    uint32_t ep;
     {
       std::lock_guard<std::mutex> g(m_);
       task_ = &f;
       n_ = n;
-      next_.store(0);
       pending_ = n;
-      ++epoch_;
+      ep = (uint32_t)++epoch_;
+      next_.store((uint64_t)ep << 32);
     }
     cv_.notify_all();
-    work();
+    work(&f, n, ep);
     std::unique_lock<std::mutex> g(m_);
     done_.wait(g, [this] { return pending_ == 0; });
     task_ = nullptr;
@@ -626,9 +627,19 @@ class WorkerPool {
 
  private:
   WorkerPool() : pid_(getpid()) {}
-  void work() {
-    for (int i; (i = next_.fetch_add(1)) < n_;) {
-      (*task_)(i);
+  // Items of run `ep` only: next_ holds {epoch, next item}, so a worker still leaving an
+  // earlier run (its last item done, the caller already returned and started a new run) takes
+  // nothing from the new one; task and n are the copies the worker read under m_.
+  void work(const std::function<void(int)>* task, int n, uint32_t ep) {
+    for (;;) {
+      uint64_t v = next_.load();
+      int i;
+      do {
+        if ((uint32_t)(v >> 32) != ep) return;
+        i = (int)(uint32_t)v;
+        if (i >= n) return;
+      } while (!next_.compare_exchange_weak(v, v + 1));
+      (*task)(i);
       std::lock_guard<std::mutex> g(m_);
       if (--pending_ == 0) done_.notify_all();
     }
@@ -636,12 +647,16 @@ class WorkerPool {
   void loop() {
     uint64_t seen = 0;
     for (;;) {
+      const std::function<void(int)>* task;
+      int n;
       {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait(g, [&] { return epoch_ != seen && task_ != nullptr; });
         seen = epoch_;
+        task = task_;
+        n = n_;
       }
-      work();
+      work(task, n, (uint32_t)seen);
     }
   }
   const pid_t pid_;
@@ -650,7 +665,7 @@ class WorkerPool {
   std::vector<std::thread> workers_;
   const std::function<void(int)>* task_ = nullptr;
   int n_ = 0, pending_ = 0;
-  std::atomic<int> next_{0};
+  std::atomic<uint64_t> next_{0};  // {epoch (32 bits), next item (32 bits)}
   uint64_t epoch_ = 0;
 };
 

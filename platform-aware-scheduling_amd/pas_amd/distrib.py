@@ -7,14 +7,40 @@ The only cross-rank traffic is the timing protocol below: a barrier on both side
 timed region and an all-reduce(MAX) of the elapsed time.  The same code runs over RCCL
 ("nccl") on GPUs and over gloo on CPU in the tests.
 """
+import contextlib
 import os
 import time
+from collections import Counter
 
 import torch
 
+# torch.distributed calls made by this package, by name (the RCCL evidence of
+# tests/test_rccl.py; a counter add per collective)
+CALLS: Counter = Counter()
+_FORCE = [False]
 
-def setup(backend=None):
-    """Read RANK/LOCAL_RANK/WORLD_SIZE (torchrun) and join the process group when N > 1.
+
+@contextlib.contextmanager
+def force_collectives():
+    """Run every collective of this package through torch.distributed even at world size 1
+    (which otherwise short-cuts them): a world-1 RCCL group then executes the same
+    all_gather_into_tensor / all_to_all_single / all_reduce calls a multi-GPU job makes."""
+    old = _FORCE[0]
+    _FORCE[0] = True
+    try:
+        yield
+    finally:
+        _FORCE[0] = old
+
+
+def collective(world):
+    """True when a collective over `world` ranks must go through torch.distributed."""
+    return world > 1 or _FORCE[0]
+
+
+def setup(backend=None, force_group=False):
+    """Read RANK/LOCAL_RANK/WORLD_SIZE (torchrun) and join the process group when N > 1 (or
+    always, with force_group: a world-1 group for tests/test_rccl.py).
 
     backend None picks "nccl" (RCCL) when HIP devices are visible, else "gloo"."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -23,7 +49,7 @@ def setup(backend=None):
     gpu = backend != "gloo" and torch.cuda.is_available()
     if gpu:
         torch.cuda.set_device(local if world > 1 else 0)
-    if world > 1:
+    if world > 1 or force_group:
         import torch.distributed as dist
         if backend is None:
             backend = "nccl" if gpu else "gloo"
@@ -32,8 +58,8 @@ def setup(backend=None):
     return world, rank, local
 
 
-def teardown(world):
-    if world > 1:
+def teardown(world, force_group=False):
+    if world > 1 or force_group:
         import torch.distributed as dist
         dist.destroy_process_group()
 
@@ -44,26 +70,29 @@ def _device():
 
 
 def barrier(world):
-    if world > 1:
+    if collective(world):
         import torch.distributed as dist
+        CALLS["barrier"] += 1
         dist.barrier()
 
 
 def max_over_ranks(x, world):
-    if world == 1:
+    if not collective(world):
         return x
     import torch.distributed as dist
     t = torch.tensor([x], dtype=torch.float64, device=_device())
+    CALLS["all_reduce"] += 1
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
 def gather_objects(obj, world):
     """All ranks' `obj`, in rank order (tests and result checks only)."""
-    if world == 1:
+    if not collective(world):
         return [obj]
     import torch.distributed as dist
-    out = [None] * world
+    out = [None] * max(world, dist.get_world_size())
+    CALLS["all_gather_object"] += 1
     dist.all_gather_object(out, obj)
     return out
 

@@ -56,6 +56,28 @@ def _compact(item: bytes) -> bytes:
         return item
 
 
+class HandlerPanic(RuntimeError):
+    """The reference handler panicked: core.EvaluateRule indexed its operator map with an
+    unknown operator and called the nil function (operator.go:13-26).  net/http recovers a
+    handler's panic and closes the connection, so no status line and no body reach the
+    scheduler; in the deschedule controller's goroutine the panic ends the process."""
+
+
+def _raise_if_panic(e: "_lib.PasError"):
+    """PAS_EINVAL from a host entry's rule validation is the reference's panic."""
+    if e.code == _lib.PAS_EINVAL and "unknown operator" in str(e):
+        raise HandlerPanic(str(e)) from e
+    raise e
+
+
+def _op_code(op: str) -> int:
+    """pas_op of a TASPolicyRule operator; an unknown one is passed on as an invalid code: the
+    library skips it where its rule is never evaluated (metric not cached or cached with no
+    node, strategy.go:27-36) and returns PAS_EINVAL where EvaluateRule would run."""
+    code = parse_operator(op)
+    return code if code >= 0 else 3
+
+
 class MetricsExtender:
     """TAS extender: Filter / Prioritize / Bind (telemetryscheduler.go:36-244).
 
@@ -112,10 +134,7 @@ class MetricsExtender:
         metric, op, target = [], [], []
         for m, o, t in triples:
             metric.append(self.metric_index.get(m, -1))  # not cached: skipped (strategy.go:28-32)
-            code = parse_operator(o)
-            if code < 0:
-                raise ValueError(f"unknown operator {o!r}")  # the reference panics
-            op.append(code)
+            op.append(_op_code(o))
             target.append(int(t))
         return make_rules(metric, op, target)
 
@@ -128,12 +147,19 @@ class MetricsExtender:
             return 200, b""  # decode error: nothing written (:164-168)
         policy = self._policy(policy_ref)
         rules = (policy or {}).get("dontschedule") or []
-        if policy is None or not rules or info.n_req == 0:
-            return 404, b"null\n"  # nil FilterResult (:189-203)
+        if policy is None or not rules:
+            return 404, b"null\n"  # nil FilterResult (:189-198)
+        # Violated runs before the empty-list check (:199-203), so an unknown operator on a
+        # cached metric panics even for an empty node list
         r = self._rules(rules)
-        pass_out, _, _ = self.ctx.tas_eval(self.gen, r, np.array([0, len(r)], np.int32),
-                                           make_rules([-1], [0], [0]), cand[None, :],
-                                           _lib.PAS_TAS_FILTER)
+        try:
+            pass_out, _, _ = self.ctx.tas_eval(self.gen, r, np.array([0, len(r)], np.int32),
+                                               make_rules([-1], [0], [0]), cand[None, :],
+                                               _lib.PAS_TAS_FILTER)
+        except _lib.PasError as e:
+            _raise_if_panic(e)
+        if info.n_req == 0:
+            return 404, b"null\n"  # nil FilterResult (:200-203)
         # the shim's json.Marshal of each v1.Node (here: the compact re-encoding of the item)
         blobs = [_compact(body[o:o + n]) for o, n in spans]
         table = wire.NodeTable(self._names(body, info, idx), blobs)
@@ -289,10 +315,7 @@ class DescheduleEnforcer:
         for _, rules in strategies:
             for m, o, t in rules:
                 metric.append(self.metric_index.get(m, -1))
-                code = parse_operator(o)
-                if code < 0:
-                    raise ValueError(f"unknown operator {o!r}")  # the reference panics
-                op.append(code)
+                op.append(_op_code(o))  # unknown: skipped or the panic, as in filter
                 target.append(int(t))
             off.append(len(metric))
         self.rules = make_rules(metric, op, target)
@@ -302,7 +325,10 @@ class DescheduleEnforcer:
         """(totalViolations, {node name: PATCH body}) for the listed nodes' current labels;
         every node gets a body, "[]" when nothing changes (enforce.go:104-135)."""
         n, s = len(self.node_names), len(self.names)
-        viol = self.ctx.tas_violations(self.gen, self.rules, self.rule_off)
+        try:
+            viol = self.ctx.tas_violations(self.gen, self.rules, self.rule_off)
+        except _lib.PasError as e:
+            _raise_if_panic(e)
         labels = np.zeros((s, w64(n)), np.uint64)
         for i, lab in enumerate(node_labels):
             for j, name in enumerate(self.names):

@@ -29,6 +29,8 @@ from typing import Tuple
 
 import torch
 
+from .distrib import CALLS, collective
+
 
 def node_range(n_total: int, world: int, rank: int, align: int = 64) -> Tuple[int, int]:
     """Contiguous node range [n0, n1) of `rank`: shards are multiples of `align` nodes (the
@@ -42,16 +44,18 @@ def node_range(n_total: int, world: int, rank: int, align: int = 64) -> Tuple[in
 
 def _all_gather(t: torch.Tensor, world: int) -> torch.Tensor:
     """[world * t.numel()] concatenation of every rank's `t` (same shape on all ranks)."""
-    if world == 1:
+    if not collective(world):
         return t.reshape(-1)
     import torch.distributed as dist
     flat = t.contiguous().reshape(-1)
     if dist.get_backend() == "nccl":
         out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
+        CALLS["all_gather_into_tensor"] += 1
         dist.all_gather_into_tensor(out, flat)
         return out
     host = flat.cpu()
     parts = [torch.empty_like(host) for _ in range(world)]
+    CALLS["all_gather"] += 1
     dist.all_gather(parts, host)
     return torch.cat(parts).to(flat.device)
 
@@ -59,16 +63,18 @@ def _all_gather(t: torch.Tensor, world: int) -> torch.Tensor:
 def _all_to_all(t: torch.Tensor, world: int) -> torch.Tensor:
     """t [world, ...]: chunk t[q] goes to rank q; returns [world, ...] with out[s] = the chunk
     rank s sent to this rank."""
-    if world == 1:
+    if not collective(world):
         return t
     import torch.distributed as dist
     flat = t.contiguous()
     if dist.get_backend() == "nccl":
         out = torch.empty_like(flat)
+        CALLS["all_to_all_single"] += 1
         dist.all_to_all_single(out, flat)
         return out
     host = flat.cpu()
     parts = [torch.empty_like(host) for _ in range(world)]
+    CALLS["all_gather"] += 1
     dist.all_gather(parts, host)
     r = dist.get_rank()
     return torch.stack([part[r] for part in parts]).to(flat.device)
@@ -207,14 +213,18 @@ class ShardedTopK:
         return out_node, out_len
 
 
+_PAD = {}  # gather_violations' padded rows of a narrower last shard, by shape and device
+
+
 def gather_violations(viol_local: torch.Tensor, world: int, n_total: int) -> torch.Tensor:
     """Cluster violation bitmaps [S][W64(n_total)] from every rank's [S][W64_shard] sweep.
 
     Shard widths are static (node_range over n_total): every shard but the last has the
-    same word count wmax, the last is padded to wmax for the collective, and the
-    concatenation is trimmed to W64(n_total).  No size exchange runs per step."""
+    same word count wmax, the last is copied into a zero-padded buffer of that width (kept
+    across calls: its extra words stay zero) for the collective, and the concatenation is
+    trimmed to W64(n_total).  No size exchange and no allocation run per step."""
     s, w = viol_local.shape
-    if world == 1:
+    if not collective(world):
         return viol_local
     n0, n1 = node_range(n_total, world, 0)
     wmax = (n1 - n0 + 63) // 64
@@ -222,7 +232,11 @@ def gather_violations(viol_local: torch.Tensor, world: int, n_total: int) -> tor
         raise ValueError(f"shard has {w} words, node_range gives at most {wmax}")
     padded = viol_local
     if w < wmax:
-        padded = torch.zeros((s, wmax), dtype=viol_local.dtype, device=viol_local.device)
+        key = (s, wmax, viol_local.dtype, str(viol_local.device))
+        padded = _PAD.get(key)
+        if padded is None:
+            padded = _PAD[key] = torch.zeros((s, wmax), dtype=viol_local.dtype,
+                                             device=viol_local.device)
         padded[:, :w] = viol_local
     parts = _all_gather(padded, world).reshape(world, s, wmax)
     return parts.permute(1, 0, 2).reshape(s, world * wmax)[:, :(n_total + 63) // 64]

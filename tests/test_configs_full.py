@@ -164,12 +164,49 @@ def c5():
     return _C5()
 
 
+def c5_oracle_sample(c5, per_cell=24, total=1024):
+    """Pods of the C5 batch to check against the oracle: up to `per_cell` of every cell of
+    (prioritize op) x (selection class: 0 / 1 / 2 / 3 / 4-8 card selections, the GAS kernels'
+    lists) x (same-metric rule: none / on the prioritize metric / on it with the prioritize
+    op, i.e. excluding the head of the pod's order: the lazy kernel's range jump,
+    tas_gas_topk.hip), then evenly spaced pods up to `total`.  Returns (pods, cells)."""
+    tb, gb = c5.tbatch, c5.gbatch
+    P = c5.P
+    live = np.arange(gb.req.shape[1])[None, :] < gb.n_containers[:, None]
+    sel = np.where(live & ((gb.req_mask & 1) != 0), gb.req[:, :, wl.I915], 0).sum(axis=1)
+    cls = np.minimum(sel, 4)
+    pm, po = tb.prio["metric"], tb.prio["op"]
+    rm = tb.rules["metric"].reshape(P, -1)
+    ro = tb.rules["op"].reshape(P, -1)
+    same = rm == pm[:, None]
+    head = same & (ro == po[:, None]) & (po[:, None] != 2)
+    jump = np.where(head.any(axis=1), 2, np.where(same.any(axis=1), 1, 0))
+    rng = np.random.default_rng(0x5A)
+    picked, cells = [], {}
+    for op in range(3):
+        for c in range(5):
+            for j in range(3):
+                ids = np.flatnonzero((po == op) & (cls == c) & (jump == j))
+                cells[(op, c, j)] = len(ids)
+                if len(ids):
+                    picked.append(rng.choice(ids, size=min(per_cell, len(ids)), replace=False))
+    picked = np.unique(np.concatenate(picked))
+    rest = np.setdiff1d(np.linspace(0, P - 1, total, dtype=np.int64), picked)
+    pods = np.unique(np.concatenate([picked, rest[: max(0, total - len(picked))]]))
+    return pods, cells
+
+
 def test_c5_sample_vs_oracle_composition(c5, oracle):
-    """128 pods of the C5 batch: GPU merged lists (8 ranges, the lazy combined top-k bench.py
-    times) == oracle composition."""
+    """>= 1,024 pods of the C5 batch, chosen to cover every (prioritize op x selection class x
+    same-metric rule) cell (c5_oracle_sample): GPU merged lists (8 ranges, the lazy combined
+    top-k bench.py times) == oracle composition.  ~0.33 s of oracle work per pod (GAS fit and
+    TAS eval over 1M nodes), ~25 s on 16 threads."""
     nodes8, lens8, _ = c5.run_ranges(8, lazy=True)
     nodes8, lens8 = nodes8.cpu().numpy(), lens8.cpu().numpy()
-    sample = np.arange(0, c5.P, c5.P // 128)
+    sample, cells = c5_oracle_sample(c5)
+    assert len(sample) >= 1024
+    # every op x class x jump cell the batch has is in the sample
+    assert sum(1 for v in cells.values() if v) >= 40, cells
     t, g, tb, gb = c5.tsnap, c5.gsnap, c5.tbatch, c5.gbatch
 
     def compose(i):

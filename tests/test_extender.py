@@ -190,3 +190,74 @@ def test_gas_filter_unknown_kind(ctx):
     assert filt([{"gpu.intel.com/tiles": "1"}, {"gpu.intel.com/i915": "1"}]) == ["node-1"]
     assert filt([{"gpu.intel.com/i915": "1", "gpu.intel.com/memory.max": "1G"},
                  {"gpu.intel.com/i915": "1", "gpu.intel.com/foo": "0"}]) is None
+
+
+def _tas2(ctx, metrics, policies, gen):
+    """Two cached metrics: dummyMetric1 on both nodes, emptyMetric cached with no node."""
+    names = ["node A", "node B"]
+    v, pres, _ = sn.tas_snapshot_from_metrics(
+        {"dummyMetric1": {k: str(x) for k, x in metrics.items()}, "emptyMetric": {}}, names,
+        ["dummyMetric1", "emptyMetric"])
+    ctx.tas_snapshot_set(gen, v, pres)
+    return ext.MetricsExtender(ctx, gen, names, ["dummyMetric1", "emptyMetric"], policies)
+
+
+def test_filter_unknown_operator(ctx):
+    """An unknown operator is never evaluated on an uncached metric or a metric cached with no
+    node (dontschedule/strategy.go:27-36: ReadMetric error -> continue; an empty node map ->
+    no EvaluateRule call), so the filter result is the other rules' one.  On a cached metric
+    with nodes core.EvaluateRule calls a nil function (operator.go:13-26): the handler panics,
+    net/http drops the connection — HandlerPanic, nothing written."""
+    vals = {"node A": 50, "node B": 30}  # node A violates GreaterThan 40
+    want_failed, want_names = ["node A"], ["node B", ""]
+    for gen, bad in enumerate([("absentMetric", "Foo", 1), ("emptyMetric", "greaterthan", 1)],
+                              start=8500):
+        pol = {("default", "test-policy"): {
+            "scheduleonmetric": [("dummyMetric1", "GreaterThan", 0)],
+            "dontschedule": [bad, ("dummyMetric1", "GreaterThan", 40)]}}
+        m = _tas2(ctx, vals, pol, gen)
+        status, body = m.filter(args(**TWO_NODES))
+        assert status == 200
+        res = json.loads(body)
+        assert sorted(res["FailedNodes"]) == want_failed and res["NodeNames"] == want_names
+        # prioritize never evaluates dontschedule rules
+        assert m.prioritize(args(**TWO_NODES))[0] == 200
+    pol = {("default", "test-policy"): {
+        "scheduleonmetric": [("dummyMetric1", "GreaterThan", 0)],
+        "dontschedule": [("dummyMetric1", "GreaterThan", 40), ("dummyMetric1", "Foo", 1)]}}
+    m = _tas2(ctx, vals, pol, 8510)
+    with pytest.raises(ext.HandlerPanic):
+        m.filter(args(**TWO_NODES))
+    # Violated runs before the empty-node-list check (telemetryscheduler.go:199-203)
+    with pytest.raises(ext.HandlerPanic):
+        m.filter(args({"telemetry-policy": "test-policy"}, []))
+    # a scheduleonmetric rule with an unknown operator is not a panic: OrderedList leaves the
+    # list unsorted (operator.go:30-42), request order here (SURVEY.md A.3)
+    pol2 = {("default", "test-policy"): {"scheduleonmetric": [("dummyMetric1", "Foo", 0)]}}
+    m2 = _tas2(ctx, vals, pol2, 8511)
+    status, body = m2.prioritize(args(**TWO_NODES))
+    assert status == 200
+    assert [[h["Host"], h["Score"]] for h in json.loads(body)] == [["node A", 10], ["node B", 9]]
+
+
+def test_deschedule_unknown_operator(ctx):
+    """deschedule.Violated (deschedule/strategy.go:31-50) skips the same rules, and panics in
+    the controller goroutine on a cached, non-empty metric."""
+    names = ["node A", "node B"]
+    v, pres, _ = sn.tas_snapshot_from_metrics(
+        {"dummyMetric1": {"node A": "50", "node B": "30"}, "emptyMetric": {}}, names,
+        ["dummyMetric1", "emptyMetric"])
+    ctx.tas_snapshot_set(8520, v, pres)
+    strategies = [("pol-a", [("absentMetric", "Foo", 1), ("dummyMetric1", "GreaterThan", 40)]),
+                  ("pol-b", [("emptyMetric", "Bar", 1)])]
+    e = ext.DescheduleEnforcer(ctx, 8520, names, ["dummyMetric1", "emptyMetric"], strategies)
+    total, bodies = e.enforce([{}, {}])
+    # pol-a: node A violates; pol-b: nobody.  totalViolations counts the non-violated pairs
+    assert total == 3
+    assert json.loads(bodies["node A"]) == [
+        {"op": "add", "path": "/metadata/labels/pol-a", "value": "violating"}]
+    assert json.loads(bodies["node B"]) == []
+    e2 = ext.DescheduleEnforcer(ctx, 8520, names, ["dummyMetric1", "emptyMetric"],
+                                [("pol-c", [("dummyMetric1", "LessThen", 40)])])
+    with pytest.raises(ext.HandlerPanic):
+        e2.enforce([{}, {}])

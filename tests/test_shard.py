@@ -498,6 +498,43 @@ def test_list_merge_kernel(ctx, S, w):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("w", [5000, 70000])
+def test_list_merge_single_shard_fresh_context(w):
+    """One shard (no merge round) on a context whose merge scratch was never grown: the run is
+    copied with sentinels as -1, nothing written past the list's row (the single-run
+    case once sized its cut buffer for width/1024 tiles but launched 2·width/1024)."""
+    import pas_amd
+    rng = np.random.default_rng(w)
+    P = 5
+    keys = np.full((1, P, w), np.iinfo(np.int64).max, np.int64)
+    nodes = np.full((1, P, w), np.iinfo(np.int32).max, np.int32)
+    for p in range(P):
+        ln = [0, w, int(rng.integers(0, w + 1)), 1, w - 1][p]
+        k = np.sort(rng.integers(-3, 3, size=ln).astype(np.int64))
+        keys[0, p, :ln] = k
+        nodes[0, p, :ln] = rng.permutation(w)[:ln].astype(np.int32)
+        o = np.lexsort((nodes[0, p, :ln], k))
+        nodes[0, p, :ln] = nodes[0, p, :ln][o]
+    want = merge_full(keys, nodes)
+    ld = w + 9
+    c = pas_amd.Context(0)
+    try:
+        out = torch.full((P + 1, ld), -7, dtype=torch.int32, device="cuda")
+        ln = torch.empty(P, dtype=torch.int32, device="cuda")
+        c.list_merge_device(P, 1, w, _dev(keys), _dev(nodes), out, ln, out_ld=ld)
+        c.synchronize()
+    finally:
+        c.close()
+    got, got_l = out.cpu().numpy(), ln.cpu().numpy()
+    for p in range(P):
+        m = len(want[p])
+        assert got_l[p] == m
+        np.testing.assert_array_equal(got[p, :m], want[p])
+        assert (got[p, m:w] == -1).all() and (got[p, w:] == -7).all()
+    assert (got[P] == -7).all()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_full_list_over_shards_equals_global(ctx, oracle, world):
     """Whole-shard device records of every shard, merged on device, equal the oracle's
