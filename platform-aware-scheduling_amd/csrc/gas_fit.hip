@@ -44,6 +44,9 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+#ifndef PAS_GAS_CONCURRENT
+#define PAS_GAS_CONCURRENT 2  // 1: multi-selection kernels on a side stream; 2: the single one
+#endif
 #ifndef PAS_GAS_BLOCKS_SINGLE
 #define PAS_GAS_BLOCKS_SINGLE 8192  // target blocks of a fit grid: (node block, pod chunk) pairs
 #endif
@@ -1942,22 +1945,46 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   PAS_HIP(ctx, hipGetLastError());
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
+  // streams of the single-selection (ss) and the multi-selection kernels (ms): disjoint pods,
+  // disjoint result rows; a side stream is forked from s here and joined before the generic
+  // kernel
+  hipStream_t ss = s, ms = s;
+  if (PAS_GAS_CONCURRENT) {
+    if (!ctx->gas_side) {
+      PAS_HIP(ctx, hipStreamCreateWithFlags(&ctx->gas_side, hipStreamNonBlocking));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_fork, hipEventDisableTiming));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_join, hipEventDisableTiming));
+    }
+    PAS_HIP(ctx, hipEventRecord(ctx->gas_fork, s));
+    PAS_HIP(ctx, hipStreamWaitEvent(ctx->gas_side, ctx->gas_fork, 0));
+    (PAS_GAS_CONCURRENT == 1 ? ms : ss) = ctx->gas_side;
+  }
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
-    gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, s>>>(                                \
-        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, ch_s, ResOut{d_res, ld_res}, d_fit);        \
-    gas_rfit_closed_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                \
+    if (PAS_GAS_CONCURRENT != 2)                                                               \
+      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
+          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
+    gas_rfit_closed_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, ms>>>(                               \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
         counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
-    gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, s>>>(                                   \
+    gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, ms>>>(                                  \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,     \
         counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
+    if (PAS_GAS_CONCURRENT == 2)                                                               \
+      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
+          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
 #undef PAS_GAS_CASE
     default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
+  }
+  if (PAS_GAS_CONCURRENT) {
+    PAS_HIP(ctx, hipEventRecord(ctx->gas_join, ctx->gas_side));
+    PAS_HIP(ctx, hipStreamWaitEvent(s, ctx->gas_join, 0));
   }
   // the wide shapes: the lists' lengths are on the device, so the grid is fixed and threads
   // past the work return at once

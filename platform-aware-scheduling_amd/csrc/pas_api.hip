@@ -200,6 +200,9 @@ void pas_destroy(pas_ctx* ctx) {
   if (ctx->gas_counts) (void)hipFree(ctx->gas_counts);
   if (ctx->tas_gpass) (void)hipFree(ctx->tas_gpass);
   if (ctx->gas_limit_ev) (void)hipEventDestroy(ctx->gas_limit_ev);
+  if (ctx->gas_fork) (void)hipEventDestroy(ctx->gas_fork);
+  if (ctx->gas_join) (void)hipEventDestroy(ctx->gas_join);
+  if (ctx->gas_side) (void)hipStreamDestroy(ctx->gas_side);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }

@@ -126,6 +126,9 @@ struct pas_ctx {
   hipStream_t gas_last_stream = nullptr;  // stream of the last fit that launched its prep
   bool gas_have_last = false;             // (the null stream is a valid one)
   hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
+  // a side stream for fit kernels running beside each other (forked / joined per fit)
+  hipStream_t gas_side = nullptr;
+  hipEvent_t gas_fork = nullptr, gas_join = nullptr;
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;

@@ -88,6 +88,43 @@ __global__ __launch_bounds__(256) void k_add64(const int64_t* in, uint64_t* out,
   out[blockIdx.x * 256 + threadIdx.x] = v[0] ^ v[1] ^ v[2] ^ v[3];
 }
 
+// 32-bit ALU ops of the ranked kernels (v_sub_u32, v_bitop3_b32, v_and_or_b32): 16
+// independent instructions per group over 8 accumulators
+__global__ __launch_bounds__(256) void k_sub32(const int64_t* in, uint64_t* out, int64_t s) {
+  uint32_t v[8];
+  for (int i = 0; i < 8; ++i) v[i] = (uint32_t)in[threadIdx.x] + i;
+  const uint32_t s32 = (uint32_t)s;
+  for (int it = 0; it < ITERS; ++it) {
+#define C(i) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(v[i & 7]) : "s"(s32 + i));
+    REP16(C)
+#undef C
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = v[0] ^ v[1] ^ v[2] ^ v[3] ^ v[4] ^ v[5] ^ v[6] ^ v[7];
+}
+__global__ __launch_bounds__(256) void k_bitop3(const int64_t* in, uint64_t* out, int64_t s) {
+  uint32_t v[8];
+  for (int i = 0; i < 8; ++i) v[i] = (uint32_t)in[threadIdx.x] + i;
+  const uint32_t s32 = (uint32_t)s;
+  for (int it = 0; it < ITERS; ++it) {
+#define C(i) \
+  asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x80" : "+v"(v[i & 7]) : "s"(s32 + i), "v"(v[(i + 3) & 7]));
+    REP16(C)
+#undef C
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = v[0] ^ v[1] ^ v[2] ^ v[3] ^ v[4] ^ v[5] ^ v[6] ^ v[7];
+}
+// a dependent chain per wave (one accumulator): the single-wave latency bound
+__global__ __launch_bounds__(256) void k_sub32_chain(const int64_t* in, uint64_t* out, int64_t s) {
+  uint32_t v = (uint32_t)in[threadIdx.x];
+  const uint32_t s32 = (uint32_t)s;
+  for (int it = 0; it < ITERS; ++it) {
+#define C(i) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(v) : "s"(s32 + i));
+    REP16(C)
+#undef C
+  }
+  out[blockIdx.x * 256 + threadIdx.x] = v;
+}
+
 typedef void (*Kern)(const int64_t*, uint64_t*, int64_t);
 
 int main(int argc, char** argv) {
@@ -108,7 +145,10 @@ int main(int argc, char** argv) {
             {"v_cmp_le_i32 + s_xor", k_cmp32, 16, 16},
             {"v_cmp_le_i64 only", k_cmp64_nosalu, 16, 0},
             {"v_cndmask_b32", k_cndmask, 16, 0},
-            {"v_lshl_add_u64", k_add64, 16, 0}};
+            {"v_lshl_add_u64", k_add64, 16, 0},
+            {"v_sub_u32 (8 chains)", k_sub32, 16, 0},
+            {"v_bitop3_b32 (8 chains)", k_bitop3, 16, 0},
+            {"v_sub_u32 (1 chain)", k_sub32_chain, 16, 0}};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);

@@ -98,7 +98,10 @@ def test_filter_nil_results(ctx):
     assert m.filter(args({"useless-label": "x"}, ["node A"])) == (404, b"null\n")
     m2 = tas(ctx, {"node A": 10, "node B": 30}, TEST_POLICY2, 8121)
     assert m2.filter(args(**TWO_NODES)) == (404, b"null\n")
-    assert m.filter(args({"telemetry-policy": "test-policy"}, [])) == (404, b"null\n")
+    # an empty node list: Violated still runs first (telemetryscheduler.go:199-203), on the
+    # resident snapshot (m2 replaced m's)
+    m4 = tas(ctx, {"node A": 10, "node B": 30}, TEST_POLICY1, 8123)
+    assert m4.filter(args({"telemetry-policy": "test-policy"}, [])) == (404, b"null\n")
     # no dontschedule strategy
     m3 = tas(ctx, {"node A": 10}, {("default", "test-policy"): {
         "scheduleonmetric": [("dummyMetric1", "GreaterThan", 0)]}}, 8122)
@@ -209,7 +212,8 @@ def test_filter_unknown_operator(ctx):
     with nodes core.EvaluateRule calls a nil function (operator.go:13-26): the handler panics,
     net/http drops the connection — HandlerPanic, nothing written."""
     vals = {"node A": 50, "node B": 30}  # node A violates GreaterThan 40
-    want_failed, want_names = ["node A"], ["node B", ""]
+    # NodeNames: strings.Split(availableNodeNames, " ") of "node B " (telemetryscheduler.go:213)
+    want_failed, want_names = ["node A"], ["node", "B", ""]
     for gen, bad in enumerate([("absentMetric", "Foo", 1), ("emptyMetric", "greaterthan", 1)],
                               start=8500):
         pol = {("default", "test-policy"): {
