@@ -535,14 +535,15 @@ def bench_deschedule(args, world, rank):
 
 # ------------------------------------------------------------------------------- C5
 
-def c5_setup(args, world, rank):
-    """The C5 workload on this rank: its node range of the cluster as resident TAS and GAS
-    snapshots (generations 1 and 2), the pod batch on the device."""
+def c5_setup(args, world, rank, whole=False, host=None):
+    """The C5 workload on this rank: its node range of the cluster (whole: every node, for
+    the pod-sharded split) as resident TAS and GAS snapshots (generations 1 and 2), the pod
+    batch on the device.  host: a dict that receives the host batches (tbatch, gbatch)."""
     P, N, M, R = args.pods, args.nodes, args.metrics, args.rules - 1
     ctx = pas_amd.Context(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
-    n0, n1 = shard.node_range(N, world, rank)
+    n0, n1 = (0, N) if whole else shard.node_range(N, world, rank)
     tsnap = wl.make_tas_snapshot(N, M, seed=0xC5)
     v, pres = shard_tas(tsnap, n0, n1)
     ctx.tas_snapshot_set_device(1, n1 - n0, M, dev(v), dev(pres.view(np.int64)), stream)
@@ -558,6 +559,8 @@ def c5_setup(args, world, rank):
          "prio": dev(tbatch.prio.view(np.uint8)), "req": dev(gbatch.req),
          "mask": dev(gbatch.req_mask.view(np.int32)), "ncont": dev(gbatch.n_containers),
          "n_rules": len(tbatch.rules), "C": gbatch.req.shape[1]}
+    if host is not None:
+        host["tbatch"], host["gbatch"] = tbatch, gbatch
     return ctx, stream, n0, n1, t
 
 
@@ -623,10 +626,12 @@ def bench_c5(args, world, rank):
 
 def node_sharded_record(args, world, rank):
     """The north_star's 1M-node scaling point, run inside a multi-GPU bench.py call: the C5
-    step (64k pods x 1M nodes, node-sharded over the ranks, RCCL all-gather + merge) and the
-    C4 deschedule sweep (1M nodes x 64 rules + all-gather of the violation bitmaps), each
+    step (64k pods x 1M nodes) split two ways -- node-sharded over the ranks (RCCL all-gather
+    + merge every step; the path for clusters past one GPU's memory) and pod-sharded over a
+    replicated snapshot (no collective in the step; lists gathered once at the end) -- and
+    the C4 deschedule sweep (1M nodes x 64 rules + all-gather of the violation bitmaps), each
     timed with the same barrier / max-over-ranks protocol.  The driver's 1/2/4/8 runs of
-    bench.py then carry the node-sharded curve without a --workload flag."""
+    bench.py then carry both curves without a --workload flag (DESIGN.md §6 cost model)."""
     import argparse as _ap
     import torch.distributed as dist
     rec = {"nodes": 1_000_000, "world_size": world,
@@ -644,12 +649,34 @@ def node_sharded_record(args, world, rank):
     digest = (int(result["nodes"].to(torch.int64).sum().item()),
               int(result["len"].to(torch.int64).sum().item()))
     rec["c5_topk"] = {"pods": a.pods, "nodes_per_gpu": n1 - n0, "topk": a.topk,
-                      "ms_per_step": el / a.steps * 1e3,
+                      "split": "node-sharded", "ms_per_step": el / a.steps * 1e3,
                       "pods_per_s": a.pods * a.steps / el, "scaling": "strong",
                       "entries": digest[1],
                       "ranks_agree": len(set(distrib.gather_objects(digest, world))) == 1}
+    node_lists = (result["nodes"].clone(), result["len"].clone())
     ctx.close()
     del topk, t, result
+    torch.cuda.empty_cache()
+    # the same step split by pod over the whole cluster on every rank
+    host = {}
+    ctx, stream, _, _, t = c5_setup(a, world, rank, whole=True, host=host)
+    tb, gb = host["tbatch"], host["gbatch"]
+    ps = shard.PodShardedTopK(ctx, a.topk, world, rank, a.pods, tb.rules, tb.rule_off, tb.prio,
+                              gb.req, gb.req_mask, gb.n_containers)
+    del t
+    for _ in range(a.warmup):
+        ps.run(1, 2, wl.I915, stream)
+    el = timed_steps(lambda: ps.run(1, 2, wl.I915, stream), a.steps, 0, world)
+    pods_nodes, pods_lens = ps.gather()
+    same = bool(torch.equal(pods_nodes, node_lists[0]) and torch.equal(pods_lens, node_lists[1]))
+    rec["c5_topk_pod_sharded"] = {
+        "pods": a.pods, "pods_per_gpu": ps.p1 - ps.p0, "nodes_per_gpu": a.nodes, "topk": a.topk,
+        "split": "pod-sharded (snapshot replicated, lists gathered once after the timed steps)",
+        "ms_per_step": el / a.steps * 1e3, "pods_per_s": a.pods * a.steps / el,
+        "scaling": "strong",
+        "equals_node_sharded": all(distrib.gather_objects(same, world))}
+    ctx.close()
+    del ps
     torch.cuda.empty_cache()
     d = bench_deschedule(a, world, rank)
     rec["c4_deschedule"] = {"nodes_per_gpu": d["config"]["nodes_per_gpu"],

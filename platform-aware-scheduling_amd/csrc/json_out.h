@@ -28,16 +28,20 @@ struct JsonOut {
     pos += n;
   }
   void lit(const char* s) { raw(s, (int64_t)std::strlen(s)); }
+  template <size_t N>
+  void lit(const char (&s)[N]) {  // a string literal: its length at compile time
+    raw(s, (int64_t)N - 1);
+  }
   void integer(int64_t v) {
     char tmp[24];
-    int n = 0;
+    int n = 24;
     uint64_t u = v < 0 ? (uint64_t)0 - (uint64_t)v : (uint64_t)v;
     do {
-      tmp[n++] = (char)('0' + u % 10);
+      tmp[--n] = (char)('0' + u % 10);
       u /= 10;
     } while (u);
-    if (v < 0) put('-');
-    while (n) put(tmp[--n]);
+    if (v < 0) tmp[--n] = '-';
+    raw(tmp + n, 24 - n);
   }
 
   // UTF-8 sequence length at s (1..4, within the `avail` bytes left) if valid per Go's
@@ -69,12 +73,80 @@ struct JsonOut {
   // String body (no quotes) of the NUL-terminated s.
   void str_body(const char* s) { str_body_n(s, (int64_t)std::strlen(s)); }
 
-  // String body (no quotes) of the n bytes at s.
+  // ASCII bytes that are copied as they are (no escape): 0x20-0x7F but '"' '\\' '<' '>' '&'.
+  struct PlainTable {
+    bool v[256];
+    constexpr PlainTable() : v() {
+      for (int c = 0x20; c < 0x80; ++c)  // DEL (0x7F) is not escaped by Go
+        v[c] = c != '"' && c != '\\' && c != '<' && c != '>' && c != '&';
+    }
+  };
+  static bool plain(unsigned char c) {
+    static constexpr PlainTable t{};
+    return t.v[c];
+  }
+
+  // String body (no quotes) of the n bytes at s: runs of plain bytes are copied whole, every
+  // other byte takes the escape path below.  When the worst case (6 output bytes per input
+  // byte) fits the buffer, the body is written through a local pointer (stores through a
+  // char pointer may alias `pos`, which would otherwise be reloaded and stored per byte).
   void str_body_n(const char* s, int64_t n) {
     static const char hex[] = "0123456789abcdef";
     const unsigned char* p = reinterpret_cast<const unsigned char*>(s);
     const unsigned char* end = p + n;
+    if (pos <= cap && cap - pos >= 6 * n) {
+      char* w = buf + pos;
+      while (p < end) {
+        const unsigned char c = *p;
+        if (plain(c)) {
+          *w++ = (char)c;
+          ++p;
+          continue;
+        }
+        if (c < 0x80) {
+          *w++ = '\\';
+          switch (c) {
+            case '"': *w++ = '"'; break;
+            case '\\': *w++ = '\\'; break;
+            case '\n': *w++ = 'n'; break;
+            case '\r': *w++ = 'r'; break;
+            case '\t': *w++ = 't'; break;
+            default:
+              std::memcpy(w, "u00", 3);
+              w[3] = hex[c >> 4];
+              w[4] = hex[c & 15];
+              w += 5;
+          }
+          ++p;
+          continue;
+        }
+        uint32_t r = 0;
+        const int len = utf8_len(p, end - p, &r);
+        if (len == 0) {
+          std::memcpy(w, "\\ufffd", 6);
+          w += 6;
+          ++p;
+        } else if (r == 0x2028 || r == 0x2029) {
+          std::memcpy(w, r == 0x2028 ? "\\u2028" : "\\u2029", 6);
+          w += 6;
+          p += len;
+        } else {
+          std::memcpy(w, p, (size_t)len);
+          w += len;
+          p += len;
+        }
+      }
+      pos = w - buf;
+      return;
+    }
     while (p < end) {
+      const unsigned char* run = p;
+      while (run < end && plain(*run)) ++run;
+      if (run > p) {
+        raw(reinterpret_cast<const char*>(p), run - p);
+        p = run;
+        if (p == end) break;
+      }
       const unsigned char c = *p;
       if (c < 0x80) {
         switch (c) {

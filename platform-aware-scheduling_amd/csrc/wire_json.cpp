@@ -58,7 +58,8 @@ void failed_nodes(pas::JsonOut& o, std::vector<const char*>& names, const char* 
 // counting pass for the size, then the writing pass), and the pieces are appended in order.
 template <class F>
 void encode_items(pas::JsonOut& o, int64_t n, char sep, int64_t bytes_per_item, F&& encode) {
-  const int T = n >= 4096 ? (int)std::min<int64_t>(pas::host_threads_for(n * bytes_per_item),
+  // one thread per 256 KiB of output: the items' scattered reads, not the bytes, set the pace
+  const int T = n >= 4096 ? (int)std::min<int64_t>(pas::host_threads_for(4 * n * bytes_per_item),
                                                    n / 1024)
                           : 1;
   auto range = [&](pas::JsonOut& w, int64_t i0, int64_t i1) {
@@ -74,11 +75,18 @@ void encode_items(pas::JsonOut& o, int64_t n, char sep, int64_t bytes_per_item, 
   std::vector<std::string> part((size_t)T);
   auto run = [&](int t) {
     const int64_t i0 = n * t / T, i1 = n * (t + 1) / T;
-    pas::JsonOut count{nullptr, 0};
-    range(count, i0, i1);
-    part[(size_t)t].resize((size_t)count.pos);
-    pas::JsonOut w{part[(size_t)t].data(), count.pos};
+    // one pass into a buffer of twice the estimate; a range that outgrows it (long names,
+    // escapes) is encoded again at its counted length
+    std::string& b = part[(size_t)t];
+    b.resize((size_t)(2 * bytes_per_item * (i1 - i0) + 4096));
+    pas::JsonOut w{&b[0], (int64_t)b.size()};
     range(w, i0, i1);
+    if (w.pos > (int64_t)b.size()) {
+      b.resize((size_t)w.pos);
+      pas::JsonOut again{&b[0], (int64_t)b.size()};
+      range(again, i0, i1);
+    }
+    b.resize((size_t)w.pos);
   };
   if (!pas::host_parallel(T, run)) {
     range(o, 0, n);
@@ -110,6 +118,9 @@ int pas_encode_host_priority_list(int32_t len, const int32_t* order, const char*
   pas::JsonOut o{buf, cap};
   o.put('[');
   encode_items(o, len, ',', 40, [&](pas::JsonOut& w, int64_t i) {
+    // the names are read in list order, i.e. scattered over the table: fetch ahead
+    if (i + 64 < len) __builtin_prefetch(&names[order[i + 64]]);
+    if (i + 24 < len) __builtin_prefetch(names[order[i + 24]]);
     w.lit("{\"Host\":");
     w.str(names[order[i]]);
     w.lit(",\"Score\":");

@@ -213,6 +213,67 @@ class ShardedTopK:
         return out_node, out_len
 
 
+class PodShardedTopK:
+    """The combined TAS + GAS top-k (BASELINE configs[4]) split by pod instead of by node: every
+    rank holds the WHOLE cluster as its resident TAS and GAS snapshots (1M nodes x 64 metrics
+    is ~3 GB with the orders: it fits one GPU many times over) and evaluates the pods of its
+    pod_slice only, so a step has no data-path collective and each rank's kernel walks P / N
+    pods.  Each pod's list is final on the rank that owns it (a pod is one scheduling request,
+    telemetryscheduler.go:184-225, gpuscheduler/scheduler.go:449-482); `gather` assembles
+    every rank's slice once, at the end.  Node sharding (ShardedTopK) stays the path for a
+    cluster that exceeds one GPU's memory.
+
+    rules / rule_off / prio / req / mask / ncont: host arrays of the WHOLE batch; the rank's
+    slice is cut out here (rule_off rebased), once."""
+
+    def __init__(self, ctx, k: int, world: int, rank: int, n_pods: int, rules, rule_off, prio,
+                 req, mask, ncont, device="cuda"):
+        import numpy as np
+        self.ctx, self.k, self.world, self.rank = ctx, k, world, rank
+        self.n_pods = n_pods
+        self.p0, self.p1 = pod_slice(n_pods, world, rank)
+        self.per = (n_pods + world - 1) // world
+        p0, p1 = self.p0, self.p1
+        r0, r1 = int(rule_off[p0]), int(rule_off[p1])
+
+        def dev(a):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(device)
+        self.n_rules = r1 - r0
+        self.rules = dev(rules[r0:r1].view(np.uint8))
+        self.off = dev((rule_off[p0:p1 + 1] - r0).astype(np.int32))
+        self.prio = dev(prio[p0:p1].view(np.uint8))
+        self.req, self.ncont = dev(req[p0:p1]), dev(ncont[p0:p1])
+        self.mask = dev(mask[p0:p1].view(np.int32))
+        self.C = req.shape[1]
+        n = p1 - p0
+        self.key = torch.empty((n, k), dtype=torch.int64, device=device)
+        self.node = torch.empty((n, k), dtype=torch.int32, device=device)
+        self.len = torch.empty((n,), dtype=torch.int32, device=device)
+        # the slice padded to `per` rows for the final gather
+        self.out_node = torch.full((self.per, k), -1, dtype=torch.int32, device=device)
+        self.out_len = torch.zeros((self.per,), dtype=torch.int32, device=device)
+
+    def run(self, tas_gen: int, gas_gen: int, i915_index: int, stream=None):
+        """One step: the rank's pods' first k (their final lists, node ids, -1 past len)."""
+        n = self.p1 - self.p0
+        if n:
+            self.ctx.tas_gas_topk_device(tas_gen, gas_gen, n, self.n_rules, self.rules, self.off,
+                                         self.prio, None, self.C, i915_index, self.req, self.mask,
+                                         self.ncont, self.k, 0, self.key, self.node, self.len,
+                                         stream)
+            # records -> node lists (one shard: the merge only maps the sentinels to -1)
+            self.ctx.topk_merge_device(n, self.k, 1, self.key, self.node, self.out_node[:n],
+                                       self.out_len[:n], stream)
+        return self.out_node[:n], self.out_len[:n]
+
+    def gather(self):
+        """Every pod's list on every rank ([P][k], [P]): one all-gather of the slices (end of
+        the job, not per step)."""
+        nodes = _all_gather(self.out_node, self.world).view(-1, self.k)[:self.n_pods]
+        lens = _all_gather(self.out_len, self.world)[:self.n_pods]
+        return nodes, lens
+
+
 _PAD = {}  # gather_violations' padded rows of a narrower last shard, by shape and device
 
 

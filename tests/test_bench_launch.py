@@ -86,3 +86,7 @@ def test_multi_rank_bench_carries_node_sharded_record():
     assert c5["ms_per_step"] > 0 and 0 < c5["entries"] <= 1024 * 16
     c4 = ns["c4_deschedule"]
     assert c4["nodes_per_gpu"] == 30016 and c4["ms_per_step"] > 0
+    # the same C5 step split by pod over the replicated cluster: same lists on every rank
+    ps = ns["c5_topk_pod_sharded"]
+    assert ps["pods"] == 1024 and ps["pods_per_gpu"] == 512 and ps["nodes_per_gpu"] == 60000
+    assert ps["ms_per_step"] > 0 and ps["equals_node_sharded"] is True

@@ -129,3 +129,18 @@ def test_node_names_with_spaces_threads(table):
     assert got["NodeNames"] == want_names.split(" ")
     for threads in (2, 16):
         assert encode(t2, req, row, threads) == one
+
+
+def test_host_priority_list_threads_past_the_estimate():
+    # names far longer than the per-item estimate (40 B) and full of escapes (6 output bytes
+    # per input byte): every thread's range outgrows its first buffer and is encoded again
+    names = [("<" * 40) + f"-{i}-" + ("\u2028" * 8) for i in range(9000)]
+    table = wire.NodeTable(names)
+    order = np.random.default_rng(9).permutation(9000).astype(np.int32)
+    one = _with_threads(1, lambda: wire.host_priority_list(order, table))
+    want = (json.dumps([{"Host": names[o], "Score": 10 - i} for i, o in enumerate(order)],
+                       separators=(",", ":"), ensure_ascii=False)
+            .replace("<", "\\u003c").replace("\u2028", "\\u2028").encode() + b"\n")
+    assert one == want
+    for threads in (2, 8, 16):
+        assert _with_threads(threads, lambda: wire.host_priority_list(order, table)) == one
