@@ -28,12 +28,13 @@ constexpr int64_t kRunsFrom = PAS_GAS_MAX_SELECTIONS;
 // per-GPU capacity cap: take t + 1 passes checkResourceCapacity iff every requested kind has
 // r >= 0, cap > 0, w + t·r >= 0 without overflow and w + t·r <= cap (free-capacity form).  A
 // request of a kind outside the snapshot has no capacity key (:349-354): no take.
+template <int QW = PAS_GAS_MAX_RES>
 __device__ __forceinline__ int64_t card_takes(int32_t Q, uint32_t m, const int64_t* r,
                                               const int64_t* cap, const int64_t* w) {
   if (m & PAS_REQ_UNKNOWN_KIND) return 0;
   int64_t t = INT64_MAX;
 #pragma unroll
-  for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+  for (int q = 0; q < QW; ++q) {
     if (q >= Q || !((m >> q) & 1u)) continue;
     if (r[q] < 0 || cap[q] <= 0 || w[q] < 0 || w[q] > cap[q]) return 0;
     if (r[q] > 0) t = min(t, (cap[q] - w[q]) / r[q]);
@@ -44,9 +45,9 @@ __device__ __forceinline__ int64_t card_takes(int32_t Q, uint32_t m, const int64
 // The container's num selections as runs over cards 0 .. ncard-1 (w: the working copy
 // [card][kind], updated); emit(card, takes) per run.  False = a selection fits no card
 // (errWontFit, :249-253).  num >= 1.
-template <int KMAX, class Emit>
+template <int KMAX, int QW = PAS_GAS_MAX_RES, class Emit>
 __device__ bool container_runs(int32_t Q, uint32_t m, const int64_t* r, int64_t num,
-                               const int64_t* cap, int64_t (&w)[KMAX][PAS_GAS_MAX_RES],
+                               const int64_t* cap, int64_t (&w)[KMAX][QW],
                                int32_t ncard, Emit emit) {
   // unrolled for register-resident copies (KMAX <= 16), so w is never indexed dynamically
   constexpr int kUnroll = KMAX <= 16 ? KMAX : 1;
@@ -54,11 +55,11 @@ __device__ bool container_runs(int32_t Q, uint32_t m, const int64_t* r, int64_t 
 #pragma unroll kUnroll
   for (int k = 0; k < KMAX; ++k) {
     if (k < ncard && rem > 0) {
-      const int64_t t = min(rem, card_takes(Q, m, r, cap, w[k]));
+      const int64_t t = min(rem, card_takes<QW>(Q, m, r, cap, w[k]));
       if (t > 0) {
         // t·r[q] <= cap[q] - w[q]: no overflow
 #pragma unroll
-        for (int q = 0; q < PAS_GAS_MAX_RES; ++q)
+        for (int q = 0; q < QW; ++q)
           if (q < Q && ((m >> q) & 1u)) w[k][q] += t * r[q];
         rem -= t;
         emit(k, t);

@@ -101,8 +101,10 @@ __device__ __forceinline__ bool kind_fits(int64_t need, int64_t cap, int64_t use
 // per container getPerGPUResourceRequest (:180-190) and numI915 selections (:192-198), each
 // the first card in lexicographic order passing checkResourceCapacity, whose usage then
 // takes the request (addRM).  KMAX: the snapshot's cards per node fit in registers
-// (fully unrolled) for KMAX <= 16; the wide case keeps the copy in scratch.
-template <int KMAX>
+// (fully unrolled) for KMAX <= 16; the wide case keeps the copy in scratch.  QW: the kinds
+// the copy holds (the snapshot's Q for KMAX <= 8, so C5's three kinds take 8 x 3 values, not
+// 8 x 4; PAS_GAS_MAX_RES otherwise).
+template <int KMAX, int QW>
 __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
   const int32_t nc = a.n_cards[n];
   if (nc <= 0) return false;  // FetchNode error / no cards label (:282-298)
@@ -110,13 +112,13 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
   const int32_t Q = a.Q;
   const int32_t ncard = min(nc, min(a.K, KMAX));
   int64_t cap[kMaxRes];
-  int64_t w[KMAX][kMaxRes];
+  int64_t w[KMAX][QW];
 #pragma unroll
   for (int q = 0; q < kMaxRes; ++q) cap[q] = q < Q ? a.cap[(int64_t)n * Q + q] : 0;
 #pragma unroll kUnroll
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-    for (int q = 0; q < kMaxRes; ++q)
+    for (int q = 0; q < QW; ++q)
       w[k][q] = (k < ncard && q < Q) ? a.used[((int64_t)n * a.K + k) * Q + q] : 0;
   const int32_t nct = a.ncont[p];
   for (int32_t c = 0; c < nct; ++c) {
@@ -132,7 +134,8 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
 #pragma unroll
       for (int q = 0; q < kMaxRes; ++q) r[q] /= num;
     if (num > kRunsFrom) {  // card runs (gas_runs.h)
-      if (!container_runs<KMAX>(Q, m, r, num, cap, w, ncard, [](int, int64_t) {})) return false;
+      if (!container_runs<KMAX, QW>(Q, m, r, num, cap, w, ncard, [](int, int64_t) {}))
+        return false;
       continue;
     }
     for (int64_t g = 0; g < num; ++g) {
@@ -141,7 +144,7 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
       for (int k = KMAX - 1; k >= 0; --k) {  // first fit = lowest k
         bool ok = k < ncard && !(m & PAS_REQ_UNKNOWN_KIND);  // (a key no capacity has)
 #pragma unroll
-        for (int q = 0; q < kMaxRes; ++q)
+        for (int q = 0; q < QW; ++q)
           if (q < Q && ((m >> q) & 1u)) ok = ok && kind_fits(r[q], cap[q], w[k][q]);
         chosen = ok ? k : chosen;
       }
@@ -149,7 +152,7 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
 #pragma unroll kUnroll
       for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-        for (int q = 0; q < kMaxRes; ++q)
+        for (int q = 0; q < QW; ++q)
           if (k == chosen && q < Q && ((m >> q) & 1u)) w[k][q] += r[q];
     }
   }
@@ -203,9 +206,46 @@ __device__ void half_bounds(const LazyTopkParams& a, int32_t m, int32_t c, int64
 constexpr int kPodLanes = 32;                // lanes per pod (order positions per round)
 constexpr int kPodsPerWave = 64 / kPodLanes;
 constexpr int kPodsPerBlock = kWaves * kPodsPerWave;
+constexpr int kStageRules = kPodLanes;       // rules of a pod compiled into LDS (one per lane)
 
-template <int KMAX>
+// A dontschedule rule compiled once per pod: EvaluateRule (operator.go:13-26) on the node's
+// value v (milli) as the range test  (uint64)(v - lo) <= span, with the saturating target
+//  folded in: LessThan t -> [INT64_MIN, t*1000 - 1], GreaterThan t ->
+// [t*1000 + 1, INT64_MAX], Equals t -> [t*1000, t*1000]; a target past the int64 milli range
+// selects every value or none.  metric < 0: never evaluated (not cached, unknown operator, or
+// a range that selects nothing).
+struct alignas(16) LazyRule {
+  int64_t lo;
+  uint64_t span;
+};
+
+__device__ __forceinline__ void compile_rule(const pas_rule& ru, int32_t M, int32_t* metric,
+                                             LazyRule* out) {
+  int64_t tm = 0;
+  const int sat = target_milli(ru.target, &tm);
+  int64_t lo = 0, hi = -1;  // empty
+  if (ru.metric >= 0 && ru.metric < M) {
+    if (ru.op == PAS_OP_LESS_THAN) {
+      if (sat > 0) lo = INT64_MIN, hi = INT64_MAX;
+      else if (sat == 0 && tm > INT64_MIN) lo = INT64_MIN, hi = tm - 1;
+    } else if (ru.op == PAS_OP_GREATER_THAN) {
+      if (sat < 0) lo = INT64_MIN, hi = INT64_MAX;
+      else if (sat == 0 && tm < INT64_MAX) lo = tm + 1, hi = INT64_MAX;
+    } else if (ru.op == PAS_OP_EQUALS) {
+      if (sat == 0) lo = hi = tm;
+    }
+  }
+  const bool live = lo <= hi;
+  *metric = live ? ru.metric : -1;
+  out->lo = lo;
+  out->span = (uint64_t)hi - (uint64_t)lo;
+}
+
+template <int KMAX, int QW>
 __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
+  // the pods' compiled rules, kStageRules per pod (pods of at most that many rules)
+  __shared__ LazyRule srule[kPodsPerBlock][kStageRules];
+  __shared__ int32_t smetric[kPodsPerBlock][kStageRules];
   const int lane = threadIdx.x & 63;
   const int half = lane / kPodLanes, sub = lane % kPodLanes;
   // XCD-aware: blocks b and b + 8 share an XCD; each XCD takes a contiguous run of the
@@ -277,6 +317,22 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
       }
     }
   }
+  // Pods of at most kStageRules rules (every pod of the wave): each lane compiles one rule
+  // of its pod into LDS, read back per round as broadcast LDS reads instead of a global load
+  // per lane, rule and round.
+  const int pslot = (int)(threadIdx.x >> 6) * kPodsPerWave + half;
+  const bool staged = !__ballot(have && r1 - r0 > kStageRules);
+  if (staged) {
+    LazyRule cr{0, 0};
+    int32_t cm = -1;
+    if (have && r0 + sub < r1) compile_rule(a.rules[r0 + sub], a.M, &cm, &cr);
+    srule[pslot][sub] = cr;
+    smetric[pslot][sub] = cm;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  }
+  const int32_t nr = have ? r1 - r0 : 0;
   const int32_t* row = a.perm + (int64_t)(d0.y >= 0 ? d0.y : 0) * a.R;
   const int64_t* mcol = a.vals + (int64_t)(d0.y >= 0 ? pr.metric : 0) * a.N;
   int64_t* keys = a.key_out + (int64_t)p * k;
@@ -301,7 +357,30 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
     const int64_t* vrow = a.vals_t + (int64_t)n * a.M;
     const uint64_t* prow = a.pres_t + (int64_t)n * a.WM;
     bool viol = false;
-    for (int32_t rb = r0; __ballot(ok && rb < r1); rb += kRuleBatch) {
+    if (staged) {
+      for (int32_t rb = 0; __ballot(ok && rb < nr); rb += kRuleBatch) {
+        int32_t m[kRuleBatch];
+        int64_t v[kRuleBatch];
+        uint64_t pw[kRuleBatch];
+#pragma unroll
+        for (int u = 0; u < kRuleBatch; ++u) m[u] = smetric[pslot][min(rb + u, kStageRules - 1)];
+#pragma unroll
+        for (int u = 0; u < kRuleBatch; ++u) {
+          const int32_t mm = m[u] >= 0 ? m[u] : 0;
+          v[u] = vrow[mm];
+          pw[u] = prow[mm >> 6];
+        }
+#pragma unroll
+        for (int u = 0; u < kRuleBatch; ++u) {
+          const LazyRule cr = srule[pslot][min(rb + u, kStageRules - 1)];
+          const bool hit = rb + u < nr && m[u] >= 0 &&
+                           (uint64_t)v[u] - (uint64_t)cr.lo <= cr.span &&
+                           ((pw[u] >> (m[u] & 63)) & 1ull);
+          viol = viol || hit;
+        }
+      }
+    }
+    for (int32_t rb = r0; !staged && __ballot(ok && rb < r1); rb += kRuleBatch) {
       pas_rule ru[kRuleBatch];
       int64_t v[kRuleBatch];
       uint64_t pw[kRuleBatch];
@@ -328,7 +407,7 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
       }
     }
     ok = ok && !viol;
-    if (ok) ok = lane_fit<KMAX>(a, p, n);
+    if (ok) ok = lane_fit<KMAX, QW>(a, p, n);
     const uint64_t keep = __ballot(ok) & half_mask;
     if (ok) {
       const int32_t rank = kept + __popcll(keep & below);
@@ -477,12 +556,18 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
   a.node_out = d_node;
   a.len_out = d_len;
   const unsigned grid = (unsigned)((n_pods + kPodsPerBlock - 1) / kPodsPerBlock);
-  if (a.K <= 8)
-    tas_gas_topk_kernel<8><<<grid, kTpb, 0, s>>>(a);
-  else if (a.K <= 16)
-    tas_gas_topk_kernel<16><<<grid, kTpb, 0, s>>>(a);
-  else
-    tas_gas_topk_kernel<PAS_GAS_MAX_CARDS><<<grid, kTpb, 0, s>>>(a);
+  if (a.K <= 8) {
+    switch (a.Q) {
+      case 1: tas_gas_topk_kernel<8, 1><<<grid, kTpb, 0, s>>>(a); break;
+      case 2: tas_gas_topk_kernel<8, 2><<<grid, kTpb, 0, s>>>(a); break;
+      case 3: tas_gas_topk_kernel<8, 3><<<grid, kTpb, 0, s>>>(a); break;
+      default: tas_gas_topk_kernel<8, kMaxRes><<<grid, kTpb, 0, s>>>(a); break;
+    }
+  } else if (a.K <= 16) {
+    tas_gas_topk_kernel<16, kMaxRes><<<grid, kTpb, 0, s>>>(a);
+  } else {
+    tas_gas_topk_kernel<PAS_GAS_MAX_CARDS, kMaxRes><<<grid, kTpb, 0, s>>>(a);
+  }
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
