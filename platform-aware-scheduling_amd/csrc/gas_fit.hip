@@ -44,6 +44,9 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+#ifndef PAS_GAS_MIXED
+#define PAS_GAS_MIXED 0  // 1: the three fit roles in one launch, blocks interleaved
+#endif
 #ifndef PAS_GAS_CONCURRENT
 #define PAS_GAS_CONCURRENT 2  // 1: multi-selection kernels on a side stream; 2: the single one
 #endif
@@ -1033,19 +1036,28 @@ __device__ __forceinline__ void fill_tab(const int64_t (&free)[kMaxCards][Q], co
       if (q != SKIP) tab.at(k, lane)[j++] = free[k][q];
 }
 
+// fill_tab with the values read from the card-major copy (no register copy of the node's
+// free values stays live in the sequential kernel).
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ void fill_tab_t(const int64_t* __restrict__ free_t, int32_t n,
+                                           bool valid, int32_t N, const FreeTab<kC>& tab,
+                                           int lane) {
+  int64_t free[kMaxCards][Q];
+  load_free_t<Q>(n, valid, N, free_t, free);
+  fill_tab<Q, SKIP, kC>(free, tab, lane);
+}
+
 // A pod with 4 to 8 selections: the selections in order on a working copy of the free values
-// (registers), each a fit mask on the copy; the chosen card's copy drops by the take, updated
-// under the lanes that chose it (one branch per card some lane chose).
+// (registers, loaded from the card-major copy per pod: the rare list without a skipped kind
+// keeps no second copy live), each a fit mask on the copy; the chosen card's copy drops by
+// the take, updated under the lanes that chose it (one branch per card some lane chose).
 template <int Q, int SKIP>
-__device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards][Q],
-                                                const GasSel* rec, int32_t S, uint64_t live,
-                                                uint32_t node_ok) {
+__device__ __forceinline__ uint32_t multi_state(const int64_t* __restrict__ free_t, int32_t n,
+                                                bool valid, int32_t N, const GasSel* rec,
+                                                int32_t S, uint64_t live, uint32_t node_ok) {
   typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
   int64_t w[kMaxCards][Q];
-#pragma unroll
-  for (int k = 0; k < kMaxCards; ++k)
-#pragma unroll
-    for (int q = 0; q < Q; ++q) w[k][q] = free[k][q];
+  load_free_t<Q>(n, valid, N, free_t, w);
   bool fits = true;
   uint32_t word = 0u;
   for (int32_t t = 0; t < S; ++t) {
@@ -1084,7 +1096,7 @@ __device__ __forceinline__ uint32_t multi_state(const int64_t (&free)[kMaxCards]
 // replicated; fa / fb the node's card ranks) instead of 64-bit compares; card k is then bit
 // 4k + 3 of a mask (rmask), else bit k.
 template <int Q, int SKIP, int kC, bool kRanked = false>
-__device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q],
+__device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMaxCards][Q]; unused ranked
                                               const GasSel* rec, int32_t S, uint64_t live,
                                               uint32_t node_ok, const FreeTab<kC>& tab,
                                               int lane, uint32_t same_row,
@@ -1194,7 +1206,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (&free)[kMaxCards][Q
 // reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
 // waiting for its copy does not hold up the other waves of the block.
 template <int Q, int SKIP, bool kBits>
-__device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], GasSel* stage,
+__device__ __forceinline__ void multi_list(const int64_t* __restrict__ free_t, GasSel* stage,
                                            int64_t* tab_base, uint32_t node_ok,
                                            int32_t N, int32_t n, bool valid,
                                            const int32_t* __restrict__ list,
@@ -1210,7 +1222,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
   constexpr bool kGather = Q > 1 && SKIP >= 0;
   constexpr int kC = Q > 1 ? Q - 1 : 1;
   const FreeTab<kC> tab{tab_base};
-  if (kGather && i0 < i1) fill_tab<Q, SKIP, kC>(free, tab, lane);
+  if (kGather && i0 < i1) fill_tab_t<Q, SKIP, kC>(free_t, n, valid, N, tab, lane);
   // a batch's rows are loaded one batch ahead: every load of the next batch is in flight
   // while this batch's pods are evaluated (rows past the batch: zeros, not read)
   constexpr int kIters = kMB * kRowChunks / 64;
@@ -1256,11 +1268,14 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
         if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
-          if constexpr (kGather)
+          if constexpr (kGather) {
+            int64_t free[kMaxCards][Q];
+            load_free_t<Q>(n, valid, N, free_t, free);
             out = multi_seq<Q, SKIP, kC>(free, rec, S, live, node_ok, tab, lane,
                                          (uint32_t)(same_m >> (32 * j)));
-          else
-            out = multi_state<Q, SKIP>(free, rec, S, live, node_ok);
+          } else {
+            out = multi_state<Q, SKIP>(free_t, n, valid, N, rec, S, live, node_ok);
+          }
         }
       }
       put_result<kBits>(res, fit, pod, N, n, valid, out);
@@ -1274,7 +1289,7 @@ __device__ __forceinline__ void multi_list(const int64_t (&free)[kMaxCards][Q], 
 // 64-bit rows for the current-free checks and their rank rows) are staged as in multi_list.
 // LDS: the FreeTab copy, then the sorted rows of the ranking, overlaid by the batch stage.
 template <int Q, int SKIP, bool kBits>
-__device__ __forceinline__ void rseq_list(const int64_t (&free)[kMaxCards][Q], char* wlds,
+__device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, char* wlds,
                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                           const int32_t* __restrict__ list,
                                           const GasSel* __restrict__ sels,
@@ -1292,7 +1307,7 @@ __device__ __forceinline__ void rseq_list(const int64_t (&free)[kMaxCards][Q], c
   constexpr int32_t gs = kRankMax / kPacked;
   int32_t g0, g1;
   chunk_groups(cnt, bt.chunks, bt.chunk, gs, &g0, &g1);
-  if (g0 < g1) fill_tab<Q, SKIP, kC>(free, tab, lane);
+  if (g0 < g1) fill_tab_t<Q, SKIP, kC>(free_t, n, valid, N, tab, lane);
   static_assert(kMB * kRowChunks == 64 && sizeof(GasSel) == 64, "one 16-B piece per lane");
   static_assert(kMB * sizeof(GasRSeq) / 16 <= 64, "rank rows");
   constexpr int kRWords = (int)(sizeof(GasRSeq) / 16);
@@ -1300,7 +1315,7 @@ __device__ __forceinline__ void rseq_list(const int64_t (&free)[kMaxCards][Q], c
     const int32_t gb = gi * gs, ge = min(cnt, gb + gs);
     load_sorted<kC>(srt, item0 + (int64_t)gb * kPacked, (ge - gb) * kPacked, lds, lane);
     uint32_t fa[kC], fb[kC];
-    rank_cards<Q, SKIP, kC>(free, lds, (ge - gb) * kPacked, fa, fb);
+    rank_cards_t<Q, SKIP, kC>(free_t, n, valid, N, lds, (ge - gb) * kPacked, fa, fb);
     for (int32_t b0 = gb; b0 < ge; b0 += kMB) {
       const int32_t nb = min(kMB, ge - b0);
       const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
@@ -1326,7 +1341,7 @@ __device__ __forceinline__ void rseq_list(const int64_t (&free)[kMaxCards][Q], c
         const int32_t S = (pw >> 24) & 0xF;
         uint32_t out = 0u;
         if (!(pw & kBadPod) && S <= kPacked)  // more: the generic kernel's, 0 here
-          out = multi_seq<Q, SKIP, kC, true>(free, stage + j * kPacked, S, 0, node_ok, tab, lane,
+          out = multi_seq<Q, SKIP, kC, true>(nullptr, stage + j * kPacked, S, 0, node_ok, tab, lane,
                                              (uint32_t)(same_m >> (32 * j)),
                                              &rstage[j].rep[0][0], fa, fb);
         put_result<kBits>(res, fit, pod, N, n, valid, out);
@@ -1339,7 +1354,7 @@ __device__ __forceinline__ void rseq_list(const int64_t (&free)[kMaxCards][Q], c
 // kind is skipped (rseq_list), else on 64-bit values (multi_list).  item0: the first sorted
 // row of list 1's groups (after the two- and three-selection lists' rows).
 template <int Q, bool kBits, int l = 0>
-__device__ __forceinline__ void seq_lists(const int64_t (&free)[kMaxCards][Q], char* wlds,
+__device__ __forceinline__ void seq_lists(const int64_t* __restrict__ free_t, char* wlds,
                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                           int32_t P, const int32_t* __restrict__ multi,
                                           const GasSel* __restrict__ sels,
@@ -1352,17 +1367,17 @@ __device__ __forceinline__ void seq_lists(const int64_t (&free)[kMaxCards][Q], c
   if constexpr (l == 0 || Q == 1) {
     GasSel* stage = reinterpret_cast<GasSel*>(wlds);
     int64_t* tab = reinterpret_cast<int64_t*>(stage + kPacked * kMB);
-    multi_list<Q, l - 1, kBits>(free, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
+    multi_list<Q, l - 1, kBits>(free_t, stage, tab, node_ok, N, n, valid, multi + (int64_t)L * P,
                                 sels + (int64_t)L * P * kPacked, counts + L, bt, res, fit);
   } else {
     cnt = __builtin_amdgcn_readfirstlane(counts[L]);
-    rseq_list<Q, l - 1, kBits>(free, wlds, node_ok, N, n, valid, multi + (int64_t)L * P,
+    rseq_list<Q, l - 1, kBits>(free_t, wlds, node_ok, N, n, valid, multi + (int64_t)L * P,
                                sels + (int64_t)L * P * kPacked, rq + (int64_t)l * P, srt, item0,
                                cnt, bt, res, fit);
   }
   __builtin_amdgcn_wave_barrier();
   if constexpr (l < Q)
-    seq_lists<Q, kBits, l + 1>(free, wlds, node_ok, N, n, valid, P, multi, sels, rq, srt,
+    seq_lists<Q, kBits, l + 1>(free_t, wlds, node_ok, N, n, valid, P, multi, sels, rq, srt,
                                item0 + (int64_t)cnt * kPacked, counts, bt, res, fit);
 }
 
@@ -1443,15 +1458,18 @@ __device__ __forceinline__ void rsingle_lists(const int64_t* __restrict__ free_t
                                    bt, lds, stage, res, fit);
 }
 
+// LDS of one wave of the one-selection path: the group's sorted rows, then the pod stage.
+template <int Q>
+struct SingleLds {
+  static constexpr size_t kBytes = sizeof(int64_t) * Q * kRankItems + sizeof(GasRSingle) * kPodBatch;
+};
+
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
-    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
-    const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs, const int64_t* __restrict__ srt,
-    const int32_t* __restrict__ counts, int32_t chunks, ResOut res,
+__device__ __forceinline__ void rfit_single_body(
+    const BlockTile& bt, char* wlds, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs,
+    const int64_t* __restrict__ srt, const int32_t* __restrict__ counts, ResOut res,
     uint64_t* __restrict__ fit) {
-  __shared__ int64_t lds[kTpb / 64][Q * kRankItems];   // sorted rows per wave
-  __shared__ GasRSingle stage[kTpb / 64][kPodBatch];  // a slice per wave
-  const BlockTile bt = block_tile(chunks);
   // chunks past every list's end: nothing to load
   int32_t most = 0;
 #pragma unroll
@@ -1461,9 +1479,22 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
+  int64_t* lds = reinterpret_cast<int64_t*>(wlds);
+  GasRSingle* stage = reinterpret_cast<GasRSingle*>(wlds + sizeof(int64_t) * Q * kRankItems);
+  rsingle_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rs, srt, 0, counts, bt, lds, stage,
+                          res, fit);
+}
+
+template <int Q, bool kBits>
+__global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
+    int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs, const int64_t* __restrict__ srt,
+    const int32_t* __restrict__ counts, int32_t chunks, ResOut res,
+    uint64_t* __restrict__ fit) {
+  __shared__ int4 smem[kTpb / 64][SingleLds<Q>::kBytes / 16];  // a slice per wave
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  rsingle_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rs, srt, 0, counts, bt, lds[wave],
-                          stage[wave], res, fit);
+  rfit_single_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                             n_cards, free_t, rs, srt, counts, res, fit);
 }
 
 // A row of packed ranks (byte j = kind j) checked at one card: x = the card's packed ranks
@@ -1620,24 +1651,52 @@ struct MultiLds {
 };
 
 template <int Q, bool kBits>
+__device__ __forceinline__ void rfit_closed_body(
+    const BlockTile& bt, char* w, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
+    const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
+    const int32_t* __restrict__ counts, ResOut res, uint64_t* __restrict__ fit) {
+  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const bool valid = n < N;
+  const int32_t nc = valid ? n_cards[n] : 0;
+  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
+  int64_t* lds = reinterpret_cast<int64_t*>(w);
+  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w + sizeof(int64_t) * Q * kRankItems);
+  uint32_t* tab = reinterpret_cast<uint32_t*>(stage + kRankMB);
+  rmulti_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
+                         tab, res, fit);
+}
+
+template <int Q, bool kBits>
 __global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(5))) void gas_rfit_closed_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ counts, int32_t chunks, ResOut res, uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kRanked / 16];
-  const BlockTile bt = block_tile(chunks);
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  rfit_closed_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                             n_cards, free_t, rm, rw, srt, counts, res, fit);
+}
+
+template <int Q, bool kBits>
+__device__ __forceinline__ void rfit_seq_body(
+    const BlockTile& bt, char* w, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
+    const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
+    const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
+    const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, ResOut res,
+    uint64_t* __restrict__ fit) {
   const int32_t n = bt.node_block * kTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
-  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char* w = reinterpret_cast<char*>(smem[wave]);
-  int64_t* lds = reinterpret_cast<int64_t*>(w);
-  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w + sizeof(int64_t) * Q * kRankItems);
-  uint32_t* tab = reinterpret_cast<uint32_t*>(stage + kRankMB);
-  rmulti_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
-                         tab, res, fit);
+  // the sequential lists' sorted rows follow every two- and three-selection list's rows
+  int64_t item_seq = 0;
+#pragma unroll
+  for (int l = 0; l <= Q; ++l)
+    item_seq += (int64_t)counts[l * kClasses] * 3 + (int64_t)counts[l * kClasses + 1] * 7;
+  seq_lists<Q, kBits>(free_t, w, node_ok, N, n, valid, P, multi, sels, rq, srt,
+                      __builtin_amdgcn_readfirstlane(item_seq), counts, bt, res, fit);
 }
 
 template <int Q, bool kBits>
@@ -1648,22 +1707,78 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_seq_kernel(
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
     ResOut res, uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kSeq / 16];
-  const BlockTile bt = block_tile(chunks);
-  const int32_t n = bt.node_block * kTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
-  int64_t free[kMaxCards][Q];
-  load_free_t<Q>(n, valid, N, free_t, free);
-  const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // the sequential lists' sorted rows follow every two- and three-selection list's rows
-  int64_t item_seq = 0;
-#pragma unroll
-  for (int l = 0; l <= Q; ++l)
-    item_seq += (int64_t)counts[l * kClasses] * 3 + (int64_t)counts[l * kClasses + 1] * 7;
-  seq_lists<Q, kBits>(free, reinterpret_cast<char*>(smem[wave]), node_ok, N, n, valid, P, multi,
-                      sels, rq, srt, __builtin_amdgcn_readfirstlane(item_seq), counts, bt, res,
-                      fit);
+  rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P, n_cards,
+                          free_t, rq, srt, multi, sels, counts, res, fit);
+}
+
+// The three fit roles in ONE launch, their blocks interleaved in dispatch order, so that every
+// CU runs store-bound one-selection blocks beside issue-bound multi-selection blocks for the
+// whole launch (separate kernels overlap only where the dispatcher happens to mix them).  The
+// grid's positions (XCD-aware, as block_tile: each XCD a contiguous run) are dealt out to the
+// roles in proportion to their tile counts (Bresenham), single vs multi first, then closed vs
+// sequential among the multi positions; each role's tiles stay node-major, so an XCD's L2
+// keeps a contiguous range of node blocks per role.
+struct MixedArgs {
+  int32_t N, P, ch_s, ch_m, t_single, t_closed, t_seq;
+  const int32_t* n_cards;
+  const int64_t* free_t;
+  const GasRSingle* rs;
+  const int64_t* srt_s;
+  const int32_t* counts;
+  const GasRMulti* rm;
+  const int32_t* rw;
+  const int64_t* srt_m;
+  const GasRSeq* rq;
+  const int32_t* multi;
+  const GasSel* sels;
+  ResOut res;
+  uint64_t* fit;
+};
+
+// How many of the first `pos` positions go to a role of `part` out of `total` positions.
+__device__ __forceinline__ int32_t share_before(int32_t pos, int32_t part, int32_t total) {
+  return (int32_t)((int64_t)pos * part / total);
+}
+
+#ifndef PAS_GAS_MIXED_WPE
+#define PAS_GAS_MIXED_WPE 4
+#endif
+template <int Q, bool kBits>
+__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(PAS_GAS_MIXED_WPE))) void
+gas_rfit_mixed_kernel(MixedArgs a) {
+  constexpr size_t kW = MultiLds<Q>::kSeq > MultiLds<Q>::kRanked
+                            ? (MultiLds<Q>::kSeq > SingleLds<Q>::kBytes ? MultiLds<Q>::kSeq
+                                                                       : SingleLds<Q>::kBytes)
+                            : (MultiLds<Q>::kRanked > SingleLds<Q>::kBytes
+                                   ? MultiLds<Q>::kRanked
+                                   : SingleLds<Q>::kBytes);
+  __shared__ int4 smem[kTpb / 64][kW / 16];
+  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  char* w = reinterpret_cast<char*>(smem[wave]);
+  const int32_t nb = gridDim.x, b = blockIdx.x;
+  const int32_t xcd = b & 7, per = nb >> 3, rem = nb & 7;
+  const int32_t pos = xcd * per + min(xcd, rem) + (b >> 3);
+  const int32_t tm = a.t_closed + a.t_seq;
+  const int32_t s0 = share_before(pos, a.t_single, nb), s1 = share_before(pos + 1, a.t_single, nb);
+  if (s1 > s0) {  // a one-selection tile
+    const BlockTile bt{s0 / a.ch_s, s0 % a.ch_s, a.ch_s};
+    rfit_single_body<Q, kBits>(bt, w, a.N, a.P, a.n_cards, a.free_t, a.rs, a.srt_s, a.counts,
+                               a.res, a.fit);
+    return;
+  }
+  const int32_t mpos = pos - s0;  // position among the multi-selection tiles
+  const int32_t c0 = share_before(mpos, a.t_closed, tm), c1 = share_before(mpos + 1, a.t_closed, tm);
+  if (c1 > c0) {
+    const BlockTile bt{c0 / a.ch_m, c0 % a.ch_m, a.ch_m};
+    rfit_closed_body<Q, kBits>(bt, w, a.N, a.P, a.n_cards, a.free_t, a.rm, a.rw, a.srt_m,
+                               a.counts + Q + 1, a.res, a.fit);
+  } else {
+    const int32_t q = mpos - c0;
+    const BlockTile bt{q / a.ch_m, q % a.ch_m, a.ch_m};
+    rfit_seq_body<Q, kBits>(bt, w, a.N, a.P, a.n_cards, a.free_t, a.rq, a.srt_m, a.multi,
+                            a.sels, a.counts + Q + 1, a.res, a.fit);
+  }
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -1949,7 +2064,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   // disjoint result rows; a side stream is forked from s here and joined before the generic
   // kernel
   hipStream_t ss = s, ms = s;
-  if (PAS_GAS_CONCURRENT) {
+  if (PAS_GAS_CONCURRENT && !PAS_GAS_MIXED) {
     if (!ctx->gas_side) {
       PAS_HIP(ctx, hipStreamCreateWithFlags(&ctx->gas_side, hipStreamNonBlocking));
       PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_fork, hipEventDisableTiming));
@@ -1959,9 +2074,17 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     PAS_HIP(ctx, hipStreamWaitEvent(ctx->gas_side, ctx->gas_fork, 0));
     (PAS_GAS_CONCURRENT == 1 ? ms : ss) = ctx->gas_side;
   }
+  MixedArgs ma{N, n_pods, ch_s, ch_m, nb_s * ch_s, nb_s * ch_m, nb_s * ch_m, g.n_cards,
+               static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, rmulti, rword, srt_m,
+               rseq, multi, sels, ResOut{d_res, ld_res}, d_fit};
+  const unsigned mixed_grid = (unsigned)(ma.t_single + ma.t_closed + ma.t_seq);
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
+    if (PAS_GAS_MIXED) {                                                                       \
+      gas_rfit_mixed_kernel<QQ, B><<<mixed_grid, kTpb, 0, s>>>(ma);                            \
+      break;                                                                                   \
+    }                                                                                          \
     if (PAS_GAS_CONCURRENT != 2)                                                               \
       gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
@@ -1982,7 +2105,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
 #undef PAS_GAS_CASE
     default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   }
-  if (PAS_GAS_CONCURRENT) {
+  if (PAS_GAS_CONCURRENT && !PAS_GAS_MIXED) {
     PAS_HIP(ctx, hipEventRecord(ctx->gas_join, ctx->gas_side));
     PAS_HIP(ctx, hipStreamWaitEvent(s, ctx->gas_join, 0));
   }

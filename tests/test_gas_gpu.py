@@ -237,3 +237,43 @@ def test_unknown_kind_flag_parity(ctx, oracle, k):
     assert blocked.any() and not (want[blocked] >> 31).any()
     clean = oracle.gas_fit(n_cards, cap, used, req, mask & 0x7FFFFFFF, ncont, 0)
     np.testing.assert_array_equal(want[~blocked], clean[~blocked])
+
+
+def test_fits_alternating_streams(oracle):
+    """Back-to-back fits on different streams without host synchronisation: each
+    fit starts from list counts the previous fit's prep kernel zeroed on ITS stream, and the
+    context's scratch is shared, so a fit on another stream waits for the previous fit
+    (gas_fit_launch).  Fresh context, batches of different shapes, every result checked."""
+    import torch
+    gs = wl.make_gas_snapshot(6000, seed=0x5A)
+    batches = [wl.make_gas_batch(p, seed=0x5A + i) for i, p in enumerate((900, 300, 1500, 40))]
+    c = pas_amd.Context(0)
+    try:
+        s0 = torch.cuda.current_stream()
+        c.gas_snapshot_set_device(9, 6000, gs.used.shape[1], gs.used.shape[2],
+                                  torch.from_numpy(gs.n_cards).cuda(),
+                                  torch.from_numpy(gs.cap).cuda(),
+                                  torch.from_numpy(gs.used).cuda(), s0)
+        streams = [torch.cuda.Stream(), torch.cuda.Stream(), None]
+        outs = []
+        for rep in range(3):
+            for i, b in enumerate(batches):
+                s = streams[(rep + i) % 3]
+                st = s if s is not None else s0
+                st.wait_stream(s0)
+                with torch.cuda.stream(st):
+                    req = torch.from_numpy(b.req).cuda()
+                    mask = torch.from_numpy(b.req_mask.view(np.int32)).cuda()
+                    nc = torch.from_numpy(b.n_containers).cuda()
+                    res = torch.empty((len(b.n_containers), 6000), dtype=torch.int32,
+                                      device="cuda")
+                c.gas_fit_device(9, len(b.n_containers), b.req.shape[1], wl.I915, req, mask, nc,
+                                 res, stream=st)
+                outs.append((i, res, st))
+        torch.cuda.synchronize()
+        want = [oracle.gas_fit(gs.n_cards, gs.cap, gs.used, b.req, b.req_mask, b.n_containers,
+                               wl.I915) for b in batches]
+        for i, res, _ in outs:
+            np.testing.assert_array_equal(res.cpu().numpy().view(np.uint32), want[i])
+    finally:
+        c.close()
