@@ -111,23 +111,48 @@ def bench_tas(args, world, rank):
     rules_t = dev(batch.rules.view(np.uint8))
     off_t = dev(batch.rule_off)
     prio_t = dev(batch.prio.view(np.uint8))
-    pass_t = torch.empty((P, pas_amd.w64(N)), dtype=torch.int64, device="cuda")
-    order_t = torch.empty((P, N), dtype=torch.int32, device="cuda")
-    len_t = torch.empty(P, dtype=torch.int32, device="cuda")
     n_rules = len(batch.rules)
     flags = pas_amd.PAS_TAS_FILTER | pas_amd.PAS_TAS_PRIORITIZE
+    # --pipeline D: consecutive batches on D streams of their own (outputs per stream), so
+    # batch i + 1's prep and first blocks run under batch i's eval (the context keeps one
+    # scratch slot per stream); D = 1: every step on the launch stream
+    D = max(1, args.pipeline)
+    lanes = [stream] if D == 1 else [torch.cuda.Stream() for _ in range(D)]
+    outs = [(torch.empty((P, pas_amd.w64(N)), dtype=torch.int64, device="cuda"),
+             torch.empty((P, N), dtype=torch.int32, device="cuda"),
+             torch.empty(P, dtype=torch.int32, device="cuda")) for _ in range(D)]
+    pass_t, order_t, len_t = outs[0]
+    turn = [0]
 
     def step():
-        ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pass_t, order_t,
-                            len_t, stream)
+        k = turn[0] % D
+        turn[0] += 1
+        pt, ot, lt = outs[k]
+        ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pt, ot, lt,
+                            lanes[k])
 
-    settle_steps = distrib.settle(step, args.settle, world=world)
+    def fork():  # the pipeline streams start after the timed region's start event
+        for ln in lanes:
+            if ln is not stream:
+                ln.wait_stream(stream)
+
+    def join():  # the end event after every pipeline stream's work
+        for ln in lanes:
+            if ln is not stream:
+                stream.wait_stream(ln)
+
+    def sync_all():
+        join()
+        torch.cuda.synchronize()
+
+    settle_steps = distrib.settle(step, args.settle, sync=sync_all, world=world)
     for _ in range(args.warmup):
         step()
     # timed steps: two HIP events on the launch stream around all of them (events between
     # the steps would add ~10 us each to the wall)
     gpu = {}
-    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu)
+    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu, fork=fork, join=join)
+    torch.cuda.synchronize()
     span_ms = gpu["ms_per_step"]
     # per-kernel breakdown from extra, untimed steps (events around every launch)
     ctx.reset_timing()
@@ -135,6 +160,7 @@ def bench_tas(args, world, rank):
     n_detail = min(args.steps, 5)
     for _ in range(n_detail):
         step()
+    torch.cuda.synchronize()
     ctx.set_timing(0)
     kern, launches = {}, {}
     for kid in (_lib.PAS_K_TAS_PREP, _lib.PAS_K_TAS_EVAL):
@@ -167,6 +193,7 @@ def bench_tas(args, world, rank):
             "workload": "tas_filter_prioritize (BASELINE configs[1])",
             "pods_per_gpu": P, "nodes": N, "metrics": M, "rules_per_pod": R + 1,
             "parallelism": f"pod-sharded x{world} (independent batches, replicated snapshot)",
+            "pipeline_streams": D,
             "prioritize_entries_per_step": sum_len * world,
             "snapshot_build_ms": snapshot_ms, "snapshot_refresh_ms": refresh,
             "kernel_ms_per_step": kern,
@@ -359,22 +386,49 @@ def bench_gas(args, world, rank):
     # result rows at a pitch of N rounded up to 32 words (pas_gas_fit_ld_device): every row
     # starts on a 128-B line; --gas-pitch dense writes [P][N] rows
     ld = N if args.gas_pitch == "dense" else (N + 31) // 32 * 32
-    res_t = torch.empty((P, ld), dtype=torch.int32, device="cuda")
+    # --pipeline D: consecutive batches on D streams of their own (results per stream): batch
+    # i + 1's prep kernels run under batch i's fit kernels (one scratch slot per stream)
+    D = max(1, args.pipeline)
+    lanes = [stream] if D == 1 else [torch.cuda.Stream() for _ in range(D)]
+    results = [torch.empty((P, ld), dtype=torch.int32, device="cuda") for _ in range(D)]
+    res_t = results[0]
+    turn = [0]
 
     def step():
-        ctx.gas_fit_ld_device(1, P, C, wl.I915, req_t, mask_t, nc_t, res_t, ld, stream=stream)
+        k = turn[0] % D
+        turn[0] += 1
+        ctx.gas_fit_ld_device(1, P, C, wl.I915, req_t, mask_t, nc_t, results[k], ld,
+                              stream=lanes[k])
 
-    settle_steps = distrib.settle(step, args.settle, world=world)
+    def fork():
+        for ln in lanes:
+            if ln is not stream:
+                ln.wait_stream(stream)
+
+    def join():
+        for ln in lanes:
+            if ln is not stream:
+                stream.wait_stream(ln)
+
+    def sync_all():
+        join()
+        torch.cuda.synchronize()
+
+    settle_steps = distrib.settle(step, args.settle, sync=sync_all, world=world)
     for _ in range(args.warmup):
         step()
     gpu = {}
-    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu)
+    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu, fork=fork, join=join)
+    torch.cuda.synchronize()
     # the fit launches alone, from extra, untimed steps (span events around them)
     ctx.reset_timing()
     ctx.set_timing(1)
     for _ in range(min(args.steps, 5)):
         step()
+    torch.cuda.synchronize()
     ctx.set_timing(0)
+    if D > 1:
+        assert all(torch.equal(r, res_t) for r in results[1:]), "pipeline results differ"
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
     # the same batch into dense [P][N] rows (pas_gas_fit_device), untimed extra steps
     dense_ms = None
@@ -401,7 +455,7 @@ def bench_gas(args, world, rank):
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "int64", "data": "synthetic (SURVEY.md §8(d) C3)",
         "config": {"settle_steps": settle_steps, "workload": "gas_fit (BASELINE configs[2])", "pods_per_gpu": P, "nodes": N,
-                   "cards": K, "resources": Q, "result_row_pitch": ld,
+                   "cards": K, "resources": Q, "result_row_pitch": ld, "pipeline_streams": D,
                    "dense_pitch_gpu_ms_per_step": dense_ms,
                    "fit_fraction": float((res_t[:, :N].cpu().numpy().view(np.uint32) >> 31)
                                          .mean())},
@@ -728,6 +782,9 @@ def main():
     ap.add_argument("--backend", choices=["auto", "nccl", "gloo"], default="auto",
                     help="collective backend of a multi-rank run (auto: RCCL on GPUs); gloo "
                          "lets several ranks share one GPU (tests)")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="TAS: consecutive batches on this many streams of their own (1: the "
+                         "launch stream only)")
     ap.add_argument("--no-request-latency", action="store_true",
                     help="skip the f2 request-latency leg of the TAS workload")
     args = ap.parse_args()

@@ -44,9 +44,6 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
-#ifndef PAS_GAS_MIXED
-#define PAS_GAS_MIXED 0  // 1: the three fit roles in one launch, blocks interleaved
-#endif
 #ifndef PAS_GAS_CONCURRENT
 #define PAS_GAS_CONCURRENT 2  // 1: multi-selection kernels on a side stream; 2: the single one
 #endif
@@ -1317,7 +1314,7 @@ __device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, ch
     uint32_t fa[kC], fb[kC];
     rank_cards_t<Q, SKIP, kC>(free_t, n, valid, N, lds, (ge - gb) * kPacked, fa, fb);
     for (int32_t b0 = gb; b0 < ge; b0 += kMB) {
-      const int32_t nb = min(kMB, ge - b0);
+      const int32_t nb = __builtin_amdgcn_readfirstlane(min(kMB, ge - b0));
       const int4* src = reinterpret_cast<const int4*>(sels + (int64_t)b0 * kPacked);
       const int4 v = lane < nb * kRowChunks ? src[lane] : int4{0, 0, 0, 0};
       const int4* rsrc = reinterpret_cast<const int4*>(rq + b0);
@@ -1400,6 +1397,15 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
   // the node's free values only while ranking, one kind at a time (registers for the pod loop)
   load_sorted<C>(srt, item0 + gb, ge - gb, lds, lane);
   rank_cards_t<Q, kSkip, C>(free_t, n, valid, N, lds, ge - gb, fa, fb);
+  // a node that fits nothing (no cards label, not in the lister, past the fast kernels' card
+  // count) as eight cards of rank 0: every one-selection row compares at least one kind of
+  // rank >= 1 (the last kind a selection requests is never skipped), so its mask is empty
+  // and the pod loop needs no node_ok (pods without a selection still take node_ok)
+#pragma unroll
+  for (int j = 0; j < C; ++j) {
+    fa[j] = node_ok ? fa[j] : 0x80808080u;
+    fb[j] = node_ok ? fb[j] : 0x80808080u;
+  }
   auto one_pod = [&](const GasRSingle& r, int32_t w) {
     const int64_t pod = w & 0xFFFFFF;
     uint32_t out = node_ok;
@@ -1407,9 +1413,13 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
       uint32_t g[C];
 #pragma unroll
       for (int jj = 0; jj < C; ++jj) g[jj] = r.g[jj];
-      const uint32_t m = (w & kBadPod) ? 0u : rmask<C>(fa, fb, g);
-      if constexpr (kBits) out = m ? node_ok : 0u;
-      else out = m ? (node_ok | (1u << 24) | (lowbit(m) >> 2)) : 0u;
+      if (w & kBadPod) {
+        out = 0u;
+      } else {
+        const uint32_t m = rmask<C>(fa, fb, g);
+        if constexpr (kBits) out = m ? 0x80000000u : 0u;
+        else out = m ? (0x81000000u | (lowbit(m) >> 2)) : 0u;
+      }
     }
     put_result<kBits>(res, fit, pod, N, n, valid, out);
   };
@@ -1430,13 +1440,19 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-    // pods in pairs: both records read (broadcast LDS reads) before the first one's tests
-    for (int32_t j = 0; j < nb; j += 2) {
-      const GasRSingle r0 = stage[j], r1 = stage[j + 1];
-      const int32_t w0 = __builtin_amdgcn_readfirstlane(r0.word);
-      const int32_t w1 = __builtin_amdgcn_readfirstlane(r1.word);
-      one_pod(r0, w0);
-      if (j + 1 < nb) one_pod(r1, w1);
+    // pods in pairs: both records read (broadcast LDS reads) before the first one's tests;
+    // eight pods per iteration, so the records' LDS offsets are constants off one address
+    for (int32_t j0 = 0; j0 < nb; j0 += 8) {
+      const GasRSingle* st = stage + j0;
+#pragma unroll
+      for (int u = 0; u < 8; u += 2) {
+        if (j0 + u >= nb) break;
+        const GasRSingle r0 = st[u], r1 = st[u + 1];
+        const int32_t w0 = __builtin_amdgcn_readfirstlane(r0.word);
+        const int32_t w1 = __builtin_amdgcn_readfirstlane(r1.word);
+        one_pod(r0, w0);
+        if (j0 + u + 1 < nb) one_pod(r1, w1);
+      }
     }
   }
 }
@@ -1587,7 +1603,7 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
       tab[k * 64 + lane] = x;
     }
     for (int32_t b0 = gb; b0 < ge; b0 += kRankMB) {
-      const int32_t nb = min(kRankMB, ge - b0);
+      const int32_t nb = __builtin_amdgcn_readfirstlane(min(kRankMB, ge - b0));
       constexpr int kWords = (int)(sizeof(GasRMulti) / 16);
       static_assert(kRankMB * kWords == 64, "one 16-B piece per lane");
       const int4* src = reinterpret_cast<const int4*>(rm + b0);
@@ -1598,15 +1614,21 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-      for (int32_t j = 0; j < nb; ++j) {
-        const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(wd, j);
-        const int64_t pod = w & 0xFFFFFF;
-        uint32_t out = 0u;
-        if (!(w & kBadPod)) {
-          out = rclosed<C, S>(fa, fb, stage[j], w, tab, lane, node_ok);
-          if constexpr (kBits) out = out ? node_ok : 0u;
+      // four pods per iteration: their records' LDS offsets are constants off one address
+      for (int32_t j0 = 0; j0 < nb; j0 += 4) {
+        const GasRMulti* st = stage + j0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (j0 + u >= nb) break;
+          const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(wd, j0 + u);
+          const int64_t pod = w & 0xFFFFFF;
+          uint32_t out = 0u;
+          if (!(w & kBadPod)) {
+            out = rclosed<C, S>(fa, fb, st[u], w, tab, lane, node_ok);
+            if constexpr (kBits) out = out ? node_ok : 0u;
+          }
+          put_result<kBits>(res, fit, pod, N, n, valid, out);
         }
-        put_result<kBits>(res, fit, pod, N, n, valid, out);
       }
     }
   }
@@ -1710,75 +1732,6 @@ __global__ __launch_bounds__(kTpb) void gas_rfit_seq_kernel(
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P, n_cards,
                           free_t, rq, srt, multi, sels, counts, res, fit);
-}
-
-// The three fit roles in ONE launch, their blocks interleaved in dispatch order, so that every
-// CU runs store-bound one-selection blocks beside issue-bound multi-selection blocks for the
-// whole launch (separate kernels overlap only where the dispatcher happens to mix them).  The
-// grid's positions (XCD-aware, as block_tile: each XCD a contiguous run) are dealt out to the
-// roles in proportion to their tile counts (Bresenham), single vs multi first, then closed vs
-// sequential among the multi positions; each role's tiles stay node-major, so an XCD's L2
-// keeps a contiguous range of node blocks per role.
-struct MixedArgs {
-  int32_t N, P, ch_s, ch_m, t_single, t_closed, t_seq;
-  const int32_t* n_cards;
-  const int64_t* free_t;
-  const GasRSingle* rs;
-  const int64_t* srt_s;
-  const int32_t* counts;
-  const GasRMulti* rm;
-  const int32_t* rw;
-  const int64_t* srt_m;
-  const GasRSeq* rq;
-  const int32_t* multi;
-  const GasSel* sels;
-  ResOut res;
-  uint64_t* fit;
-};
-
-// How many of the first `pos` positions go to a role of `part` out of `total` positions.
-__device__ __forceinline__ int32_t share_before(int32_t pos, int32_t part, int32_t total) {
-  return (int32_t)((int64_t)pos * part / total);
-}
-
-#ifndef PAS_GAS_MIXED_WPE
-#define PAS_GAS_MIXED_WPE 4
-#endif
-template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(PAS_GAS_MIXED_WPE))) void
-gas_rfit_mixed_kernel(MixedArgs a) {
-  constexpr size_t kW = MultiLds<Q>::kSeq > MultiLds<Q>::kRanked
-                            ? (MultiLds<Q>::kSeq > SingleLds<Q>::kBytes ? MultiLds<Q>::kSeq
-                                                                       : SingleLds<Q>::kBytes)
-                            : (MultiLds<Q>::kRanked > SingleLds<Q>::kBytes
-                                   ? MultiLds<Q>::kRanked
-                                   : SingleLds<Q>::kBytes);
-  __shared__ int4 smem[kTpb / 64][kW / 16];
-  const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  char* w = reinterpret_cast<char*>(smem[wave]);
-  const int32_t nb = gridDim.x, b = blockIdx.x;
-  const int32_t xcd = b & 7, per = nb >> 3, rem = nb & 7;
-  const int32_t pos = xcd * per + min(xcd, rem) + (b >> 3);
-  const int32_t tm = a.t_closed + a.t_seq;
-  const int32_t s0 = share_before(pos, a.t_single, nb), s1 = share_before(pos + 1, a.t_single, nb);
-  if (s1 > s0) {  // a one-selection tile
-    const BlockTile bt{s0 / a.ch_s, s0 % a.ch_s, a.ch_s};
-    rfit_single_body<Q, kBits>(bt, w, a.N, a.P, a.n_cards, a.free_t, a.rs, a.srt_s, a.counts,
-                               a.res, a.fit);
-    return;
-  }
-  const int32_t mpos = pos - s0;  // position among the multi-selection tiles
-  const int32_t c0 = share_before(mpos, a.t_closed, tm), c1 = share_before(mpos + 1, a.t_closed, tm);
-  if (c1 > c0) {
-    const BlockTile bt{c0 / a.ch_m, c0 % a.ch_m, a.ch_m};
-    rfit_closed_body<Q, kBits>(bt, w, a.N, a.P, a.n_cards, a.free_t, a.rm, a.rw, a.srt_m,
-                               a.counts + Q + 1, a.res, a.fit);
-  } else {
-    const int32_t q = mpos - c0;
-    const BlockTile bt{q / a.ch_m, q % a.ch_m, a.ch_m};
-    rfit_seq_body<Q, kBits>(bt, w, a.N, a.P, a.n_cards, a.free_t, a.rq, a.srt_m, a.multi,
-                            a.sels, a.counts + Q + 1, a.res, a.fit);
-  }
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -1937,38 +1890,13 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const GasSnapshot& g = ctx->gas;
   const int32_t N = g.n_nodes, Q = g.n_res, K = g.max_cards;
   constexpr int32_t kCounts = (1 + kClasses) * (PAS_GAS_MAX_RES + 1) + 1;  // lists + generic pods
-  if (!ctx->gas_limit) {
-    PAS_HIP(ctx, hipMalloc(&ctx->gas_limit, sizeof(int64_t)));
-    PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_limit_ev, hipEventDisableTiming));
-  }
-  if (!ctx->gas_counts) {  // both sets zero before their first use
-    int32_t* c = nullptr;
-    PAS_HIP(ctx, hipMalloc(&c, 2 * kCounts * sizeof(int32_t)));
-    if (hipMemsetAsync(c, 0, 2 * kCounts * sizeof(int32_t), s) != hipSuccess) {
-      (void)hipFree(c);
-      return set_error(ctx, PAS_EDEVICE, "pas_gas_fit: counts init failed");
-    }
-    ctx->gas_counts = c;
-    ctx->gas_counts_set = 0;
-  }
-  // A fit on another stream than the previous one: order it after that fit, whose prep
-  // kernel zeroed this fit's list counts and whose kernels may still read the shared aux
-  // scratch (gas_limit_ev is recorded on every exit after a prep launch).
-  if (ctx->gas_have_last && ctx->gas_last_stream != s)
-    PAS_HIP(ctx, hipStreamWaitEvent(s, ctx->gas_limit_ev, 0));
   if (Q < 1 || Q > PAS_GAS_MAX_RES) return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
-  if (N == 0 || n_pods == 0) {
-    PAS_HIP(ctx, hipMemsetAsync(ctx->gas_limit, 0, sizeof(int64_t), s));
-    if (d_side_count) PAS_HIP(ctx, hipMemsetAsync(d_side_count, 0, sizeof(int64_t), s));
-    PAS_HIP(ctx, hipEventRecord(ctx->gas_limit_ev, s));
-    return PAS_OK;
-  }
+  if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][3][P] |
   // their selection rows [Q+1][3][P][8] | the generic path's pods [P] and per-pod selection
   // counts [P] | list counts [Q+1] + [(Q+1)3] and the generic pod count (zeroed together).  The flipped
   // kind minima and the generic path's nodes depend on the snapshot alone: they sit in
   // g.derived and are recomputed only after the snapshot changed.
-  if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
   const int32_t NL = Q + 1;
   auto al = [](size_t b) { return (b + 255) & ~size_t(255); };
   const size_t b_single = al(sizeof(GasSingle) * (size_t)NL * n_pods);
@@ -1982,19 +1910,40 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_srs = al(sizeof(int64_t) * PAS_GAS_MAX_RES * (size_t)n_pods);
   const size_t b_srm = al(sizeof(int64_t) * PAS_GAS_MAX_RES * kPacked * (size_t)n_pods);
   const size_t b_rq = al(sizeof(GasRSeq) * (size_t)NL * n_pods);
-  const size_t need = b_single + b_multi + b_sels + 2 * b_pods + b_rs + b_rm + b_rw + b_srs +
-                      b_srm + b_rq;
-  if (need > ctx->aux_bytes) {
-    if (ctx->aux) {
-      PAS_HIP(ctx, hipStreamSynchronize(s));
-      PAS_HIP(ctx, hipFree(ctx->aux));
-      ctx->aux = nullptr;
-      ctx->aux_bytes = 0;
+  const bool empty = N == 0 || n_pods == 0;
+  const size_t need = empty ? 0
+                            : b_single + b_multi + b_sels + 2 * b_pods + b_rs + b_rm + b_rw +
+                                  b_srs + b_srm + b_rq;
+  // the stream's scratch slot (ordered after its previous user on another stream)
+  int rc = PAS_OK;
+  AuxSlot* slot = aux_acquire(ctx, s, need, &rc);
+  if (!slot) return rc;
+  if (!slot->gas_limit) PAS_HIP(ctx, hipMalloc(&slot->gas_limit, sizeof(int64_t)));
+  if (!slot->gas_counts) {  // both sets zero before their first use
+    int32_t* c = nullptr;
+    PAS_HIP(ctx, hipMalloc(&c, 2 * kCounts * sizeof(int32_t)));
+    if (hipMemsetAsync(c, 0, 2 * kCounts * sizeof(int32_t), s) != hipSuccess) {
+      (void)hipFree(c);
+      return set_error(ctx, PAS_EDEVICE, "pas_gas_fit: counts init failed");
     }
-    PAS_HIP(ctx, hipMalloc(&ctx->aux, need));
-    ctx->aux_bytes = need;
+    slot->gas_counts = c;
+    slot->gas_counts_set = 0;
   }
-  char* base = static_cast<char*>(ctx->aux);
+  ctx->gas_last_slot = (int)(slot - ctx->aux_slot);
+  // every exit from here records the slot's event on s (a later call on another stream
+  // waits for it before it reuses the slot)
+  struct ReleaseOnExit {
+    pas_ctx* c;
+    AuxSlot* a;
+    hipStream_t s;
+    ~ReleaseOnExit() { aux_release(c, a, s); }
+  } done{ctx, slot, s};
+  if (empty) {
+    PAS_HIP(ctx, hipMemsetAsync(slot->gas_limit, 0, sizeof(int64_t), s));
+    if (d_side_count) PAS_HIP(ctx, hipMemsetAsync(d_side_count, 0, sizeof(int64_t), s));
+    return PAS_OK;
+  }
+  char* base = static_cast<char*>(slot->p);
   GasSingle* single = reinterpret_cast<GasSingle*>(base);
   base += b_single;
   int32_t* multi = reinterpret_cast<int32_t*>(base);
@@ -2019,8 +1968,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   base += b_rq;
   // this fit's list counts (zeroed by the previous fit's prep kernel, or at allocation) and
   // the other set, which this fit's prep kernel zeroes for the next one
-  int32_t* counts = ctx->gas_counts + kCounts * ctx->gas_counts_set;
-  int32_t* counts_next = ctx->gas_counts + kCounts * (1 - ctx->gas_counts_set);
+  int32_t* counts = slot->gas_counts + kCounts * slot->gas_counts_set;
+  int32_t* counts_next = slot->gas_counts + kCounts * (1 - slot->gas_counts_set);
   int32_t* n_big_pods = counts + (1 + kClasses) * (PAS_GAS_MAX_RES + 1);
   unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
   int32_t* n_big_nodes = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
@@ -2036,19 +1985,11 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   }
   gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
-      multi, sels, counts, big_pods, n_big_pods, pod_steps, counts_next, kCounts, ctx->gas_limit,
-      d_side_count);
+      multi, sels, counts, big_pods, n_big_pods, pod_steps, counts_next, kCounts,
+      slot->gas_limit, d_side_count);
   PAS_HIP(ctx, hipGetLastError());
-  // the prep kernel ran: the other set is zeroed (on s) for the next fit, and every exit from
-  // here records gas_limit_ev on s for a next fit on another stream to wait on
-  ctx->gas_counts_set = 1 - ctx->gas_counts_set;
-  ctx->gas_last_stream = s;
-  ctx->gas_have_last = true;
-  struct RecordOnExit {
-    hipEvent_t e;
-    hipStream_t s;
-    ~RecordOnExit() { (void)hipEventRecord(e, s); }
-  } done{ctx->gas_limit_ev, s};
+  // the prep kernel ran: the other set is zeroed (on s) for the slot's next fit
+  slot->gas_counts_set = 1 - slot->gas_counts_set;
   // grids: (node block, pod chunk) pairs, ~8192 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
   const int32_t nb_s = (N + kTpb - 1) / kTpb;
@@ -2064,27 +2005,19 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   // disjoint result rows; a side stream is forked from s here and joined before the generic
   // kernel
   hipStream_t ss = s, ms = s;
-  if (PAS_GAS_CONCURRENT && !PAS_GAS_MIXED) {
-    if (!ctx->gas_side) {
-      PAS_HIP(ctx, hipStreamCreateWithFlags(&ctx->gas_side, hipStreamNonBlocking));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_fork, hipEventDisableTiming));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&ctx->gas_join, hipEventDisableTiming));
+  if (PAS_GAS_CONCURRENT) {
+    if (!slot->side) {
+      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side, hipStreamNonBlocking));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->fork, hipEventDisableTiming));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join, hipEventDisableTiming));
     }
-    PAS_HIP(ctx, hipEventRecord(ctx->gas_fork, s));
-    PAS_HIP(ctx, hipStreamWaitEvent(ctx->gas_side, ctx->gas_fork, 0));
-    (PAS_GAS_CONCURRENT == 1 ? ms : ss) = ctx->gas_side;
+    PAS_HIP(ctx, hipEventRecord(slot->fork, s));
+    PAS_HIP(ctx, hipStreamWaitEvent(slot->side, slot->fork, 0));
+    (PAS_GAS_CONCURRENT == 1 ? ms : ss) = slot->side;
   }
-  MixedArgs ma{N, n_pods, ch_s, ch_m, nb_s * ch_s, nb_s * ch_m, nb_s * ch_m, g.n_cards,
-               static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts, rmulti, rword, srt_m,
-               rseq, multi, sels, ResOut{d_res, ld_res}, d_fit};
-  const unsigned mixed_grid = (unsigned)(ma.t_single + ma.t_closed + ma.t_seq);
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
-    if (PAS_GAS_MIXED) {                                                                       \
-      gas_rfit_mixed_kernel<QQ, B><<<mixed_grid, kTpb, 0, s>>>(ma);                            \
-      break;                                                                                   \
-    }                                                                                          \
     if (PAS_GAS_CONCURRENT != 2)                                                               \
       gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
@@ -2105,9 +2038,9 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
 #undef PAS_GAS_CASE
     default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   }
-  if (PAS_GAS_CONCURRENT && !PAS_GAS_MIXED) {
-    PAS_HIP(ctx, hipEventRecord(ctx->gas_join, ctx->gas_side));
-    PAS_HIP(ctx, hipStreamWaitEvent(s, ctx->gas_join, 0));
+  if (PAS_GAS_CONCURRENT) {
+    PAS_HIP(ctx, hipEventRecord(slot->join, slot->side));
+    PAS_HIP(ctx, hipStreamWaitEvent(s, slot->join, 0));
   }
   // the wide shapes: the lists' lengths are on the device, so the grid is fixed and threads
   // past the work return at once
@@ -2135,7 +2068,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   ga.side = d_side;
   ga.side_cap = d_side ? side_cap : 0;
   ga.side_count = reinterpret_cast<unsigned long long*>(d_side_count);
-  ga.limit_count = reinterpret_cast<unsigned long long*>(ctx->gas_limit);
+  ga.limit_count = reinterpret_cast<unsigned long long*>(slot->gas_limit);
   constexpr int kGenericBlocks = 512;
   if (K <= 8)
     gas_fit_generic_kernel<8><<<kGenericBlocks, 64, 0, s>>>(ga);

@@ -46,6 +46,53 @@ int ensure_scratch(pas_ctx* ctx, size_t bytes) {
   return PAS_OK;
 }
 
+// PAS_OK, or check_hip's status for a failed call
+static int hip_status(pas_ctx* ctx, hipError_t e, const char* what) {
+  return e == hipSuccess ? PAS_OK : check_hip(ctx, e, what);
+}
+
+AuxSlot* aux_acquire(pas_ctx* ctx, hipStream_t s, size_t bytes, int* rc) {
+  AuxSlot* slot = nullptr;
+  for (AuxSlot& a : ctx->aux_slot)
+    if (a.used && a.stream == s) slot = &a;  // this stream's own slot: stream order
+  if (!slot)
+    for (AuxSlot& a : ctx->aux_slot)
+      if (!a.used && !slot) slot = &a;
+  if (!slot) {  // the least recently used slot, after its last call
+    slot = &ctx->aux_slot[0];
+    for (AuxSlot& a : ctx->aux_slot)
+      if (a.last < slot->last) slot = &a;
+    *rc = hip_status(ctx, hipStreamWaitEvent(s, slot->ev, 0), "aux_acquire: hipStreamWaitEvent");
+    if (*rc) return nullptr;
+  }
+  if (!slot->ev) {
+    *rc = hip_status(ctx, hipEventCreateWithFlags(&slot->ev, hipEventDisableTiming),
+                    "aux_acquire: hipEventCreateWithFlags");
+    if (*rc) return nullptr;
+  }
+  if (bytes > slot->bytes) {
+    if (slot->p) {  // the slot's earlier calls are ordered before s: let them finish
+      *rc = hip_status(ctx, hipStreamSynchronize(s), "aux_acquire: hipStreamSynchronize");
+      if (!*rc) *rc = hip_status(ctx, hipFree(slot->p), "aux_acquire: hipFree");
+      if (*rc) return nullptr;
+      slot->p = nullptr;
+      slot->bytes = 0;
+    }
+    *rc = hip_status(ctx, hipMalloc(&slot->p, bytes), "aux_acquire: hipMalloc");
+    if (*rc) return nullptr;
+    slot->bytes = bytes;
+  }
+  *rc = PAS_OK;
+  return slot;
+}
+
+void aux_release(pas_ctx* ctx, AuxSlot* slot, hipStream_t s) {
+  (void)hipEventRecord(slot->ev, s);
+  slot->stream = s;
+  slot->used = true;
+  slot->last = ++ctx->aux_clock;
+}
+
 static hipEvent_t take_event(pas_ctx* ctx) {
   if (!ctx->event_pool.empty()) {
     hipEvent_t e = ctx->event_pool.back();
@@ -193,16 +240,18 @@ void pas_destroy(pas_ctx* ctx) {
   free_tas(ctx);
   free_gas(ctx);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
-  if (ctx->aux) (void)hipFree(ctx->aux);
+  for (AuxSlot& a : ctx->aux_slot) {
+    if (a.p) (void)hipFree(a.p);
+    if (a.gas_counts) (void)hipFree(a.gas_counts);
+    if (a.gas_limit) (void)hipFree(a.gas_limit);
+    if (a.ev) (void)hipEventDestroy(a.ev);
+    if (a.fork) (void)hipEventDestroy(a.fork);
+    if (a.join) (void)hipEventDestroy(a.join);
+    if (a.side) (void)hipStreamDestroy(a.side);
+  }
   if (ctx->merge_buf) (void)hipFree(ctx->merge_buf);
   if (ctx->label_part) (void)hipFree(ctx->label_part);
-  if (ctx->gas_limit) (void)hipFree(ctx->gas_limit);
-  if (ctx->gas_counts) (void)hipFree(ctx->gas_counts);
   if (ctx->tas_gpass) (void)hipFree(ctx->tas_gpass);
-  if (ctx->gas_limit_ev) (void)hipEventDestroy(ctx->gas_limit_ev);
-  if (ctx->gas_fork) (void)hipEventDestroy(ctx->gas_fork);
-  if (ctx->gas_join) (void)hipEventDestroy(ctx->gas_join);
-  if (ctx->gas_side) (void)hipStreamDestroy(ctx->gas_side);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -1023,11 +1072,12 @@ int pas_gas_limit_count(pas_ctx* ctx, int64_t* n_pods_out) {
   if (!ctx) return PAS_EINVAL;
   if (!n_pods_out) return set_error(ctx, PAS_EINVAL, "pas_gas_limit_count: null output");
   *n_pods_out = 0;
-  if (!ctx->gas_limit) return PAS_OK;  // no fit on this context yet
+  if (ctx->gas_last_slot < 0) return PAS_OK;  // no fit on this context yet
+  const AuxSlot& a = ctx->aux_slot[ctx->gas_last_slot];
   int rc = activate(ctx);
   if (rc) return rc;
-  PAS_HIP(ctx, hipEventSynchronize(ctx->gas_limit_ev));
-  PAS_HIP(ctx, hipMemcpy(n_pods_out, ctx->gas_limit, sizeof(int64_t), hipMemcpyDeviceToHost));
+  PAS_HIP(ctx, hipEventSynchronize(a.ev));
+  PAS_HIP(ctx, hipMemcpy(n_pods_out, a.gas_limit, sizeof(int64_t), hipMemcpyDeviceToHost));
   return PAS_OK;
 }
 

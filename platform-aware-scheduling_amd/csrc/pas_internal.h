@@ -92,6 +92,30 @@ struct GasSnapshot {
   void* free_t = nullptr;
 };
 
+// Per-call device scratch of the _device entry points (TAS rule ranges and pod descriptors,
+// GAS lists, rank rows and list counts), one set per stream in use.  A call takes the slot of
+// its stream (stream order protects it), else a free slot, else the least recently used one
+// after waiting (hipStreamWaitEvent) for that slot's last call: calls on different streams
+// never share scratch while they may run, and calls on two alternating streams (a pipeline
+// of batches) run without waiting for each other.
+struct AuxSlot {
+  void* p = nullptr;  // aux: TAS ranges | desc | keys, or the GAS fit's lists and rank rows
+  size_t bytes = 0;
+  hipStream_t stream = nullptr;
+  bool used = false;      // stream / ev are valid
+  hipEvent_t ev = nullptr;  // recorded on `stream` after the slot's last call
+  uint64_t last = 0;      // use clock (LRU)
+  // the GAS fit's list counts, two sets: a fit uses one (zero) and its prep kernel zeroes the
+  // other for the next fit on this slot (no fill launch per fit)
+  int32_t* gas_counts = nullptr;
+  int gas_counts_set = 0;
+  int64_t* gas_limit = nullptr;  // pods of the slot's last GAS fit past PAS_GAS_MAX_SELECTIONS
+  // a side stream for fit kernels running beside each other (forked / joined per fit)
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+constexpr int kAuxSlots = 2;
+
 struct TimedLaunch {
   hipEvent_t start;
   hipEvent_t stop;
@@ -111,24 +135,14 @@ struct pas_ctx {
   // per-call scratch (grown on demand, never freed inside a launch function)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
-  void* aux = nullptr;  // per-call device table: TAS rule ranges / GAS container steps
-  size_t aux_bytes = 0;
+  pas::AuxSlot aux_slot[pas::kAuxSlots];
+  uint64_t aux_clock = 0;
   int64_t* label_part = nullptr;  // per-workgroup partial counts of the label plan
   void* tas_gpass = nullptr;  // pass bitmaps of clusters past the LDS bitmap (tas_eval)
   size_t tas_gpass_bytes = 0;
   void* merge_buf = nullptr;  // ping-pong rows of the full-list merge (tas_list_merge.hip)
   size_t merge_bytes = 0;
-  int64_t* gas_limit = nullptr;     // pods of the last GAS fit past PAS_GAS_MAX_SELECTIONS
-  // the GAS fit's list counts, two sets: a fit uses one (zero) and its prep kernel zeroes the
-  // other for the next fit (no fill launch per fit); gas_counts_set = the set of the next fit
-  int32_t* gas_counts = nullptr;
-  int gas_counts_set = 0;
-  hipStream_t gas_last_stream = nullptr;  // stream of the last fit that launched its prep
-  bool gas_have_last = false;             // (the null stream is a valid one)
-  hipEvent_t gas_limit_ev = nullptr;  // recorded after that fit
-  // a side stream for fit kernels running beside each other (forked / joined per fit)
-  hipStream_t gas_side = nullptr;
-  hipEvent_t gas_fork = nullptr, gas_join = nullptr;
+  int gas_last_slot = -1;  // aux slot of the last GAS fit (pas_gas_limit_count)
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;
@@ -148,6 +162,11 @@ int check_hip(pas_ctx* ctx, hipError_t e, const char* what);
   } while (0)
 
 int ensure_scratch(pas_ctx* ctx, size_t bytes);
+// The aux slot for a call on stream s with at least `bytes` of aux (ordered after the slot's
+// previous user when that ran on another stream), and its release after the call's launches
+// (records the slot's event on s).  nullptr on error (ctx->err set, *rc the status).
+AuxSlot* aux_acquire(pas_ctx* ctx, hipStream_t s, size_t bytes, int* rc);
+void aux_release(pas_ctx* ctx, AuxSlot* slot, hipStream_t s);
 int activate(pas_ctx* ctx);  // hipSetDevice(ctx->device)
 hipStream_t pick_stream(pas_ctx* ctx, void* s);
 

@@ -793,17 +793,18 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
                            align256(sizeof(int4) * 2 * (size_t)n_pods),
                            align256(sizeof(int2) * (size_t)n_pods)};
   const size_t need = sizes[0] + sizes[1] + sizes[2];
-  if (need > ctx->aux_bytes) {
-    if (ctx->aux) {
-      PAS_HIP(ctx, hipStreamSynchronize(s));
-      PAS_HIP(ctx, hipFree(ctx->aux));
-      ctx->aux = nullptr;
-      ctx->aux_bytes = 0;
-    }
-    PAS_HIP(ctx, hipMalloc(&ctx->aux, need));
-    ctx->aux_bytes = need;
-  }
-  char* cur = static_cast<char*>(ctx->aux);
+  // the stream's scratch slot: evals on two alternating streams (a pipeline of batches) run
+  // beside each other, batch i + 1's prep under batch i's eval
+  int rc = PAS_OK;
+  AuxSlot* slot = aux_acquire(ctx, s, need, &rc);
+  if (!slot) return rc;
+  struct ReleaseOnExit {
+    pas_ctx* c;
+    AuxSlot* a;
+    hipStream_t s;
+    ~ReleaseOnExit() { aux_release(c, a, s); }
+  } done{ctx, slot, s};
+  char* cur = static_cast<char*>(slot->p);
   int2* d_ranges = reinterpret_cast<int2*>(cur);
   int4* d_desc = reinterpret_cast<int4*>(cur + sizes[0]);
   int2* d_keys = reinterpret_cast<int2*>(cur + sizes[0] + sizes[1]);

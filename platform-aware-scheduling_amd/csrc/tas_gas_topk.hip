@@ -21,9 +21,8 @@
 // The node values come from node-major copies of the snapshot (vals_t [N][M], pres_t
 // [N][M/64], built once per snapshot change): a lane's rules read its node's own row (the
 // 16 metrics of a 128-byte line together) and one presence word, instead of one line per
-// rule in the metric-major columns.  Pods are bucketed by order row (the eval prep's
-// grouping) and each XCD takes a contiguous run of the buckets, so the first positions of a
-// row — the nodes every pod of that row evaluates — stay in that XCD's L2.
+// rule in the metric-major columns.  A pod's dontschedule rules are compiled once into LDS
+// as value ranges (LazyRule) and read back per round as broadcast LDS reads.
 //
 // Records: key = order key of the node's value under the pod's operator (tas_topk.hip),
 // node = global id (local + node_base); past len: key INT64_MAX, node INT32_MAX.
@@ -38,10 +37,6 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
-#ifndef PAS_LAZY_GROUP
-#define PAS_LAZY_GROUP 0  // 1: pods bucketed by order row first (measured slower: the one-block
-                          // grouping of 64k pods costs more than the L2 locality gains)
-#endif
 constexpr int kWaves = kTpb / 64;
 constexpr int kRuleBatch = 8;  // rule gathers in flight per lane
 constexpr int kMaxRes = PAS_GAS_MAX_RES;
@@ -58,7 +53,6 @@ struct LazyTopkParams {
   const int64_t* vals_t;    // [N][M]
   const uint64_t* pres_t;   // [N][WM]
   int32_t WM;
-  const int4* desc;       // [2P] pods bucketed by order row (tas_group_launch)
   const int64_t* sorted;  // [M][R] ascending present values; fences f1k [M][R/1024], f32
   const int64_t* f1k;
   const int64_t* f32;
@@ -257,13 +251,12 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
   const uint64_t half_mask = half ? ~0ull << 32 : 0xFFFFFFFFull;
   const uint64_t below = half_mask & ((1ull << lane) - 1ull);
   const bool have = pos < a.n_pods;
+  // the pod's descriptor (the eval prep's form): {pod, order row or -1, present count},
+  // {first rule, end rule}; pods in index order (bucketing them by order row first, as the
+  // eval prep does, was measured slower here: the one-block grouping of 64k pods costs more
+  // than the L2 locality gains)
   int4 d0 = make_int4(0, -1, 0, 0), d1 = make_int4(0, 0, 0, 0);
-  if (a.desc) {  // bucketed by order row
-    if (have) {
-      d0 = a.desc[2 * pos];
-      d1 = a.desc[2 * pos + 1];
-    }
-  } else if (have) {  // index order: the same descriptor, computed here
+  if (have) {
     const pas_rule q = a.prio[pos];
     const int32_t cq = (q.metric >= 0 && q.metric < a.M) ? a.cnt[q.metric] : 0;
     const int oq = q.op == PAS_OP_GREATER_THAN ? kOrderDesc
@@ -497,29 +490,8 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
     PAS_HIP(ctx, hipGetLastError());
     t.t_epoch = t.epoch;
   }
-  // scratch: desc [2P] | keys [P] of the grouping
-  auto al = [](size_t x) { return (x + 255) & ~size_t(255); };
-  const size_t b_desc = al(sizeof(int4) * 2 * (size_t)n_pods), b_keys = al(sizeof(int2) * n_pods);
-  const size_t b_rng = 0;
-  if (PAS_LAZY_GROUP && b_desc + b_keys + b_rng > ctx->aux_bytes) {
-    if (ctx->aux) {
-      PAS_HIP(ctx, hipStreamSynchronize(s));
-      PAS_HIP(ctx, hipFree(ctx->aux));
-      ctx->aux = nullptr;
-      ctx->aux_bytes = 0;
-    }
-    PAS_HIP(ctx, hipMalloc(&ctx->aux, b_desc + b_keys + b_rng));
-    ctx->aux_bytes = b_desc + b_keys + b_rng;
-  }
-  int4* d_desc = static_cast<int4*>(ctx->aux);
-  int2* d_keys = reinterpret_cast<int2*>(static_cast<char*>(ctx->aux) + b_desc);
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_GAS_TOPK, &tl);
-  if (PAS_LAZY_GROUP) {
-    if (int rc = tas_group_launch(ctx, n_pods, d_prio, d_rule_off, d_desc, d_keys, 0, nullptr,
-                                  nullptr, s))
-      return rc;
-  }
   LazyTopkParams a;
   a.n_pods = n_pods;
   a.N = N;
@@ -538,7 +510,6 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
   a.vals_t = t.vals_t;
   a.pres_t = t.pres_t;
   a.WM = WM;
-  a.desc = PAS_LAZY_GROUP ? d_desc : nullptr;
   a.sorted = t.sorted;
   a.f1k = t.f1k;
   a.f32 = t.f32;

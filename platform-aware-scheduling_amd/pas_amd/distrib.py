@@ -118,11 +118,13 @@ def settle(step, seconds, sync=None, world=1):
         sync()
 
 
-def timed_steps(step, steps, warmup, world, sync=None, gpu=None):
+def timed_steps(step, steps, warmup, world, sync=None, gpu=None, fork=None, join=None):
     """Run `warmup` untimed steps, then time exactly `steps` steps bracketed by
     sync + barrier on both sides; returns the MAX elapsed seconds over ranks.
     gpu: a dict that receives "ms_per_step", the GPU time of the timed steps measured by two
-    HIP events on the current stream around them (no events between the steps)."""
+    HIP events on the current stream around them (no events between the steps).
+    fork / join: called right after the start event and right before the end event (steps
+    launched on streams of their own: those wait for the start and the end waits for them)."""
     if sync is None:
         sync = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
     for _ in range(warmup):
@@ -136,8 +138,12 @@ def timed_steps(step, steps, warmup, world, sync=None, gpu=None):
     t0 = time.perf_counter()
     if ev:
         ev[0].record()
+    if fork:
+        fork()
     for _ in range(steps):
         step()
+    if join:
+        join()
     if ev:
         ev[1].record()
     sync()
