@@ -60,6 +60,21 @@ def dev(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
+# streams of the pipelined run reported beside the headline (same-box sweeps, DESIGN.md §5:
+# TAS best at 2, deeper pipelines thrash the list stores; GAS, issue-bound, gains to 4)
+PIPE_TAS, PIPE_GAS = 2, 4
+
+
+def pipelined_record(depth, elapsed, gpu_ms, units, world, steps, alg_bytes):
+    """The same steps on `depth` streams in turn: whole-job rate and the path's HBM fraction
+    over the GPU time per step (consecutive launches overlap, so a launch's own duration is
+    longer than the time per step: rocprofv3 averages do not apply to this record)."""
+    return {"pipeline_streams": depth, "value": units * world * steps / elapsed,
+            "ms_per_step": elapsed / steps * 1e3, "gpu_ms_per_step": gpu_ms,
+            "achieved_gbs": alg_bytes / (gpu_ms / 1e3) / 1e9,
+            "frac": alg_bytes / (gpu_ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+
+
 def load_traffic(name):
     """Per-launch HBM bytes for `name` from the committed rocprofv3 PMC summary, if any."""
     path = os.path.join(ROOT, "profiles", "traffic.json")
@@ -94,6 +109,48 @@ def snapshot_refresh_ms(ctx, N, M, v_t, p_t, stream, gen=1):
     return out
 
 
+class StreamPipeline:
+    """Consecutive steps on `depth` streams of their own, in turn (depth 1: every step on the
+    launch stream).  launch(k, stream) issues step k's work into output set k % depth, so batch
+    i + 1's prep and first blocks run under batch i's last ones (the context keeps one scratch
+    slot per stream).  fork / join order the streams after the timed region's start event and
+    the end event after them (distrib.timed_steps)."""
+
+    def __init__(self, stream, depth, launch):
+        self.stream, self.depth, self.launch = stream, max(1, depth), launch
+        self.lanes = [stream] if self.depth == 1 else [torch.cuda.Stream()
+                                                      for _ in range(self.depth)]
+        self.turn = 0
+
+    def step(self):
+        k = self.turn % self.depth
+        self.turn += 1
+        self.launch(k, self.lanes[k])
+
+    def fork(self):
+        for ln in self.lanes:
+            if ln is not self.stream:
+                ln.wait_stream(self.stream)
+
+    def join(self):
+        for ln in self.lanes:
+            if ln is not self.stream:
+                self.stream.wait_stream(ln)
+
+    def sync(self):
+        self.join()
+        torch.cuda.synchronize()
+
+    def timed(self, steps, warmup, world):
+        """(wall seconds max over ranks, GPU ms per step) of `steps` timed steps."""
+        for _ in range(warmup):
+            self.step()
+        gpu = {}
+        el = timed_steps(self.step, steps, 0, world, gpu=gpu, fork=self.fork, join=self.join)
+        torch.cuda.synchronize()
+        return el, gpu["ms_per_step"]
+
+
 def bench_tas(args, world, rank):
     P, N, M, R = args.pods, args.nodes, args.metrics, args.rules - 1
     ctx = pas_amd.Context(torch.cuda.current_device())
@@ -114,53 +171,32 @@ def bench_tas(args, world, rank):
     n_rules = len(batch.rules)
     flags = pas_amd.PAS_TAS_FILTER | pas_amd.PAS_TAS_PRIORITIZE
     # --pipeline D: consecutive batches on D streams of their own (outputs per stream), so
-    # batch i + 1's prep and first blocks run under batch i's eval (the context keeps one
-    # scratch slot per stream); D = 1: every step on the launch stream
+    # batch i + 1's prep and first blocks run under batch i's eval; D = 1 (default): every
+    # step on the launch stream.  A pipelined run (PIPE_TAS streams) is reported beside it.
     D = max(1, args.pipeline)
-    lanes = [stream] if D == 1 else [torch.cuda.Stream() for _ in range(D)]
+    depth = max(D, PIPE_TAS)
     outs = [(torch.empty((P, pas_amd.w64(N)), dtype=torch.int64, device="cuda"),
              torch.empty((P, N), dtype=torch.int32, device="cuda"),
-             torch.empty(P, dtype=torch.int32, device="cuda")) for _ in range(D)]
+             torch.empty(P, dtype=torch.int32, device="cuda")) for _ in range(depth)]
     pass_t, order_t, len_t = outs[0]
-    turn = [0]
 
-    def step():
-        k = turn[0] % D
-        turn[0] += 1
+    def launch(k, s):
         pt, ot, lt = outs[k]
-        ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pt, ot, lt,
-                            lanes[k])
+        ctx.tas_eval_device(1, P, n_rules, rules_t, off_t, prio_t, None, flags, pt, ot, lt, s)
 
-    def fork():  # the pipeline streams start after the timed region's start event
-        for ln in lanes:
-            if ln is not stream:
-                ln.wait_stream(stream)
-
-    def join():  # the end event after every pipeline stream's work
-        for ln in lanes:
-            if ln is not stream:
-                stream.wait_stream(ln)
-
-    def sync_all():
-        join()
-        torch.cuda.synchronize()
-
-    settle_steps = distrib.settle(step, args.settle, sync=sync_all, world=world)
-    for _ in range(args.warmup):
-        step()
+    pipe = StreamPipeline(stream, D, launch)
+    step = pipe.step
+    settle_steps = distrib.settle(step, args.settle, sync=pipe.sync, world=world)
     # timed steps: two HIP events on the launch stream around all of them (events between
     # the steps would add ~10 us each to the wall)
-    gpu = {}
-    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu, fork=fork, join=join)
-    torch.cuda.synchronize()
-    span_ms = gpu["ms_per_step"]
+    elapsed, span_ms = pipe.timed(args.steps, args.warmup, world)
     # per-kernel breakdown from extra, untimed steps (events around every launch)
     ctx.reset_timing()
     ctx.set_timing(2)
     n_detail = min(args.steps, 5)
     for _ in range(n_detail):
         step()
-    torch.cuda.synchronize()
+    pipe.sync()
     ctx.set_timing(0)
     kern, launches = {}, {}
     for kid in (_lib.PAS_K_TAS_PREP, _lib.PAS_K_TAS_EVAL):
@@ -213,6 +249,10 @@ def bench_tas(args, world, rank):
             "kernel_ms": kernel_s * 1e3,
         },
     }
+    if D == 1 and PIPE_TAS > 1:
+        el2, ms2 = StreamPipeline(stream, PIPE_TAS, launch).timed(args.steps, args.warmup, world)
+        out["pipelined"] = pipelined_record(PIPE_TAS, el2, ms2, P * N, world, args.steps,
+                                            alg_bytes)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline_tas(snap, batch, args.cpu_seconds)
     if rank == 0 and not args.no_request_latency:
@@ -387,47 +427,33 @@ def bench_gas(args, world, rank):
     # starts on a 128-B line; --gas-pitch dense writes [P][N] rows
     ld = N if args.gas_pitch == "dense" else (N + 31) // 32 * 32
     # --pipeline D: consecutive batches on D streams of their own (results per stream): batch
-    # i + 1's prep kernels run under batch i's fit kernels (one scratch slot per stream)
+    # i + 1's prep kernels run under batch i's fit kernels (one scratch slot per stream); a
+    # pipelined run (PIPE_GAS streams) is reported beside the D = 1 line
     D = max(1, args.pipeline)
-    lanes = [stream] if D == 1 else [torch.cuda.Stream() for _ in range(D)]
-    results = [torch.empty((P, ld), dtype=torch.int32, device="cuda") for _ in range(D)]
+    depth = max(D, PIPE_GAS)
+    results = [torch.empty((P, ld), dtype=torch.int32, device="cuda") for _ in range(depth)]
     res_t = results[0]
-    turn = [0]
 
-    def step():
-        k = turn[0] % D
-        turn[0] += 1
-        ctx.gas_fit_ld_device(1, P, C, wl.I915, req_t, mask_t, nc_t, results[k], ld,
-                              stream=lanes[k])
+    def launch(k, s):
+        ctx.gas_fit_ld_device(1, P, C, wl.I915, req_t, mask_t, nc_t, results[k], ld, stream=s)
 
-    def fork():
-        for ln in lanes:
-            if ln is not stream:
-                ln.wait_stream(stream)
-
-    def join():
-        for ln in lanes:
-            if ln is not stream:
-                stream.wait_stream(ln)
-
-    def sync_all():
-        join()
-        torch.cuda.synchronize()
-
-    settle_steps = distrib.settle(step, args.settle, sync=sync_all, world=world)
-    for _ in range(args.warmup):
-        step()
-    gpu = {}
-    elapsed = timed_steps(step, args.steps, 0, world, gpu=gpu, fork=fork, join=join)
-    torch.cuda.synchronize()
+    pipe = StreamPipeline(stream, D, launch)
+    step = pipe.step
+    settle_steps = distrib.settle(step, args.settle, sync=pipe.sync, world=world)
+    elapsed, gpu_ms = pipe.timed(args.steps, args.warmup, world)
+    gpu = {"ms_per_step": gpu_ms}
     # the fit launches alone, from extra, untimed steps (span events around them)
     ctx.reset_timing()
     ctx.set_timing(1)
     for _ in range(min(args.steps, 5)):
         step()
-    torch.cuda.synchronize()
+    pipe.sync()
     ctx.set_timing(0)
-    if D > 1:
+    pipelined = None
+    if D == 1 and PIPE_GAS > 1:
+        pipelined = StreamPipeline(stream, PIPE_GAS, launch).timed(args.steps, args.warmup,
+                                                                   world)
+    if depth > 1:
         assert all(torch.equal(r, res_t) for r in results[1:]), "pipeline results differ"
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
     # the same batch into dense [P][N] rows (pas_gas_fit_device), untimed extra steps
@@ -471,6 +497,9 @@ def bench_gas(args, world, rank):
                      "traffic": load_traffic("gas_fit_kernel"), "algorithmic_bytes": alg_bytes,
                      "kernel_ms": kernel_s * 1e3},
     }
+    if pipelined:
+        out["pipelined"] = pipelined_record(PIPE_GAS, pipelined[0], pipelined[1], P * N, world,
+                                            args.steps, alg_bytes)
     # The fit kernels are bound by VALU issue, not by HBM: their VALU
     # wave-instructions per step (SQ_INSTS_VALU, committed PMC pass) over the same GPU time,
     # against the chip's issue peak: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU

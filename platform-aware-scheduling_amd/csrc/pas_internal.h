@@ -114,7 +114,7 @@ struct AuxSlot {
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
 };
-constexpr int kAuxSlots = 2;
+constexpr int kAuxSlots = 4;
 
 struct TimedLaunch {
   hipEvent_t start;
