@@ -453,8 +453,8 @@ def bench_gas(args, world, rank):
     if D == 1 and PIPE_GAS > 1:
         pipelined = StreamPipeline(stream, PIPE_GAS, launch).timed(args.steps, args.warmup,
                                                                    world)
-    if depth > 1:
-        assert all(torch.equal(r, res_t) for r in results[1:]), "pipeline results differ"
+    written = max(D, PIPE_GAS if pipelined else 1)  # result sets some step wrote
+    assert all(torch.equal(r, res_t) for r in results[1:written]), "pipeline results differ"
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
     # the same batch into dense [P][N] rows (pas_gas_fit_device), untimed extra steps
     dense_ms = None

@@ -82,7 +82,13 @@ void pas_destroy(pas_ctx* ctx);
 const char* pas_last_error(const pas_ctx* ctx);
 int pas_set_stream(pas_ctx* ctx, void* hip_stream); /* NULL = the context's own stream */
 /* A hip_stream argument (here and in every _device entry point) of NULL names the context's
- * current stream; PAS_STREAM_NULL names the HIP null stream (e.g. torch's default stream). */
+ * current stream; PAS_STREAM_NULL names the HIP null stream (e.g. torch's default stream).
+ * Evaluation calls may be issued on several streams without host synchronisation: the
+ * context keeps per-stream scratch (calls on two or more streams in turn overlap), orders a
+ * call after the last user of the scratch it takes over, and orders readers of data it
+ * derives from a snapshot after that data's build.  A call that CHANGES a resident snapshot
+ * (snapshot_set, snapshot_update, gas_bind, gas_release) must be ordered by the caller after
+ * the calls on other streams that still read it. */
 #define PAS_STREAM_NULL ((void*)1)
 int pas_synchronize(pas_ctx* ctx);
 

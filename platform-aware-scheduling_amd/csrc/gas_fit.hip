@@ -1981,7 +1981,11 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     gas_minfree_kernel<<<(N + kTpb - 1) / kTpb, kTpb, 0, s>>>(N, K, Q, g.n_cards, g.cap, g.used,
                                                              gflip, big_nodes, n_big_nodes,
                                                              static_cast<int64_t*>(g.free_t));
+    PAS_HIP(ctx, hipGetLastError());
     ctx->gas.derived_epoch = ctx->gas.epoch;
+    if (int e = derived_built(ctx, ctx->gas.derived_sync, s)) return e;
+  } else if (int e = derived_wait(ctx, ctx->gas.derived_sync, s)) {
+    return e;  // built by a fit on another stream, maybe still running
   }
   gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(
       n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,

@@ -86,6 +86,24 @@ AuxSlot* aux_acquire(pas_ctx* ctx, hipStream_t s, size_t bytes, int* rc) {
   return slot;
 }
 
+int derived_built(pas_ctx* ctx, DerivedSync& d, hipStream_t s) {
+  if (!d.ev) {
+    int rc = hip_status(ctx, hipEventCreateWithFlags(&d.ev, hipEventDisableTiming),
+                        "derived_built: hipEventCreateWithFlags");
+    if (rc) return rc;
+  }
+  int rc = hip_status(ctx, hipEventRecord(d.ev, s), "derived_built: hipEventRecord");
+  if (rc) return rc;
+  d.stream = s;
+  d.valid = true;
+  return PAS_OK;
+}
+
+int derived_wait(pas_ctx* ctx, const DerivedSync& d, hipStream_t s) {
+  if (!d.valid || d.stream == s) return PAS_OK;  // same stream: stream order
+  return hip_status(ctx, hipStreamWaitEvent(s, d.ev, 0), "derived_wait: hipStreamWaitEvent");
+}
+
 void aux_release(pas_ctx* ctx, AuxSlot* slot, hipStream_t s) {
   (void)hipEventRecord(slot->ev, s);
   slot->stream = s;
@@ -166,7 +184,9 @@ void free_tas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(t.rows));
   free_ptr(t.sort_tmp);
   free_ptr(t.scan_tmp);
+  const hipEvent_t ev = t.t_sync.ev;  // kept for the context's life (pas_destroy)
   t = TasSnapshot{};
+  t.t_sync.ev = ev;
 }
 
 void free_gas(pas_ctx* ctx) {
@@ -176,7 +196,9 @@ void free_gas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(g.used));
   free_ptr(g.derived);
   free_ptr(g.free_t);
+  const hipEvent_t ev = g.derived_sync.ev;
   g = GasSnapshot{};
+  g.derived_sync.ev = ev;
 }
 
 struct Carve {
@@ -239,6 +261,8 @@ void pas_destroy(pas_ctx* ctx) {
   for (hipEvent_t e : ctx->event_pool) (void)hipEventDestroy(e);
   free_tas(ctx);
   free_gas(ctx);
+  if (ctx->tas.t_sync.ev) (void)hipEventDestroy(ctx->tas.t_sync.ev);
+  if (ctx->gas.derived_sync.ev) (void)hipEventDestroy(ctx->gas.derived_sync.ev);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   for (AuxSlot& a : ctx->aux_slot) {
     if (a.p) (void)hipFree(a.p);

@@ -24,6 +24,15 @@ inline int64_t w32(int64_t n) { return (n + 31) / 32; }
 constexpr int kOrderPad = 1024;
 inline int64_t order_row(int64_t n) { return (n + kOrderPad - 1) / kOrderPad * kOrderPad + kOrderPad; }
 
+// Data a call derives from the resident snapshot on its own stream (once per snapshot
+// change) and later calls read, possibly on other streams: an event recorded after the build
+// orders those calls after it (derived_wait).
+struct DerivedSync {
+  hipEvent_t ev = nullptr;
+  hipStream_t stream = nullptr;
+  bool valid = false;
+};
+
 // Device-resident TAS snapshot.  Layout in HBM (M metrics, N nodes, R = order_row(N)):
 //   vals     int64 [M][N]      raw v_milli (deschedule sweep reads it directly)
 //   present  uint64 [M][W64]
@@ -68,6 +77,7 @@ struct TasSnapshot {
   int64_t* vals_t = nullptr;
   uint64_t* pres_t = nullptr;
   size_t t_bytes = 0;
+  DerivedSync t_sync;  // the copies' build
 };
 
 // Device-resident GAS snapshot (node-major):
@@ -90,6 +100,7 @@ struct GasSnapshot {
   // card-major free values of the first 8 cards, free_t[k][q][n] (gas_fit.hip), derived
   // with the above: the fit kernels' per-node loads are then coalesced
   void* free_t = nullptr;
+  DerivedSync derived_sync;  // the derived values' build
 };
 
 // Per-call device scratch of the _device entry points (TAS rule ranges and pod descriptors,
@@ -162,6 +173,9 @@ int check_hip(pas_ctx* ctx, hipError_t e, const char* what);
   } while (0)
 
 int ensure_scratch(pas_ctx* ctx, size_t bytes);
+// After building snapshot-derived data on s / before reading it on s.
+int derived_built(pas_ctx* ctx, DerivedSync& d, hipStream_t s);
+int derived_wait(pas_ctx* ctx, const DerivedSync& d, hipStream_t s);
 // The aux slot for a call on stream s with at least `bytes` of aux (ordered after the slot's
 // previous user when that ran on another stream), and its release after the call's launches
 // (records the slot's event on s).  nullptr on error (ctx->err set, *rc the status).

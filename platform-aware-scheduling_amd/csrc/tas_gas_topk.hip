@@ -489,6 +489,9 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
         N, M, (int32_t)w64(N), WM, t.present, t.pres_t);
     PAS_HIP(ctx, hipGetLastError());
     t.t_epoch = t.epoch;
+    if (int e = derived_built(ctx, t.t_sync, s)) return e;
+  } else if (int e = derived_wait(ctx, t.t_sync, s)) {
+    return e;  // built by a call on another stream, maybe still running
   }
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_GAS_TOPK, &tl);

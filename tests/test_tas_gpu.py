@@ -435,3 +435,50 @@ def test_unknown_operator_on_empty_metric_map(ctx, oracle):
     np.testing.assert_array_equal(got[0], want[0])
     np.testing.assert_array_equal(got[2], want[2])
     np.testing.assert_array_equal(got[1][0, :got[2][0]], want[1][0, :want[2][0]])
+
+
+def test_evals_pipelined_on_streams(oracle):
+    """Batches issued on three streams in turn without host synchronisation (bench.py
+    --pipeline): each stream's calls take their own scratch slot, so consecutive batches
+    overlap; every batch's pass rows, lengths and ordered lists equal the oracle's."""
+    import torch
+    snap = wl.make_tas_snapshot(3000, 8, seed=0x71)
+    batches = [wl.make_tas_batch(snap, p, 6, seed=0x71 + i, cand_frac=0.8)
+               for i, p in enumerate((300, 77, 513, 300))]
+    c = pas_amd.Context(0)
+    try:
+        s0 = torch.cuda.current_stream()
+        c.tas_snapshot_set_device(5, 3000, 8, torch.from_numpy(snap.v_milli).cuda(),
+                                  torch.from_numpy(snap.present.view(np.int64)).cuda(), s0)
+        streams = [torch.cuda.Stream() for _ in range(3)]
+        for st in streams:
+            st.wait_stream(s0)
+        flags = pas_amd.PAS_TAS_FILTER | pas_amd.PAS_TAS_PRIORITIZE
+        outs = []
+        for rep in range(2):
+            for i, b in enumerate(batches):
+                st = streams[(rep * len(batches) + i) % 3]
+                with torch.cuda.stream(st):
+                    t = [torch.from_numpy(np.ascontiguousarray(x)).cuda() for x in
+                         (b.rules.view(np.uint8), b.rule_off, b.prio.view(np.uint8),
+                          b.cand.view(np.int64))]
+                    P = len(b.prio)
+                    pt = torch.empty((P, pas_amd.w64(3000)), dtype=torch.int64, device="cuda")
+                    ot = torch.empty((P, 3000), dtype=torch.int32, device="cuda")
+                    lt = torch.empty(P, dtype=torch.int32, device="cuda")
+                c.tas_eval_device(5, P, len(b.rules), t[0], t[1], t[2], t[3], flags, pt, ot, lt,
+                                  st)
+                outs.append((i, t, pt, ot, lt))
+        torch.cuda.synchronize()
+        for i, _, pt, ot, lt in outs:
+            b = batches[i]
+            wp, wo, wl_ = oracle.tas_eval(snap.v_milli, snap.present, b.rules, b.rule_off, b.prio,
+                                          b.cand, 3)
+            np.testing.assert_array_equal(pt.cpu().numpy().view(np.uint64), wp)
+            gl = lt.cpu().numpy()
+            np.testing.assert_array_equal(gl, wl_)
+            go = ot.cpu().numpy()
+            for p in range(len(gl)):
+                np.testing.assert_array_equal(go[p, :gl[p]], wo[p, :gl[p]])
+    finally:
+        c.close()
