@@ -141,8 +141,11 @@ class StreamPipeline:
         self.join()
         torch.cuda.synchronize()
 
-    def timed(self, steps, warmup, world):
-        """(wall seconds max over ranks, GPU ms per step) of `steps` timed steps."""
+    def timed(self, steps, warmup, world, settle=0.0):
+        """(wall seconds max over ranks, GPU ms per step) of `steps` timed steps, after
+        `settle` seconds of untimed steps and `warmup` more."""
+        if settle > 0:
+            distrib.settle(self.step, settle, sync=self.sync, world=world)
         for _ in range(warmup):
             self.step()
         gpu = {}
@@ -250,7 +253,8 @@ def bench_tas(args, world, rank):
         },
     }
     if D == 1 and PIPE_TAS > 1:
-        el2, ms2 = StreamPipeline(stream, PIPE_TAS, launch).timed(args.steps, args.warmup, world)
+        el2, ms2 = StreamPipeline(stream, PIPE_TAS, launch).timed(args.steps, args.warmup, world,
+                                                                  args.settle)
         out["pipelined"] = pipelined_record(PIPE_TAS, el2, ms2, P * N, world, args.steps,
                                             alg_bytes)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -452,7 +456,7 @@ def bench_gas(args, world, rank):
     pipelined = None
     if D == 1 and PIPE_GAS > 1:
         pipelined = StreamPipeline(stream, PIPE_GAS, launch).timed(args.steps, args.warmup,
-                                                                   world)
+                                                                   world, args.settle)
     written = max(D, PIPE_GAS if pipelined else 1)  # result sets some step wrote
     assert all(torch.equal(r, res_t) for r in results[1:written]), "pipeline results differ"
     k_ms, k_n = ctx.kernel_time(_lib.PAS_K_GAS_FIT)
