@@ -252,7 +252,7 @@ def bench_tas(args, world, rank):
             "kernel_ms": kernel_s * 1e3,
         },
     }
-    if D == 1 and PIPE_TAS > 1:
+    if D == 1 and PIPE_TAS > 1 and not args.no_pipelined:
         el2, ms2 = StreamPipeline(stream, PIPE_TAS, launch).timed(args.steps, args.warmup, world,
                                                                   args.settle)
         out["pipelined"] = pipelined_record(PIPE_TAS, el2, ms2, P * N, world, args.steps,
@@ -454,7 +454,7 @@ def bench_gas(args, world, rank):
     pipe.sync()
     ctx.set_timing(0)
     pipelined = None
-    if D == 1 and PIPE_GAS > 1:
+    if D == 1 and PIPE_GAS > 1 and not args.no_pipelined:
         pipelined = StreamPipeline(stream, PIPE_GAS, launch).timed(args.steps, args.warmup,
                                                                    world, args.settle)
     written = max(D, PIPE_GAS if pipelined else 1)  # result sets some step wrote
@@ -816,8 +816,10 @@ def main():
                     help="collective backend of a multi-rank run (auto: RCCL on GPUs); gloo "
                          "lets several ranks share one GPU (tests)")
     ap.add_argument("--pipeline", type=int, default=1,
-                    help="TAS: consecutive batches on this many streams of their own (1: the "
-                         "launch stream only)")
+                    help="TAS/GAS: consecutive batches on this many streams of their own (1: "
+                         "the launch stream only)")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the pipelined sub-record (kernel profiles of the D = 1 line)")
     ap.add_argument("--no-request-latency", action="store_true",
                     help="skip the f2 request-latency leg of the TAS workload")
     args = ap.parse_args()

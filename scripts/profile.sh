@@ -7,7 +7,7 @@ W="${1:-tas}"; TAG="${2:-$W}"; shift 2 || true
 OUT="$R/gpurun_out/prof_$TAG"; mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-B=(python3 "$R/bench.py" --workload "$W" --no-cpu-baseline --no-request-latency "$@")
+B=(python3 "$R/bench.py" --workload "$W" --no-cpu-baseline --no-request-latency --no-pipelined "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- "${B[@]}" --steps 10 --warmup 2 > "$OUT/kt.log" 2>&1 || exit $?
 for C in FETCH_SIZE WRITE_SIZE "TCC_HIT_sum TCC_MISS_sum" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES GRBM_GUI_ACTIVE"; do
   N="$(echo $C | tr ' ' '_')"

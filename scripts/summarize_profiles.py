@@ -4,6 +4,10 @@
 Writes per workload:
   <round>_<w>_kernel_stats.csv  rocprofv3 --kernel-trace --stats summary, short kernel names
   <round>_<w>_pmc.csv           per-kernel average PMC values per launch
+  <round>_<w>_kernel_resources.csv  per kernel: VGPR / AGPR / SGPR counts, LDS and scratch
+                                bytes, workgroup and grid size of its first dispatch (VGPR as
+                                rocprofv3 reports it on gfx950: half the compiler's granule-
+                                rounded .vgpr_count, e.g. 48 for a 96-VGPR kernel)
 and updates profiles/traffic.json with HBM bytes per launch of the bench's dominant kernel(s):
   bytes = 2 * FETCH_SIZE + WRITE_SIZE  (KB -> bytes).  FETCH_SIZE on gfx950 reports half the
   bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section), WRITE_SIZE is exact for
@@ -47,6 +51,20 @@ def kernel_stats(d):
     return rows
 
 
+def kernel_resources(d):
+    seen = {}
+    with open(os.path.join(d, "kt", "kt_kernel_trace.csv")) as f:
+        for r in csv.DictReader(f):
+            k = short(r["Kernel_Name"])
+            if k not in seen:
+                seen[k] = {"kernel": k, "vgpr": int(r["VGPR_Count"]),
+                           "agpr": int(r["Accum_VGPR_Count"]), "sgpr": int(r["SGPR_Count"]),
+                           "lds_bytes": int(r["LDS_Block_Size"]),
+                           "scratch_bytes": int(r["Scratch_Size"]),
+                           "workgroup": int(r["Workgroup_Size_X"]), "grid": int(r["Grid_Size_X"])}
+    return list(seen.values())
+
+
 def pmc(d):
     agg = defaultdict(list)
     for sub in os.listdir(d):
@@ -72,6 +90,11 @@ def main():
             wr = csv.DictWriter(f, fieldnames=list(rows[0].keys()))
             wr.writeheader()
             wr.writerows(rows)
+        res = kernel_resources(d)
+        with open(os.path.join(OUT, f"{rnd}_{w}_kernel_resources.csv"), "w", newline="") as f:
+            wr = csv.DictWriter(f, fieldnames=list(res[0].keys()))
+            wr.writeheader()
+            wr.writerows(res)
         p = pmc(d)
         kernels = sorted({k for k, _ in p})
         counters = sorted({c for _, c in p})
