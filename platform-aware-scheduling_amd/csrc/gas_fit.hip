@@ -1110,7 +1110,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
         if (q != SKIP) fr[k][j++] = free[k][q];
   }
   int64_t cur[kPacked][kC];
-  uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot (0: stale)
+  uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot
   uint32_t word = 0u, m = 0u, bad_prev = 0u;
   bool fits = true;
 #pragma unroll
@@ -1142,9 +1142,9 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
     }
     uint32_t bad = 0u;
     if (same) {
-      // the need of step t - 1: the entries before t - 1 that are still valid are unchanged
-      // since then (a take only adds an entry and marks the card's older one stale, and the
-      // card taken was not in the old set), so only entry t - 1 is new
+      // the need of step t - 1: the entries before t - 1 are unchanged since then (a take
+      // only adds an entry, and the card taken was not in the old set), so only entry t - 1
+      // is new
       bool ok = true;
 #pragma unroll
       for (int j = 0; j < kC; ++j) ok = ok && need[j] <= cur[t > 0 ? t - 1 : 0][j];
@@ -1178,14 +1178,14 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
 #pragma unroll
       for (int j = 0; j < kC; ++j) g[j] = p[j];
     }
-    // one valid entry per card: the newest take's; the entry it replaces is marked stale
-    // (no card bit) instead of being rewritten
+    // the card's newest entry (later entries override earlier ones).  Older entries of a card
+    // stay: free only falls, so an older entry fails a need only when the newest one does,
+    // and the checks above read them harmlessly
 #pragma unroll
     for (int s2 = 0; s2 < t; ++s2) {
       const bool e = cb[s2] == bc;
 #pragma unroll
       for (int j = 0; j < kC; ++j) g[j] = e ? cur[s2][j] : g[j];
-      cb[s2] = e ? 0u : cb[s2];
     }
 #pragma unroll
     for (int j = 0; j < kC; ++j) {
