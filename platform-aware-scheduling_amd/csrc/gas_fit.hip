@@ -1112,7 +1112,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
   int64_t cur[kPacked][kC];
   uint32_t cb[kPacked];  // the card of each earlier selection's entry, one-hot
   uint32_t word = 0u, m = 0u, bad_prev = 0u;
-  bool fits = true;
+  uint64_t fit_m = __ballot(true);  // lanes whose every step so far found a card
 #pragma unroll
   for (int t = 0; t < kPacked; ++t) {
     if (t >= S) break;
@@ -1170,8 +1170,8 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
       c = lowest(m & ~bad);
       bc = 1u << c;  // c = 8 (no card): bit 8, outside every 8-card mask
     }
-    fits = fits && c < 8u;
-    if (!__ballot(fits)) break;
+    fit_m &= __ballot(c < 8u);  // (a lane mask in SGPRs: one compare per step)
+    if (!fit_m) break;
     int64_t g[kC];
     {
       const int64_t* p = tab.at(min(c, 7u), lane);
@@ -1195,7 +1195,7 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
     cb[t] = bc;
     word |= (c & 7u) << (3 * t);
   }
-  return fits ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
+  return ((fit_m >> lane) & 1u) ? (node_ok | ((uint32_t)S << 24) | word) : 0u;
 }
 
 // Pods of 4 to 8 selections (list `list`, kind SKIP = list - 1 dropped).  Each wave stages
