@@ -27,9 +27,10 @@
 //   - resource.Quantity.UnmarshalJSON (apimachinery v0.22.2 quantity.go): null is the zero
 //     quantity; otherwise the literal bytes, with surrounding quotes removed and spaces
 //     trimmed, go to ParseQuantity (a failure is a decode error).
-// Type checks cover the fields read here; the rest of v1.Pod / v1.Node is skipped as
-// syntax only (a type error deep inside, e.g. a node's "status": 5, fails the reference's
-// decode but not this one — parity unpinned for such bodies, which no kube-scheduler sends).
+// Every field of v1.Pod / v1.NodeList is type-checked against k8s.io/api v0.22.2's Go types
+// (k8s_schema.h: a mistyped field anywhere, e.g. a node's "status": 5 or a malformed
+// creationTimestamp, fails the request as it fails the reference's decode); unknown keys
+// are skipped as syntax.
 #include <emmintrin.h>
 
 #ifdef PAS_DECODE_TRACE  // diagnostic builds: phase times of the threaded decode on stderr
@@ -59,6 +60,7 @@
 #include <vector>
 
 #include "host_pool.h"
+#include "k8s_schema.h"
 #include "pas.h"
 
 namespace {
@@ -453,6 +455,230 @@ bool string_map(Scanner& s, F&& on_entry) {
   });
 }
 
+// ---------------------------------------------------------------------------- typed skip
+//
+// Every value inside the Pod and the nodes is checked against the Go type json.Unmarshal
+// decodes it into (k8s_schema.h), so a request the reference fails with an
+// UnmarshalTypeError (or a Quantity / Time / IntOrString UnmarshalJSON error) fails here too.
+
+std::string trim_space(const std::string& v);  // strings.TrimSpace, below
+
+// strconv.ParseInt(tok, 10, 64) succeeds and the value fits `bits` (reflect OverflowInt):
+// JSON number tokens with a fraction or an exponent fail ParseInt.
+bool go_int_ok(const char* b, const char* e, int bits) {
+  bool neg = false;
+  if (b < e && *b == '-') {
+    neg = true;
+    ++b;
+  }
+  if (b == e) return false;
+  const uint64_t limit = (bits == 32 ? (1ull << 31) : (1ull << 63)) - (neg ? 0 : 1);
+  uint64_t v = 0;
+  for (; b < e; ++b) {
+    if (*b < '0' || *b > '9') return false;
+    const uint64_t d = (uint64_t)(*b - '0');
+    if (v > (limit - d) / 10) return false;
+    v = v * 10 + d;
+  }
+  return true;
+}
+
+// Resource.Quantity.UnmarshalJSON on a value's literal bytes (apimachinery v0.22.2
+// quantity.go): null handled by the caller; one pair of surrounding quotes removed, spaces
+// trimmed, then ParseQuantity.
+// The common forms first: [sign] digits + a suffix of the suffixer's tables, no fraction or
+// exponent, and no byte that trimming could remove (such a string always parses:
+// parseQuantityString accepts it and the digits make the inf.Dec path's SetString succeed);
+// everything else goes through the full ParseQuantity restatement.
+bool quantity_simple(std::string_view q) {
+  size_t i = 0;
+  if (i < q.size() && (q[i] == '-' || q[i] == '+')) ++i;
+  const size_t d0 = i;
+  while (i < q.size() && q[i] >= '0' && q[i] <= '9') ++i;
+  if (i == d0) return false;
+  const std::string_view suf = q.substr(i);
+  static const char* const kSuffixes[] = {"",   "n",  "u",  "m",  "k",  "M",  "G",  "T",
+                                          "P",  "E",  "Ki", "Mi", "Gi", "Ti", "Pi", "Ei"};
+  for (const char* x : kSuffixes)
+    if (suf == x) return true;
+  return false;
+}
+
+bool quantity_literal_ok(const char* b, const char* e) {
+  std::string_view lit(b, (size_t)(e - b));
+  if (lit.size() >= 2 && lit.front() == '"' && lit.back() == '"') lit = lit.substr(1, lit.size() - 2);
+  if (quantity_simple(lit)) return true;
+  const std::string q = trim_space(std::string(lit));
+  int64_t v;
+  return q.find('\0') == std::string::npos && pas_quantity_as_int64(q.c_str(), &v) == PAS_OK;
+}
+
+// time.Parse(time.RFC3339, v) of Go 1.16 (format.go), accept / reject only.  Layout chunks:
+// "2006" (4 bytes, the first a digit, atoi), "-", "01" (2 digits, 1..12), "-", "02"
+// (2 digits), "T", "15" (1 or 2 digits, < 24), ":", "04" (2 digits, < 60), ":", "05"
+// (2 digits, < 60, then an optional '.' + digits: parseNanoseconds, < 1e9), "Z07:00" ('Z',
+// or sign + atoi(2) + ':' + atoi(2), no range check), nothing after; the day must exist in
+// the month (daysIn, leap years).
+bool time_atoi(std::string_view s, int64_t* out) {  // the time package's atoi / leadingInt
+  bool neg = false;
+  if (!s.empty() && (s[0] == '-' || s[0] == '+')) {
+    neg = s[0] == '-';
+    s.remove_prefix(1);
+  }
+  uint64_t x = 0;
+  size_t i = 0;
+  for (; i < s.size() && s[i] >= '0' && s[i] <= '9'; ++i) {
+    if (x > (1ull << 63) / 10) return false;
+    x = x * 10 + (uint64_t)(s[i] - '0');
+    if (x > (1ull << 63)) return false;
+  }
+  if (i != s.size()) return false;
+  const int64_t v = (int64_t)x;  // int(q): 2^63 wraps negative, as in Go
+  *out = neg ? -v : v;
+  return true;
+}
+
+bool rfc3339_ok(std::string_view v) {
+  auto digit = [&](size_t i) { return i < v.size() && v[i] >= '0' && v[i] <= '9'; };
+  auto getnum = [&](bool fixed, int* out) {
+    if (!digit(0)) return false;
+    if (!digit(1)) {
+      if (fixed) return false;
+      *out = v[0] - '0';
+      v.remove_prefix(1);
+      return true;
+    }
+    *out = (v[0] - '0') * 10 + (v[1] - '0');
+    v.remove_prefix(2);
+    return true;
+  };
+  auto lit = [&](char c) {
+    if (v.empty() || v[0] != c) return false;
+    v.remove_prefix(1);
+    return true;
+  };
+  if (v.size() < 4 || !digit(0)) return false;
+  int64_t year;
+  if (!time_atoi(v.substr(0, 4), &year)) return false;
+  v.remove_prefix(4);
+  int month, day, hour, minute, sec;
+  if (!lit('-') || !getnum(true, &month) || month < 1 || month > 12) return false;
+  if (!lit('-') || !getnum(true, &day)) return false;
+  if (!lit('T') || !getnum(false, &hour) || hour >= 24) return false;
+  if (!lit(':') || !getnum(true, &minute) || minute >= 60) return false;
+  if (!lit(':') || !getnum(true, &sec) || sec >= 60) return false;
+  if (v.size() >= 2 && v[0] == '.' && digit(1)) {  // fractional seconds the layout lacks
+    size_t n = 2;
+    while (digit(n)) ++n;
+    int64_t ns;
+    if (!time_atoi(v.substr(1, n - 1), &ns) || ns < 0 || ns >= 1000000000) return false;
+    v.remove_prefix(n);
+  }
+  if (!v.empty() && v[0] == 'Z') {
+    v.remove_prefix(1);
+  } else {
+    if (v.size() < 6 || v[3] != ':') return false;
+    int64_t hh, mm;
+    if (!time_atoi(v.substr(1, 2), &hh) || !time_atoi(v.substr(4, 2), &mm)) return false;
+    if (v[0] != '+' && v[0] != '-') return false;
+    v.remove_prefix(6);
+  }
+  if (!v.empty()) return false;  // extra text
+  static const int kDays[12] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+  const bool leap = year % 4 == 0 && (year % 100 != 0 || year % 400 == 0);
+  const int dim = kDays[month - 1] + (month == 2 && leap ? 1 : 0);
+  return day >= 1 && day <= dim;
+}
+
+// The struct field a key decodes into: an exact name match, else the first field (declaration
+// order) whose fold function matches (encoding/json object(): nameIndex, then equalFold).
+const pas_schema::GoField* go_field(const pas_schema::GoType* t, std::string_view key) {
+  for (int32_t i = 0; i < t->n_fields; ++i) {
+    const pas_schema::GoField& f = t->fields[i];
+    if ((size_t)f.len == key.size() && f.name[0] == key[0] &&
+        std::memcmp(f.name, key.data(), key.size()) == 0)
+      return &f;
+  }
+  for (int32_t i = 0; i < t->n_fields; ++i)
+    if (fold_match(t->fields[i].name, key)) return &t->fields[i];
+  return nullptr;
+}
+
+bool check_value(Scanner& s, const pas_schema::GoType* t);
+
+// A struct value; hook(field) returns -1 to check the field's value by its type, else it has
+// consumed the value (1: ok, 0: failed).  Unknown keys are skipped (no DisallowUnknownFields).
+template <class Hook>
+bool check_struct(Scanner& s, const pas_schema::GoType* t, Hook&& hook) {
+  const char c = s.peek();
+  if (c == 'n') return s.literal("null");
+  if (c != '{') return s.mismatch();
+  return s.object([&](std::string_view k) {
+    const pas_schema::GoField* f = go_field(t, k);
+    if (!f) return s.skip();
+    const int r = hook(f);
+    if (r >= 0) return r != 0;
+    return check_value(s, f->type);
+  });
+}
+
+bool check_value(Scanner& s, const pas_schema::GoType* t) {
+  using pas_schema::GoKind;
+  const char c = s.peek();
+  if (c == 'n') return s.literal("null");  // accepted by every kind
+  switch (t->kind) {
+    case GoKind::kString:
+      if (c != '"') return s.mismatch();
+      return s.string(nullptr);
+    case GoKind::kBool:
+      if (c == 't') return s.literal("true");
+      if (c == 'f') return s.literal("false");
+      return s.mismatch();
+    case GoKind::kIntOrString:
+      if (c == '"') return s.string(nullptr);  // intstr.UnmarshalJSON: StrVal
+      [[fallthrough]];                         // else IntVal (int32)
+    case GoKind::kInt32:
+    case GoKind::kInt64: {
+      if (c != '-' && (c < '0' || c > '9')) return s.mismatch();
+      const char* b = s.p;
+      if (!s.number()) return false;
+      if (!go_int_ok(b, s.p, t->kind == GoKind::kInt64 ? 64 : 32)) s.type_err = true;
+      return true;
+    }
+    case GoKind::kQuantity: {
+      const char* b = s.p;
+      if (!s.skip()) return false;
+      if (!quantity_literal_ok(b, s.p)) s.type_err = true;
+      return true;
+    }
+    case GoKind::kTime: {
+      if (c != '"') return s.mismatch();  // json.Unmarshal(b, &str)
+      std::string v;
+      if (!s.string(&v)) return false;
+      if (!rfc3339_ok(v)) s.type_err = true;
+      return true;
+    }
+    case GoKind::kRaw:
+      return s.skip();
+    case GoKind::kMap:
+      if (c != '{') return s.mismatch();
+      return s.object([&](std::string_view) { return check_value(s, t->elem); });
+    case GoKind::kSlice:
+      if (c != '[') return s.mismatch();
+      return s.array([&](int64_t) { return check_value(s, t->elem); });
+    case GoKind::kStruct:
+      return check_struct(s, t, [](const pas_schema::GoField*) { return -1; });
+  }
+  return s.skip();
+}
+
+// The whole v1.Pod value type-checked (the pod entry points decode a pod on its own; the Args
+// decode checks it in place).
+bool pod_typed_ok(const char* pod, int64_t len) {
+  Scanner s{pod, pod + len};
+  return check_value(s, &pas_schema::Pod) && !s.syntax_err && !s.type_err;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------- name table
@@ -487,20 +713,16 @@ struct NodeList {
   std::vector<int64_t> spans;  // [2 * i]: offset, length of item i's latest decode
 };
 
-// v1.Node: metadata.name (the only field read); *name keeps its value on null / absence.
+// v1.Node: metadata.name is read (*name keeps its value on null / absence); every other
+// field is type-checked (k8s_schema.h).
 bool decode_node(Scanner& s, std::string* name) {
-  const char c = s.peek();
-  if (c == 'n') return s.literal("null");  // null into a struct: no effect
-  if (c != '{') return s.mismatch();
-  return s.object([&](std::string_view k) {
-    if (!fold_match("metadata", k)) return s.skip();
-    const char m = s.peek();
-    if (m == 'n') return s.literal("null");
-    if (m != '{') return s.mismatch();
-    return s.object([&](std::string_view mk) {
-      if (!fold_match("name", mk)) return s.skip();
-      return string_field(s, name);
-    });
+  using namespace pas_schema;
+  return check_struct(s, &Node, [&](const GoField* f) -> int {
+    if (f->type != &ObjectMeta) return -1;
+    return check_struct(s, &ObjectMeta, [&](const GoField* mf) -> int {
+      if (mf != &ObjectMeta_fields[0]) return -1;  // "name"
+      return string_field(s, name) ? 1 : 0;
+    }) ? 1 : 0;
   });
 }
 
@@ -540,11 +762,7 @@ bool decode_node_list(Scanner& s, NodeList* out, const char* base, ItemIndex* id
       out->spans.resize(2 * n);
       return ok;
     }
-    if (fold_match("metadata", k)) {  // ListMeta: object or null
-      const char c = s.peek();
-      if (c != '{' && c != 'n') return s.mismatch();
-      return s.skip();
-    }
+    if (fold_match("metadata", k)) return check_value(s, &pas_schema::ListMeta);
     if (fold_match("kind", k) || fold_match("apiVersion", k)) {
       std::string ignored;
       return string_field(s, &ignored);
@@ -1051,7 +1269,7 @@ int decode_args_core(const char* body, int64_t len, int32_t which,
         if (c == 'n') return s.literal("null");  // a struct keeps its value
         if (c != '{') return s.mismatch();
         pod_b = s.p;
-        if (!s.skip()) return false;
+        if (!check_value(s, &pas_schema::Pod)) return false;  // v1.Pod, type-checked
         pod_e = s.p;
         return true;
       }
@@ -1251,7 +1469,7 @@ int pas_decode_pod_policy(const char* pod, int64_t len, const char* label, char*
         });
       });
     }
-    if (!ok || s.syntax_err || s.type_err) return PAS_EDECODE;
+    if (!ok || s.syntax_err || s.type_err || !pod_typed_ok(pod, len)) return PAS_EDECODE;
   }
   *ns_len = (int64_t)ns.size();
   *label_len = has_label ? (int64_t)value.size() : -1;
@@ -1383,7 +1601,7 @@ int pas_decode_pod_requests(const char* pod, int64_t len, int32_t n_kinds,
         });
       });
     }
-    if (!ok || s.syntax_err || s.type_err) return PAS_EDECODE;
+    if (!ok || s.syntax_err || s.type_err || !pod_typed_ok(pod, len)) return PAS_EDECODE;
   }
   *n_containers = (int32_t)cont.size();
   *n_unknown = 0;

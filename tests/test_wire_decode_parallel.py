@@ -108,7 +108,9 @@ def test_errors_same_as_sequential(case, mutate):
     elif mutate == "control_char":
         items[k] = items[k].replace('"l":"', '"l":"\x01', 1)
     elif mutate == "deep":
-        items[k] = '{"spec":' + "[" * 9997 + "]" * 9997 + "}"  # past encoding/json's 10000
+        # under an unknown key (skipped, still depth-checked by the scanner): an array under
+        # "spec" would be a type error of its own (NodeSpec is a struct)
+        items[k] = '{"x":' + "[" * 9997 + "]" * 9997 + "}"  # past encoding/json's 10000
     body = body_of(items)
     seq = decode(table, body, 1)
     assert seq[0] != 0 or mutate == "deep"
@@ -118,7 +120,7 @@ def test_errors_same_as_sequential(case, mutate):
 def test_depth_just_inside_limit(case):
     table, items = case
     items = list(items[:6000])
-    items[100] = '{"spec":' + "[" * 9995 + "]" * 9995 + "}"  # depth 4 + 9995 < 10001
+    items[100] = '{"x":' + "[" * 9995 + "]" * 9995 + "}"  # depth 4 + 9995 < 10001
     body = body_of(items)
     seq = decode(table, body, 1)
     assert seq[0] == 0
