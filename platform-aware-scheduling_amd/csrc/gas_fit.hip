@@ -496,10 +496,17 @@ __device__ __forceinline__ void put_result(ResOut res, uint64_t* __restrict__ fi
 struct BlockTile {
   int32_t node_block, chunk, chunks;
 };
+#ifndef PAS_GAS_POD_MAJOR
+#define PAS_GAS_POD_MAJOR 0  // 1: a chunk's node blocks consecutive on an XCD (diagnostic)
+#endif
 __device__ __forceinline__ BlockTile block_tile(int32_t chunks) {
   const int32_t nb = gridDim.x, b = blockIdx.x;
   const int32_t xcd = b & 7, per = nb >> 3, rem = nb & 7;
   const int32_t pos = xcd * per + min(xcd, rem) + (b >> 3);
+  if (PAS_GAS_POD_MAJOR) {
+    const int32_t node_blocks = nb / chunks;
+    return BlockTile{pos % node_blocks, pos / node_blocks, chunks};
+  }
   return BlockTile{pos / chunks, pos % chunks, chunks};
 }
 
