@@ -94,6 +94,21 @@ __global__ void oneshot_rows(uint32_t* res, int P, int N, int pitch, int node_bl
   }
 }
 
+// map 7: row streams (the TAS ordered lists' pattern): a block writes whole rows front to back
+// (4 KB per iteration: 16 B per lane), blocks b, b + G, ... of a G-block grid
+__global__ void row_streams(uint32_t* res, int P, int N, int pitch, int aux) {
+  typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+  for (int p = blockIdx.x; p < P; p += gridDim.x) {
+    const __amdgpu_buffer_rsrc_t row =
+        __builtin_amdgcn_make_buffer_rsrc(res + (int64_t)p * pitch, 0, N * 4, 0x00020000);
+    for (int n = threadIdx.x * 4; n < N; n += blockDim.x * 4) {
+      const v4u w = {(uint32_t)p, (uint32_t)n, 2u, 3u};
+      if (aux) __builtin_amdgcn_raw_buffer_store_b128(w, row, n * 4, 0, 2);
+      else __builtin_amdgcn_raw_buffer_store_b128(w, row, n * 4, 0, 0);
+    }
+  }
+}
+
 extern "C" int run(uint32_t* res, int P, int N, int pitch, int npl, int tpb, int blocks_target,
                    int aux, int map, int iters, float* ms) {
   const int node_blocks = (N + tpb * npl - 1) / (tpb * npl);
@@ -101,7 +116,9 @@ extern "C" int run(uint32_t* res, int P, int N, int pitch, int npl, int tpb, int
   auto launch = [&] {
     const dim3 g(node_blocks * chunks);
     const int64_t vecs = ((int64_t)P * N + 3) / 4;
-    if (map == 4 || map == 5) {
+    if (map == 7) {
+      row_streams<<<blocks_target, tpb>>>(res, P, N, pitch, aux);
+    } else if (map == 4 || map == 5) {
       const int nbk = (N + tpb * npl - 1) / (tpb * npl);
       if (npl == 1) oneshot_rows<1><<<P * nbk, tpb>>>(res, P, N, pitch, nbk, aux, map == 5);
       else oneshot_rows<4><<<P * nbk, tpb>>>(res, P, N, pitch, nbk, aux, map == 5);

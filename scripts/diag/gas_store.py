@@ -25,6 +25,10 @@ if os.environ.get("GAS_STORE_ONESHOT"):  # one-shot row pieces vs the looped til
     cases = [(m, 50_016, 4, 256, 0, 1) for m in (4, 5)]
     cases += [(m, 50_016, npl, 256, b, 1) for m in (0, 1, 6) for npl in (1, 4)
               for b in (2048, 8192, 32768)]
+if os.environ.get("GAS_STORE_STREAMS"):  # whole-row streams (TAS lists): concurrency sweep
+    cases = [(4, 50_016, 4, 256, 0, 1)]
+    cases += [(7, 50_016, 4, t, g, a) for t in (256, 1024) for g in (128, 256, 512, 1024, 2048, 4096)
+              for a in (1, 0)]
 if os.environ.get("GAS_STORE_PITCHES"):  # pitch sweep of the fit kernels' mapping (map 0)
     cases = [(0, 50_016 + 32 * i, 1, 256, 8192, 1) for i in range(40)]
     cases += [(0, p, 1, 256, 8192, 1) for p in (51_200, 52_224, 53_248, 57_344, 65_536)]
@@ -35,7 +39,8 @@ for m, pitch, npl, tpb, blocks, aux in cases:
     print(f"map={m} pitch={pitch} npl={npl} tpb={tpb:4d} blocks={blocks:5d} "
           f"{'nt   ' if aux else 'plain'}: {ms.value * 1e3:7.1f} us "
           f"{gb / ms.value:6.0f} GB/s", flush=True)
-if os.environ.get("GAS_STORE_PITCHES") or os.environ.get("GAS_STORE_ONESHOT"):
+if os.environ.get("GAS_STORE_PITCHES") or os.environ.get("GAS_STORE_ONESHOT") or \
+        os.environ.get("GAS_STORE_STREAMS"):
     sys.exit(0)
 t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 y = x[:, :N]
