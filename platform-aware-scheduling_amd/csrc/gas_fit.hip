@@ -22,7 +22,10 @@
 // Launches per fit: gas_prep_kernel (lists), gas_rank_prep_kernel (rank groups, below),
 // gas_rfit_single_kernel (one-selection pods), gas_rfit_closed_kernel (two and three
 // selections in closed form), gas_rfit_seq_kernel (four to eight in order),
-// gas_fit_generic_kernel (shapes past 8 cards or 8 selections).
+// gas_fit_generic_kernel (shapes past 8 cards or 8 selections).  The three fit kernels run
+// side by side: the closed-form one on the caller's stream, the single-selection (store-bound)
+// and sequential ones on two side streams of the call's scratch slot, forked after the prep
+// launches and joined before the generic kernel.
 //
 // Rank compression (the ranked fit section): every "need <= free" compare of a group of at
 // most 127 thresholds becomes a compare of 7-bit ranks, four cards of one kind per 32-bit
@@ -44,8 +47,14 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+#ifndef PAS_GAS_SEQ_FIRST
+#define PAS_GAS_SEQ_FIRST 0  // 1: the sequential kernel before the closed-form one (diagnostic)
+#endif
 #ifndef PAS_GAS_CONCURRENT
-#define PAS_GAS_CONCURRENT 2  // 1: multi-selection kernels on a side stream; 2: the single one
+// 1: multi-selection kernels on a side stream; 2: the single-selection one; 3: the single- and
+// the sequential-selection kernels each on a side stream of their own, the closed-form one on
+// the caller's (same-box C3 A/B: 2 -> 3, 0.733-0.737 -> 0.719-0.725 ms)
+#define PAS_GAS_CONCURRENT 3
 #endif
 #ifndef PAS_GAS_BLOCKS_SINGLE
 #define PAS_GAS_BLOCKS_SINGLE 8192  // target blocks of a fit grid: (node block, pod chunk) pairs
@@ -2012,9 +2021,9 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   PAS_HIP(ctx, hipGetLastError());
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
-  // streams of the single-selection (ss) and the multi-selection kernels (ms): disjoint pods,
-  // disjoint result rows; a side stream is forked from s here and joined before the generic
-  // kernel
+  // streams of the single-selection (ss), closed-form (ms) and sequential (qs) kernels:
+  // disjoint pods, disjoint result rows; the side streams are forked from s here and joined
+  // before the generic kernel
   hipStream_t ss = s, ms = s;
   if (PAS_GAS_CONCURRENT) {
     if (!slot->side) {
@@ -2026,20 +2035,34 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     PAS_HIP(ctx, hipStreamWaitEvent(slot->side, slot->fork, 0));
     (PAS_GAS_CONCURRENT == 1 ? ms : ss) = slot->side;
   }
+  hipStream_t qs = ms;  // the sequential kernel's stream (the second side stream with 3)
+  if (PAS_GAS_CONCURRENT == 3) {
+    if (!slot->side2) {
+      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side2, hipStreamNonBlocking));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join2, hipEventDisableTiming));
+    }
+    PAS_HIP(ctx, hipStreamWaitEvent(slot->side2, slot->fork, 0));
+    qs = slot->side2;
+  }
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
-    if (PAS_GAS_CONCURRENT != 2)                                                               \
+    if (PAS_GAS_CONCURRENT != 2 && PAS_GAS_CONCURRENT != 3)                                    \
       gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
           ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
+    if (PAS_GAS_SEQ_FIRST)                                                                     \
+      gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, qs>>>(                                \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
+          counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                      \
     gas_rfit_closed_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, ms>>>(                               \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
         counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
-    gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, ms>>>(                                  \
-        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,     \
-        counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
-    if (PAS_GAS_CONCURRENT == 2)                                                               \
+    if (!PAS_GAS_SEQ_FIRST)                                                                    \
+      gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, qs>>>(                                \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
+          counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                      \
+    if (PAS_GAS_CONCURRENT == 2 || PAS_GAS_CONCURRENT == 3)                                    \
       gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
           ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
@@ -2052,6 +2075,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   if (PAS_GAS_CONCURRENT) {
     PAS_HIP(ctx, hipEventRecord(slot->join, slot->side));
     PAS_HIP(ctx, hipStreamWaitEvent(s, slot->join, 0));
+  }
+  if (PAS_GAS_CONCURRENT == 3) {
+    PAS_HIP(ctx, hipEventRecord(slot->join2, slot->side2));
+    PAS_HIP(ctx, hipStreamWaitEvent(s, slot->join2, 0));
   }
   // the wide shapes: the lists' lengths are on the device, so the grid is fixed and threads
   // past the work return at once

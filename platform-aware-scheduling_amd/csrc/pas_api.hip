@@ -272,6 +272,8 @@ void pas_destroy(pas_ctx* ctx) {
     if (a.fork) (void)hipEventDestroy(a.fork);
     if (a.join) (void)hipEventDestroy(a.join);
     if (a.side) (void)hipStreamDestroy(a.side);
+    if (a.join2) (void)hipEventDestroy(a.join2);
+    if (a.side2) (void)hipStreamDestroy(a.side2);
   }
   if (ctx->merge_buf) (void)hipFree(ctx->merge_buf);
   if (ctx->label_part) (void)hipFree(ctx->label_part);

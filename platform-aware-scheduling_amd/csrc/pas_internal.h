@@ -124,6 +124,8 @@ struct AuxSlot {
   // a side stream for fit kernels running beside each other (forked / joined per fit)
   hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  hipStream_t side2 = nullptr;  // the sequential GAS kernel's side stream (joined per fit)
+  hipEvent_t join2 = nullptr;
 };
 constexpr int kAuxSlots = 4;
 
