@@ -1705,8 +1705,17 @@ __device__ __forceinline__ void rfit_closed_body(
                          tab, res, fit);
 }
 
+// Waves per SIMD the closed-form kernel is compiled for (its LDS allows 6 below four kinds, 5
+// with four).  With all three fit kernels side by side, 6 (80 VGPRs, 80 B of scratch per lane)
+// beats 5 (96 VGPRs, 16 B): C3 0.710-0.723 -> 0.684-0.692 ms, same box; 4 (no scratch):
+// 0.743-0.748.
+#ifndef PAS_GAS_CLOSED_WAVES
+#define PAS_GAS_CLOSED_WAVES 6
+#endif
+template <int Q>
+constexpr int closed_waves() { return Q < 4 ? PAS_GAS_CLOSED_WAVES : 5; }
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(5))) void gas_rfit_closed_kernel(
+__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(closed_waves<Q>()))) void gas_rfit_closed_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
