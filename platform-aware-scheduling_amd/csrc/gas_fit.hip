@@ -47,6 +47,17 @@ namespace pas {
 namespace {
 
 constexpr int kTpb = 256;
+#ifndef PAS_GAS_SEQ_TPB
+#define PAS_GAS_SEQ_TPB 128  // threads per block of the sequential kernel (two waves: its 10 KB
+                             // per wave of LDS then fits the CUs the other two fit kernels leave;
+                             // C3 0.687-0.691 -> 0.665-0.672 ms against 256, 0.692-0.696 at 64)
+#endif
+constexpr int kSeqTpb = PAS_GAS_SEQ_TPB;
+#ifndef PAS_GAS_CLOSED_TPB
+#define PAS_GAS_CLOSED_TPB 256  // threads per block of the closed-form kernel (128: C3 0.670 ->
+                                // 0.698-0.700 ms, 64: 0.700-0.702)
+#endif
+constexpr int kClosedTpb = PAS_GAS_CLOSED_TPB;
 #ifndef PAS_GAS_SEQ_FIRST
 #define PAS_GAS_SEQ_FIRST 0  // 1: the sequential kernel before the closed-form one (diagnostic)
 #endif
@@ -1694,7 +1705,7 @@ __device__ __forceinline__ void rfit_closed_body(
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ counts, ResOut res, uint64_t* __restrict__ fit) {
-  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const int32_t n = bt.node_block * kClosedTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
@@ -1715,12 +1726,12 @@ __device__ __forceinline__ void rfit_closed_body(
 template <int Q>
 constexpr int closed_waves() { return Q < 4 ? PAS_GAS_CLOSED_WAVES : 5; }
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(closed_waves<Q>()))) void gas_rfit_closed_kernel(
+__global__ __launch_bounds__(kClosedTpb) __attribute__((amdgpu_waves_per_eu(closed_waves<Q>()))) void gas_rfit_closed_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ counts, int32_t chunks, ResOut res, uint64_t* __restrict__ fit) {
-  __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kRanked / 16];
+  __shared__ int4 smem[kClosedTpb / 64][MultiLds<Q>::kRanked / 16];
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_closed_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
                              n_cards, free_t, rm, rw, srt, counts, res, fit);
@@ -1733,7 +1744,7 @@ __device__ __forceinline__ void rfit_seq_body(
     const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, ResOut res,
     uint64_t* __restrict__ fit) {
-  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const int32_t n = bt.node_block * kSeqTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
@@ -1747,13 +1758,13 @@ __device__ __forceinline__ void rfit_seq_body(
 }
 
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_rfit_seq_kernel(
+__global__ __launch_bounds__(kSeqTpb) void gas_rfit_seq_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
     const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
     ResOut res, uint64_t* __restrict__ fit) {
-  __shared__ int4 smem[kTpb / 64][MultiLds<Q>::kSeq / 16];
+  __shared__ int4 smem[kSeqTpb / 64][MultiLds<Q>::kSeq / 16];
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P, n_cards,
                           free_t, rq, srt, multi, sels, counts, res, fit);
@@ -2023,7 +2034,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   // device-counted lists evenly over the chunks
   const int32_t nb_s = (N + kTpb - 1) / kTpb;
   const int32_t ch_s = (n_pods + kRankMax - 1) / kRankMax;  // fixed one-group chunks
-  const int32_t ch_m = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_s - 1) / nb_s));
+  const int32_t nb_c = (N + kClosedTpb - 1) / kClosedTpb;  // the closed-form kernel's
+  const int32_t ch_c = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_c - 1) / nb_c));
+  const int32_t nb_q = (N + kSeqTpb - 1) / kSeqTpb;  // the sequential kernel's node blocks
+  const int32_t ch_q = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_q - 1) / nb_q));
   gas_rank_prep_kernel<<<kRankPrepBlocks, kRankPrepTpb, 0, s>>>(
       n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword, rseq);
   timing_end(ctx, s, &tl);
@@ -2061,16 +2075,16 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
           ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
     if (PAS_GAS_SEQ_FIRST)                                                                     \
-      gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, qs>>>(                                \
+      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                          \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                      \
-    gas_rfit_closed_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, ms>>>(                               \
+          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                      \
+    gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, ms>>>(                         \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
-        counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                        \
+        counts + NL, ch_c, ResOut{d_res, ld_res}, d_fit);                                        \
     if (!PAS_GAS_SEQ_FIRST)                                                                    \
-      gas_rfit_seq_kernel<QQ, B><<<nb_s * ch_m, kTpb, 0, qs>>>(                                \
+      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                          \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_m, ResOut{d_res, ld_res}, d_fit);                                      \
+          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                      \
     if (PAS_GAS_CONCURRENT == 2 || PAS_GAS_CONCURRENT == 3)                                    \
       gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
