@@ -58,6 +58,11 @@ constexpr int kSeqTpb = PAS_GAS_SEQ_TPB;
                                 // 0.698-0.700 ms, 64: 0.700-0.702)
 #endif
 constexpr int kClosedTpb = PAS_GAS_CLOSED_TPB;
+#ifndef PAS_GAS_SINGLE_TPB
+#define PAS_GAS_SINGLE_TPB 256  // threads per block of the single-selection kernel (128: C3
+                                // 0.665-0.671 -> 0.759-0.763 ms)
+#endif
+constexpr int kSingleTpb = PAS_GAS_SINGLE_TPB;
 #ifndef PAS_GAS_SEQ_FIRST
 #define PAS_GAS_SEQ_FIRST 0  // 1: the sequential kernel before the closed-form one (diagnostic)
 #endif
@@ -1518,7 +1523,7 @@ __device__ __forceinline__ void rfit_single_body(
 #pragma unroll
   for (int l = 0; l <= Q; ++l) most = max(most, counts[l]);
   if (bt.chunk * kRankMax >= __builtin_amdgcn_readfirstlane(most)) return;
-  const int32_t n = bt.node_block * kTpb + threadIdx.x;
+  const int32_t n = bt.node_block * kSingleTpb + threadIdx.x;
   const bool valid = n < N;
   const int32_t nc = valid ? n_cards[n] : 0;
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
@@ -1529,12 +1534,12 @@ __device__ __forceinline__ void rfit_single_body(
 }
 
 template <int Q, bool kBits>
-__global__ __launch_bounds__(kTpb) void gas_rfit_single_kernel(
+__global__ __launch_bounds__(kSingleTpb) void gas_rfit_single_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ counts, int32_t chunks, ResOut res,
     uint64_t* __restrict__ fit) {
-  __shared__ int4 smem[kTpb / 64][SingleLds<Q>::kBytes / 16];  // a slice per wave
+  __shared__ int4 smem[kSingleTpb / 64][SingleLds<Q>::kBytes / 16];  // a slice per wave
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_single_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
                              n_cards, free_t, rs, srt, counts, res, fit);
@@ -2032,7 +2037,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   slot->gas_counts_set = 1 - slot->gas_counts_set;
   // grids: (node block, pod chunk) pairs, ~8192 blocks; each kernel splits each of its
   // device-counted lists evenly over the chunks
-  const int32_t nb_s = (N + kTpb - 1) / kTpb;
+  const int32_t nb_s = (N + kSingleTpb - 1) / kSingleTpb;  // the single-selection kernel's
   const int32_t ch_s = (n_pods + kRankMax - 1) / kRankMax;  // fixed one-group chunks
   const int32_t nb_c = (N + kClosedTpb - 1) / kClosedTpb;  // the closed-form kernel's
   const int32_t ch_c = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_c - 1) / nb_c));
@@ -2071,7 +2076,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
     if (PAS_GAS_CONCURRENT != 2 && PAS_GAS_CONCURRENT != 3)                                    \
-      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
+      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
           ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
     if (PAS_GAS_SEQ_FIRST)                                                                     \
@@ -2086,7 +2091,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
           counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                      \
     if (PAS_GAS_CONCURRENT == 2 || PAS_GAS_CONCURRENT == 3)                                    \
-      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kTpb, 0, ss>>>(                             \
+      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
           ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
     break;
