@@ -78,6 +78,10 @@ constexpr int kSingleTpb = PAS_GAS_SINGLE_TPB;
 #ifndef PAS_GAS_BLOCKS_MULTI
 #define PAS_GAS_BLOCKS_MULTI 8192
 #endif
+#ifndef PAS_GAS_BLOCKS_SEQ
+#define PAS_GAS_BLOCKS_SEQ PAS_GAS_BLOCKS_MULTI  // target blocks of the sequential kernel's grid
+                                                // (2 048 / 4 096 / 16 384: within +-1 %)
+#endif
 constexpr int kPrepTpb = 64;  // pods per prep block: small blocks spread the pods over the CUs
 constexpr int kMaxCards = PAS_GAS_PACKED;  // cards of a fast-path node, in registers
 constexpr int kPacked = PAS_GAS_PACKED;    // selections of a fast-path pod
@@ -2042,7 +2046,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const int32_t nb_c = (N + kClosedTpb - 1) / kClosedTpb;  // the closed-form kernel's
   const int32_t ch_c = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_c - 1) / nb_c));
   const int32_t nb_q = (N + kSeqTpb - 1) / kSeqTpb;  // the sequential kernel's node blocks
-  const int32_t ch_q = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_q - 1) / nb_q));
+  const int32_t ch_q = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_SEQ + nb_q - 1) / nb_q));
   gas_rank_prep_kernel<<<kRankPrepBlocks, kRankPrepTpb, 0, s>>>(
       n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword, rseq);
   timing_end(ctx, s, &tl);
