@@ -1699,8 +1699,12 @@ __device__ __forceinline__ void rmulti_lists(const int64_t* __restrict__ free_t,
 template <int Q>
 struct MultiLds {
   static constexpr int kC = Q > 1 ? Q - 1 : 1;
-  static constexpr size_t kRanked =
-      sizeof(int64_t) * Q * kRankItems + sizeof(GasRMulti) * kRankMB + sizeof(uint32_t) * kMaxCards * 64;
+  // the closed-form kernel: a group's sorted rows (ranking only), overlaid by the pod batch
+  // stage (pod loop only), then the lane's packed-rank table
+  static constexpr size_t kRows = sizeof(int64_t) * Q * kRankItems;
+  static constexpr size_t kRowsOrStage =
+      kRows > sizeof(GasRMulti) * kRankMB ? kRows : sizeof(GasRMulti) * kRankMB;
+  static constexpr size_t kRanked = kRowsOrStage + sizeof(uint32_t) * kMaxCards * 64;
   static constexpr size_t kSeqOver = sizeof(int64_t) * kC * kRankItems >
                                              sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB
                                          ? sizeof(int64_t) * kC * kRankItems
@@ -1719,18 +1723,19 @@ __device__ __forceinline__ void rfit_closed_body(
   const int32_t nc = valid ? n_cards[n] : 0;
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   int64_t* lds = reinterpret_cast<int64_t*>(w);
-  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w + sizeof(int64_t) * Q * kRankItems);
-  uint32_t* tab = reinterpret_cast<uint32_t*>(stage + kRankMB);
+  GasRMulti* stage = reinterpret_cast<GasRMulti*>(w);  // overlays the rows (MultiLds)
+  uint32_t* tab = reinterpret_cast<uint32_t*>(w + MultiLds<Q>::kRowsOrStage);
   rmulti_lists<Q, kBits>(free_t, node_ok, N, n, valid, P, rm, rw, srt, 0, counts, bt, lds, stage,
                          tab, res, fit);
 }
 
-// Waves per SIMD the closed-form kernel is compiled for (its LDS allows 6 below four kinds, 5
-// with four).  With all three fit kernels side by side, 6 (80 VGPRs, 80 B of scratch per lane)
-// beats 5 (96 VGPRs, 16 B): C3 0.710-0.723 -> 0.684-0.692 ms, same box; 4 (no scratch):
-// 0.743-0.748.
+// Waves per SIMD the closed-form kernel is compiled for.  Its LDS (the sorted rows overlaid
+// by the pod stage, MultiLds) allows 8 below four kinds.  With all three fit kernels side by
+// side, same box, C3 ms: 5 waves (96 VGPRs, 16 B of scratch per lane, the rows and the stage
+// apart) 0.710-0.723 -> 6 waves 0.684-0.692 -> overlay 0.660-0.668 -> 7 waves (72 VGPRs,
+// 112 B) 0.648-0.649; 8 waves (64 VGPRs, 144 B) 0.669-0.672; 4 waves 0.743-0.748.
 #ifndef PAS_GAS_CLOSED_WAVES
-#define PAS_GAS_CLOSED_WAVES 6
+#define PAS_GAS_CLOSED_WAVES 7
 #endif
 template <int Q>
 constexpr int closed_waves() { return Q < 4 ? PAS_GAS_CLOSED_WAVES : 5; }
