@@ -20,8 +20,10 @@ import os
 import sys
 import time
 
-import numpy as np
-import torch
+T_START = time.perf_counter()
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "platform-aware-scheduling_amd"))
@@ -860,6 +862,14 @@ def main():
                 # the north_star's node-sharded curve at 1M nodes rides on every multi-GPU
                 # run of the headline workload (the N = 1 line is unchanged)
                 out["node_sharded"] = node_sharded_record(args, world, rank)
+            # orchestration cost of the multi-rank run: each rank's wall time
+            # since its start and its peak host RSS
+            import resource
+            mine = (round(time.perf_counter() - T_START, 1),
+                    resource.getrusage(resource.RUSAGE_SELF).ru_maxrss // 1024)
+            per = distrib.gather_objects(mine, world)
+            out["config"]["rank_wall_s"] = [p[0] for p in per]
+            out["config"]["rank_host_rss_peak_mb"] = [p[1] for p in per]
     if rank == 0:
         print(json.dumps(out), flush=True)
     distrib.teardown(world)

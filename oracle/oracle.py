@@ -15,7 +15,8 @@ from ctypes import POINTER, c_int, c_int32, c_int64, c_uint32, c_void_p
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+# PAS_ORACLE_LIB=<path>: a sanitizer build of the same restatement (make -C oracle sanitize)
+LIB_PATH = os.environ.get("PAS_ORACLE_LIB") or os.path.join(HERE, "build", "liboracle.so")
 
 RULE_DTYPE = np.dtype([("metric", "<i4"), ("op", "<i4"), ("target", "<i8")], align=True)
 RM_MAX_KEYS = 8

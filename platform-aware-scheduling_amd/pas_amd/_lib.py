@@ -236,10 +236,31 @@ SIGNATURES = {
 _lib = None
 
 
+def _load_host_only(path: str) -> ctypes.CDLL:
+    """A host-only build of the C++ translation units (wire encoders, request decode,
+    Quantity parsing) under a sanitizer, `make -C platform-aware-scheduling_amd sanitize`
+    (scripts/sanitize.sh).  It has no HIP code: only the symbols it exports are bound, and a
+    test that reaches a device entry point fails on the missing attribute."""
+    lib = ctypes.CDLL(path)
+    for name, (restype, argtypes) in SIGNATURES.items():
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            continue
+        fn.restype = restype
+        fn.argtypes = argtypes
+    return lib
+
+
 def load() -> ctypes.CDLL:
-    """Load libpas.so once; raises if it has not been built."""
+    """Load libpas.so once; raises if it has not been built.  PAS_HOST_LIB=<path> loads a
+    sanitizer build of the host-only translation units instead (test tooling only)."""
     global _lib
     if _lib is not None:
+        return _lib
+    host = os.environ.get("PAS_HOST_LIB")
+    if host:
+        _lib = _load_host_only(host)
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(
