@@ -63,6 +63,9 @@ constexpr int kClosedTpb = PAS_GAS_CLOSED_TPB;
                                 // 0.665-0.671 -> 0.759-0.763 ms)
 #endif
 constexpr int kSingleTpb = PAS_GAS_SINGLE_TPB;
+#ifndef PAS_GAS_SPIN_SYNC
+#define PAS_GAS_SPIN_SYNC 1  // 1: fork / join the fit's side streams with device flags (0: events)
+#endif
 #ifndef PAS_GAS_SEQ_FIRST
 #define PAS_GAS_SEQ_FIRST 0  // 1: the sequential kernel before the closed-form one (diagnostic)
 #endif
@@ -232,27 +235,50 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
 // and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
 // go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
 // PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
-__global__ __launch_bounds__(kPrepTpb) void gas_prep_kernel(int32_t n_pods, int32_t max_containers, int32_t n_res,
-                                int32_t i915, const int64_t* __restrict__ req,
-                                const uint32_t* __restrict__ mask,
-                                const int32_t* __restrict__ n_containers,
-                                const unsigned long long* __restrict__ gflip,
-                                GasSingle* __restrict__ single, int32_t* __restrict__ multi,
-                                GasSel* __restrict__ sels, int32_t* __restrict__ counts,
-                                int32_t* __restrict__ big_pods, int32_t* __restrict__ n_big_pods,
-                                int32_t* __restrict__ pod_steps, int32_t* __restrict__ counts_next,
-                                int32_t n_counts, int64_t* __restrict__ limit_count,
-                                int64_t* __restrict__ side_count) {
-  const int32_t p = blockIdx.x * kPrepTpb + threadIdx.x;
-  // block 0 zeroes the next fit's counts and this fit's generic-kernel counters (read after
-  // this kernel in stream order), in place of fill launches
-  if (blockIdx.x == 0) {
-    for (int32_t i = threadIdx.x; i < n_counts; i += kPrepTpb) counts_next[i] = 0;
-    if (threadIdx.x == 0) {
-      *limit_count = 0;
-      if (side_count) *side_count = 0;
-    }
+struct PrepArgs {
+  int32_t n_pods, max_containers, n_res, i915;
+  const int64_t* req;
+  const uint32_t* mask;
+  const int32_t* n_containers;
+  const unsigned long long* gflip;
+  GasSingle* single;
+  int32_t* multi;
+  GasSel* sels;
+  int32_t* counts;
+  int32_t* big_pods;
+  int32_t* n_big_pods;
+  int32_t* pod_steps;
+  int32_t* counts_next;
+  int32_t n_counts;
+  int64_t* limit_count;
+  int64_t* side_count;
+};
+
+// Block 0 of the prep zeroes the next fit's counts and this fit's generic-kernel counters
+// (read after the prep in stream order), in place of fill launches.
+template <int TPB>
+__device__ __forceinline__ void prep_zero(const PrepArgs& a) {
+  for (int32_t i = threadIdx.x; i < a.n_counts; i += TPB) a.counts_next[i] = 0;
+  if (threadIdx.x == 0) {
+    *a.limit_count = 0;
+    if (a.side_count) *a.side_count = 0;
   }
+}
+
+__device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
+  const int32_t n_pods = a.n_pods, max_containers = a.max_containers, n_res = a.n_res,
+                i915 = a.i915;
+  const int64_t* __restrict__ req = a.req;
+  const uint32_t* __restrict__ mask = a.mask;
+  const int32_t* __restrict__ n_containers = a.n_containers;
+  const unsigned long long* __restrict__ gflip = a.gflip;
+  GasSingle* __restrict__ single = a.single;
+  int32_t* __restrict__ multi = a.multi;
+  GasSel* __restrict__ sels = a.sels;
+  int32_t* __restrict__ counts = a.counts;
+  int32_t* __restrict__ big_pods = a.big_pods;
+  int32_t* __restrict__ n_big_pods = a.n_big_pods;
+  int32_t* __restrict__ pod_steps = a.pod_steps;
   if (p >= n_pods) return;
   const int32_t nc = min(max(n_containers[p], 0), max_containers);
   const int64_t row = (int64_t)p * max_containers;
@@ -421,6 +447,12 @@ __global__ __launch_bounds__(kPrepTpb) void gas_prep_kernel(int32_t n_pods, int3
   multi[(int64_t)ml * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
 }
 
+// One thread per pod.
+__global__ __launch_bounds__(kPrepTpb) void gas_prep_kernel(PrepArgs a) {
+  if (blockIdx.x == 0) prep_zero<kPrepTpb>(a);
+  prep_pod(a, blockIdx.x * kPrepTpb + threadIdx.x);
+}
+
 // gflip[q] = INT64_MAX - gmin[q] (kept flipped so that a zeroed buffer is the identity of the
 // unsigned atomicMax): per node the minimum free over its cards, per workgroup the minimum
 // over its nodes, one atomic per workgroup and kind.  Nodes without the cards label or not in
@@ -468,16 +500,31 @@ __global__ __launch_bounds__(kTpb) void gas_minfree_kernel(int32_t N, int32_t K,
 // free[k][q] = cap[q] - used[k][q] if cap[q] > 0 and used[k][q] >= 0, else -1 (and -1 for
 // cards the node does not have), from the card-major copy (GasSnapshot::free_t, built by
 // gas_minfree_kernel; one coalesced load per card and kind).
+//
+// free_t[(k Q + q) N + n] through a buffer resource per card (base free_t + k Q N, Q N values):
+// the lane's byte offset n * 8 is the only per-lane operand, so no 64-bit address per card and
+// kind is computed or held live (as plain pointers they spilled to scratch in the closed-form
+// kernel).  gas_fit_launch bounds N so that the offsets fit 32 bits.
+template <int Q>
+__device__ __forceinline__ int64_t free_at(const int64_t* __restrict__ free_t, int32_t N, int k,
+                                           int q, uint32_t off) {
+  typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int64_t*>(free_t) + (size_t)k * Q * (uint32_t)N, 0, Q * N * 8, 0x00020000);
+  const v2u32 v = __builtin_amdgcn_raw_buffer_load_b64(r, off, q * N * 8, 0);
+  return (int64_t)(((uint64_t)v.y << 32) | v.x);
+}
+
 template <int Q>
 __device__ __forceinline__ void load_free_t(int32_t n, bool valid, int32_t N,
                                             const int64_t* __restrict__ free_t,
                                             int64_t (&free)[kMaxCards][Q]) {
-  const int32_t nn = valid ? n : 0;
+  const uint32_t off = valid ? (uint32_t)n * 8u : 0u;
 #pragma unroll
   for (int k = 0; k < kMaxCards; ++k)
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-      const int64_t f = free_t[((int64_t)k * Q + q) * N + nn];
+      const int64_t f = free_at<Q>(free_t, N, k, q, off);
       free[k][q] = valid ? f : -1;
     }
 }
@@ -512,7 +559,7 @@ __device__ __forceinline__ void put_result(ResOut res, uint64_t* __restrict__ fi
     // the pod's row as a buffer (lanes past N store nothing), with the store cache policy
     const __amdgpu_buffer_rsrc_t row =
         __builtin_amdgcn_make_buffer_rsrc(res.w + p * res.ld, 0, N * 4, 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b32(out, row, n * 4, 0, PAS_GAS_STORE_AUX);
+    __builtin_amdgcn_raw_buffer_store_b32(out, row, valid ? n * 4 : N * 4, 0, PAS_GAS_STORE_AUX);
   } else if (valid) {
     res.w[p * res.ld + n] = out;
   }
@@ -865,15 +912,30 @@ __device__ __forceinline__ void chunk_groups(int32_t cnt, int32_t chunks, int32_
 // so a group's sorted rows are contiguous.
 constexpr int kRankPrepTpb = kRankItems * PAS_GAS_MAX_RES;
 constexpr int kRankPrepBlocks = 256;  // one per CU: a group per block at a time
-__global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
-    int32_t P, int32_t Q, const int32_t* counts,
-    const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
-    const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
-    GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti,
-    int32_t* __restrict__ rword, GasRSeq* __restrict__ rseq) {
-  __shared__ int64_t v[PAS_GAS_MAX_RES][kRankItems];
-  __shared__ uint32_t pks[kRankItems];
-  __shared__ int32_t cnt_s[(1 + kClasses) * (PAS_GAS_MAX_RES + 1)];
+struct RankArgs {
+  int32_t P, Q;
+  const int32_t* counts;
+  const GasSingle* single;
+  const int32_t* multi;
+  const GasSel* sels;
+  int64_t* srt_s;
+  int64_t* srt_m;
+  GasRSingle* rsingle;
+  GasRMulti* rmulti;
+  int32_t* rword;
+  GasRSeq* rseq;
+};
+struct RankLds {
+  int64_t v[PAS_GAS_MAX_RES][kRankItems];
+  uint32_t pks[kRankItems];
+  int32_t cnt_s[(1 + kClasses) * (PAS_GAS_MAX_RES + 1)];
+};
+// The groups w = first, first + stride, ... of every list slot, one at a time per block.
+__device__ __forceinline__ void rank_prep_body(const RankArgs& a, int32_t first, int32_t stride,
+                                               RankLds& L) {
+  const int32_t P = a.P, Q = a.Q;
+  const int32_t* counts = a.counts;
+  int32_t (&cnt_s)[(1 + kClasses) * (PAS_GAS_MAX_RES + 1)] = L.cnt_s;
   const int32_t NL = Q + 1, slots = NL * 4;
   // the list counts, loaded once (a slot scan of dependent global loads costs a round trip each)
   if (threadIdx.x < (1 + kClasses) * NL) cnt_s[threadIdx.x] = counts[threadIdx.x];
@@ -893,7 +955,7 @@ __global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
     }
     return (cnt + rank_gs(cls) - 1) / rank_gs(cls);
   };
-  for (int32_t w = blockIdx.x;; w += gridDim.x) {
+  for (int32_t w = first;; w += stride) {
     // the group: w-th over the slots' groups in slot order
     int32_t slot = 0, gi = w;
     for (; slot < slots; ++slot) {
@@ -903,10 +965,16 @@ __global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(
     }
     if (slot >= slots) return;
     __syncthreads();  // the previous group's reads of v / pks are done
-    rank_group(P, Q, counts, slot, gi, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword,
-               rseq, v, pks);
+    rank_group(P, Q, counts, slot, gi, a.single, a.multi, a.sels, a.srt_s, a.srt_m, a.rsingle,
+               a.rmulti, a.rword, a.rseq, L.v, L.pks);
   }
 }
+
+__global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(RankArgs a) {
+  __shared__ RankLds L;
+  rank_prep_body(a, blockIdx.x, gridDim.x, L);
+}
+
 
 // The group's sorted rows of the C compared kinds into the wave's LDS slice [C][128]
 // (positions past the group's items: INT64_MAX).
@@ -997,14 +1065,14 @@ template <int Q, int SKIP, int C>
 __device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t, int32_t n_node,
                                              bool valid, int32_t N, const int64_t* lds,
                                              int32_t n, uint32_t (&fa)[C], uint32_t (&fb)[C]) {
-  const int32_t nn = valid ? n_node : 0;
+  const uint32_t off = valid ? (uint32_t)n_node * 8u : 0u;
 #pragma unroll
   for (int q = 0, j = 0; q < Q; ++q) {
     if (q == SKIP) continue;
     int64_t f[kMaxCards];
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) {
-      const int64_t x = free_t[((int64_t)k * Q + q) * N + nn];
+      const int64_t x = free_at<Q>(free_t, N, k, q, off);
       f[k] = valid ? x : -1;
     }
     uint32_t pos[kMaxCards];
@@ -1298,6 +1366,7 @@ __device__ __forceinline__ void multi_list(const int64_t* __restrict__ free_t, G
       const int32_t pod = pw & 0xFFFFFF;
       const int32_t S = (pw >> 24) & 0xF;
       const GasSel* rec = stage + j * kPacked;
+      if (!kBits && S > kPacked) continue;  // the generic kernel's row (it runs beside this one)
       uint32_t out = 0u;
       if (!(pw & kBadPod)) {
         if (S <= kPacked) {  // 4..8 in order (more: the generic kernel's, 0 here)
@@ -1372,8 +1441,9 @@ __device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, ch
         const int32_t pw = __builtin_amdgcn_readlane(wd, j);
         const int32_t pod = pw & 0xFFFFFF;
         const int32_t S = (pw >> 24) & 0xF;
+        if (!kBits && S > kPacked) continue;  // the generic kernel's row (it runs beside this one)
         uint32_t out = 0u;
-        if (!(pw & kBadPod) && S <= kPacked)  // more: the generic kernel's, 0 here
+        if (!(pw & kBadPod) && S <= kPacked)  // more: the generic kernel's (bitmaps: 0 here)
           out = multi_seq<Q, SKIP, kC, true>(nullptr, stage + j * kPacked, S, 0, node_ok, tab, lane,
                                              (uint32_t)(same_m >> (32 * j)),
                                              &rstage[j].rep[0][0], fa, fb);
@@ -1528,8 +1598,11 @@ __device__ __forceinline__ void rfit_single_body(
   for (int l = 0; l <= Q; ++l) most = max(most, counts[l]);
   if (bt.chunk * kRankMax >= __builtin_amdgcn_readfirstlane(most)) return;
   const int32_t n = bt.node_block * kSingleTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
+  const bool in = n < N;
+  const int32_t nc = in ? n_cards[n] : 0;
+  // word results: a node past the fast kernels' card count is the generic kernel's alone (it
+  // runs beside them), so its lane stores nothing here
+  const bool valid = in && (kBits || nc <= kMaxCards);
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   int64_t* lds = reinterpret_cast<int64_t*>(wlds);
   GasRSingle* stage = reinterpret_cast<GasRSingle*>(wlds + sizeof(int64_t) * Q * kRankItems);
@@ -1719,8 +1792,11 @@ __device__ __forceinline__ void rfit_closed_body(
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ counts, ResOut res, uint64_t* __restrict__ fit) {
   const int32_t n = bt.node_block * kClosedTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
+  const bool in = n < N;
+  const int32_t nc = in ? n_cards[n] : 0;
+  // word results: a node past the fast kernels' card count is the generic kernel's alone (it
+  // runs beside them), so its lane stores nothing here
+  const bool valid = in && (kBits || nc <= kMaxCards);
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   int64_t* lds = reinterpret_cast<int64_t*>(w);
   GasRMulti* stage = reinterpret_cast<GasRMulti*>(w);  // overlays the rows (MultiLds)
@@ -1759,8 +1835,11 @@ __device__ __forceinline__ void rfit_seq_body(
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, ResOut res,
     uint64_t* __restrict__ fit) {
   const int32_t n = bt.node_block * kSeqTpb + threadIdx.x;
-  const bool valid = n < N;
-  const int32_t nc = valid ? n_cards[n] : 0;
+  const bool in = n < N;
+  const int32_t nc = in ? n_cards[n] : 0;
+  // word results: a node past the fast kernels' card count is the generic kernel's alone (it
+  // runs beside them), so its lane stores nothing here
+  const bool valid = in && (kBits || nc <= kMaxCards);
   const uint32_t node_ok = (nc > 0 && nc <= kMaxCards) ? 0x80000000u : 0u;
   // the sequential lists' sorted rows follow every two- and three-selection list's rows
   int64_t item_seq = 0;
@@ -1930,6 +2009,28 @@ __global__ __launch_bounds__(64) void gas_fit_generic_kernel(GenericArgs a) {
   }
 }
 
+// Device-side fork / join of the fit's streams (PAS_GAS_SPIN_SYNC): a one-thread kernel
+// sets a flag to the fit's epoch after the work before it on its stream; another waits on
+// flags before the work after it on its stream.  Host order is the deadlock guard: every
+// wait is enqueued after the signal it waits for, so streams that share a hardware queue
+// still reach the signal first.  A wait gives up after ~2 s of the 100 MHz clock (a signal
+// that never comes is an enqueue failure the host already reported) rather than hang.
+__global__ __launch_bounds__(64) void gas_signal_kernel(uint32_t* flag, uint32_t epoch) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ __launch_bounds__(64) void gas_wait_kernel(const uint32_t* flags, int32_t n,
+                                                      uint32_t epoch) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int32_t i = 0; i < n; ++i)
+    while ((int32_t)(__hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                     epoch) < 0) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return;
+      __builtin_amdgcn_s_sleep(2);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
 }  // namespace
 
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
@@ -1942,6 +2043,9 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   constexpr int32_t kCounts = (1 + kClasses) * (PAS_GAS_MAX_RES + 1) + 1;  // lists + generic pods
   if (Q < 1 || Q > PAS_GAS_MAX_RES) return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   if (n_pods > (1 << 24)) return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: > 2^24 pods");
+  // the fit kernels' 32-bit byte offsets into the card-major free table (free_at)
+  if ((int64_t)N * PAS_GAS_MAX_RES * 8 > INT32_MAX)
+    return set_error(ctx, PAS_ECAPACITY, "pas_gas_fit: more than 2^26 nodes");
   // scratch: single-selection records [Q+1][P] | multi-selection pod words [Q+1][3][P] |
   // their selection rows [Q+1][3][P][8] | the generic path's pods [P] and per-pod selection
   // counts [P] | list counts [Q+1] + [(Q+1)3] and the generic pod count (zeroed together).  The flipped
@@ -2037,10 +2141,12 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   } else if (int e = derived_wait(ctx, ctx->gas.derived_sync, s)) {
     return e;  // built by a fit on another stream, maybe still running
   }
-  gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(
-      n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers, gflip, single,
-      multi, sels, counts, big_pods, n_big_pods, pod_steps, counts_next, kCounts,
-      slot->gas_limit, d_side_count);
+  const PrepArgs pa{n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers,
+                    gflip, single, multi, sels, counts, big_pods, n_big_pods, pod_steps,
+                    counts_next, kCounts, slot->gas_limit, d_side_count};
+  const RankArgs ra{n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword,
+                    rseq};
+  gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(pa);
   PAS_HIP(ctx, hipGetLastError());
   // the prep kernel ran: the other set is zeroed (on s) for the slot's next fit
   slot->gas_counts_set = 1 - slot->gas_counts_set;
@@ -2052,71 +2158,11 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const int32_t ch_c = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_MULTI + nb_c - 1) / nb_c));
   const int32_t nb_q = (N + kSeqTpb - 1) / kSeqTpb;  // the sequential kernel's node blocks
   const int32_t ch_q = std::max(1, std::min(n_pods, (PAS_GAS_BLOCKS_SEQ + nb_q - 1) / nb_q));
-  gas_rank_prep_kernel<<<kRankPrepBlocks, kRankPrepTpb, 0, s>>>(
-      n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword, rseq);
+  gas_rank_prep_kernel<<<kRankPrepBlocks, kRankPrepTpb, 0, s>>>(ra);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   timing_begin(ctx, s, PAS_K_GAS_FIT, &tl);
   const bool bits = d_fit != nullptr;
-  // streams of the single-selection (ss), closed-form (ms) and sequential (qs) kernels:
-  // disjoint pods, disjoint result rows; the side streams are forked from s here and joined
-  // before the generic kernel
-  hipStream_t ss = s, ms = s;
-  if (PAS_GAS_CONCURRENT) {
-    if (!slot->side) {
-      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side, hipStreamNonBlocking));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->fork, hipEventDisableTiming));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join, hipEventDisableTiming));
-    }
-    PAS_HIP(ctx, hipEventRecord(slot->fork, s));
-    PAS_HIP(ctx, hipStreamWaitEvent(slot->side, slot->fork, 0));
-    (PAS_GAS_CONCURRENT == 1 ? ms : ss) = slot->side;
-  }
-  hipStream_t qs = ms;  // the sequential kernel's stream (the second side stream with 3)
-  if (PAS_GAS_CONCURRENT == 3) {
-    if (!slot->side2) {
-      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side2, hipStreamNonBlocking));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join2, hipEventDisableTiming));
-    }
-    PAS_HIP(ctx, hipStreamWaitEvent(slot->side2, slot->fork, 0));
-    qs = slot->side2;
-  }
-  switch (Q * 2 + (bits ? 1 : 0)) {
-#define PAS_GAS_CASE(QQ, B)                                                                    \
-  case QQ * 2 + B:                                                                             \
-    if (PAS_GAS_CONCURRENT != 2 && PAS_GAS_CONCURRENT != 3)                                    \
-      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                             \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
-          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
-    if (PAS_GAS_SEQ_FIRST)                                                                     \
-      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                          \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                      \
-    gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, ms>>>(                         \
-        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
-        counts + NL, ch_c, ResOut{d_res, ld_res}, d_fit);                                        \
-    if (!PAS_GAS_SEQ_FIRST)                                                                    \
-      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                          \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                      \
-    if (PAS_GAS_CONCURRENT == 2 || PAS_GAS_CONCURRENT == 3)                                    \
-      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                             \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
-          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
-    break;
-    PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
-    PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
-#undef PAS_GAS_CASE
-    default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
-  }
-  if (PAS_GAS_CONCURRENT) {
-    PAS_HIP(ctx, hipEventRecord(slot->join, slot->side));
-    PAS_HIP(ctx, hipStreamWaitEvent(s, slot->join, 0));
-  }
-  if (PAS_GAS_CONCURRENT == 3) {
-    PAS_HIP(ctx, hipEventRecord(slot->join2, slot->side2));
-    PAS_HIP(ctx, hipStreamWaitEvent(s, slot->join2, 0));
-  }
   // the wide shapes: the lists' lengths are on the device, so the grid is fixed and threads
   // past the work return at once
   GenericArgs ga;
@@ -2144,13 +2190,136 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   ga.side_cap = d_side ? side_cap : 0;
   ga.side_count = reinterpret_cast<unsigned long long*>(d_side_count);
   ga.limit_count = reinterpret_cast<unsigned long long*>(slot->gas_limit);
-  constexpr int kGenericBlocks = 512;
-  if (K <= 8)
-    gas_fit_generic_kernel<8><<<kGenericBlocks, 64, 0, s>>>(ga);
-  else if (K <= 16)
-    gas_fit_generic_kernel<16><<<kGenericBlocks, 64, 0, s>>>(ga);
-  else
-    gas_fit_generic_kernel<PAS_GAS_MAX_CARDS><<<kGenericBlocks, 64, 0, s>>>(ga);
+  auto generic = [&](hipStream_t st) {
+    constexpr int kGenericBlocks = 512;
+    if (K <= 8)
+      gas_fit_generic_kernel<8><<<kGenericBlocks, 64, 0, st>>>(ga);
+    else if (K <= 16)
+      gas_fit_generic_kernel<16><<<kGenericBlocks, 64, 0, st>>>(ga);
+    else
+      gas_fit_generic_kernel<PAS_GAS_MAX_CARDS><<<kGenericBlocks, 64, 0, st>>>(ga);
+  };
+  // streams of the single-selection (ss), closed-form (ms) and sequential (qs) kernels:
+  // disjoint pods, disjoint result rows; the side streams are forked from s here and joined
+  // at the end.  They and their events exist before the fork is recorded, and every exit after
+  // the fork joins them (Joins), so a later user of the slot never waits on an event that
+  // does not cover side-stream work.
+  if (PAS_GAS_CONCURRENT) {
+    if (!slot->side) {
+      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side, hipStreamNonBlocking));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->fork, hipEventDisableTiming));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join, hipEventDisableTiming));
+    }
+    if (PAS_GAS_CONCURRENT == 3 && !slot->side2) {
+      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side2, hipStreamNonBlocking));
+      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join2, hipEventDisableTiming));
+    }
+  }
+  struct Joins {
+    AuxSlot* a;
+    hipStream_t s;
+    int forked = 0;  // side streams forked and not yet joined
+    hipError_t join() {
+      hipError_t e = hipSuccess;
+      if (forked >= 1 && e == hipSuccess) e = hipEventRecord(a->join, a->side);
+      if (forked >= 1 && e == hipSuccess) e = hipStreamWaitEvent(s, a->join, 0);
+      if (forked >= 2 && e == hipSuccess) e = hipEventRecord(a->join2, a->side2);
+      if (forked >= 2 && e == hipSuccess) e = hipStreamWaitEvent(s, a->join2, 0);
+      forked = 0;
+      return e;
+    }
+    ~Joins() {
+      if (forked) (void)join();  // an error exit: runs before ReleaseOnExit records the slot
+    }
+  } joins{slot, s};
+  // the fork: with PAS_GAS_SPIN_SYNC the side streams start with a wait kernel on the prep's
+  // flag (set by a signal kernel on s after the rank prep); else they wait on an event
+  constexpr bool kSpin = PAS_GAS_SPIN_SYNC && PAS_GAS_CONCURRENT == 3;
+  uint32_t* sync = nullptr;
+  uint32_t epoch = 0;
+  if (kSpin) {
+    if (!slot->gas_sync) {
+      uint32_t* f = nullptr;
+      PAS_HIP(ctx, hipMalloc(&f, 4 * sizeof(uint32_t)));
+      // zero before any side stream can read them (once per slot)
+      if (hipMemsetAsync(f, 0, 4 * sizeof(uint32_t), s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        (void)hipFree(f);
+        return set_error(ctx, PAS_EDEVICE, "pas_gas_fit: sync flags init failed");
+      }
+      slot->gas_sync = f;
+      slot->gas_epoch = 0;
+    }
+    sync = slot->gas_sync;
+    epoch = ++slot->gas_epoch;
+    if (epoch == 0) epoch = ++slot->gas_epoch;  // flags start at 0: never wait for epoch 0
+    gas_signal_kernel<<<1, 64, 0, s>>>(sync, epoch);
+  }
+  hipStream_t ss = s, ms = s, qs = s;
+  if (PAS_GAS_CONCURRENT) {
+    if (kSpin) {
+      gas_wait_kernel<<<1, 64, 0, slot->side>>>(sync, 1, epoch);
+      gas_wait_kernel<<<1, 64, 0, slot->side2>>>(sync, 1, epoch);
+      PAS_HIP(ctx, hipGetLastError());
+      joins.forked = 2;
+    } else {
+      PAS_HIP(ctx, hipEventRecord(slot->fork, s));
+      PAS_HIP(ctx, hipStreamWaitEvent(slot->side, slot->fork, 0));
+      joins.forked = 1;
+      if (PAS_GAS_CONCURRENT == 3) {
+        PAS_HIP(ctx, hipStreamWaitEvent(slot->side2, slot->fork, 0));
+        joins.forked = 2;
+      }
+    }
+    (PAS_GAS_CONCURRENT == 1 ? ms : ss) = slot->side;
+    qs = ms;
+    if (PAS_GAS_CONCURRENT == 3) qs = slot->side2;
+  }
+  // word results: the generic kernel writes its (pod, node) words alone (the fast kernels
+  // skip pods past 8 selections and nodes past 8 cards), so it runs beside them, after the
+  // single-selection kernel on that stream; bitmap rows are or-ed into the fast kernels'
+  // words, so it runs after the join
+  switch (Q * 2 + (bits ? 1 : 0)) {
+#define PAS_GAS_CASE(QQ, B)                                                                    \
+  case QQ * 2 + B:                                                                             \
+    if (PAS_GAS_CONCURRENT != 2 && PAS_GAS_CONCURRENT != 3)                                    \
+      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                       \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
+          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
+    if (PAS_GAS_SEQ_FIRST)                                                                     \
+      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
+          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                     \
+    gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, ms>>>(                         \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
+        counts + NL, ch_c, ResOut{d_res, ld_res}, d_fit);                                       \
+    if (!PAS_GAS_SEQ_FIRST)                                                                    \
+      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
+          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                     \
+    if (PAS_GAS_CONCURRENT == 2 || PAS_GAS_CONCURRENT == 3)                                    \
+      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                       \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
+          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
+    break;
+    PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
+    PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
+#undef PAS_GAS_CASE
+    default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
+  }
+  if (!bits) generic(ss);
+  if (kSpin) {
+    // the join: each side stream sets its flag after its work; s waits for both (enqueued
+    // after the signals)
+    gas_signal_kernel<<<1, 64, 0, ss>>>(sync + 1, epoch);
+    gas_signal_kernel<<<1, 64, 0, qs>>>(sync + 2, epoch);
+    gas_wait_kernel<<<1, 64, 0, s>>>(sync + 1, 2, epoch);
+    PAS_HIP(ctx, hipGetLastError());
+    joins.forked = 0;
+  } else {
+    PAS_HIP(ctx, joins.join());
+  }
+  if (bits) generic(s);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;

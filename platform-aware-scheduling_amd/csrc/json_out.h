@@ -27,11 +27,8 @@ struct JsonOut {
     if (pos < cap) std::memcpy(buf + pos, s, (size_t)(pos + n <= cap ? n : cap - pos));
     pos += n;
   }
+  // inline: for a string literal the compiler folds strlen to a constant
   void lit(const char* s) { raw(s, (int64_t)std::strlen(s)); }
-  template <size_t N>
-  void lit(const char (&s)[N]) {  // a string literal: its length at compile time
-    raw(s, (int64_t)N - 1);
-  }
   void integer(int64_t v) {
     char tmp[24];
     int n = 24;

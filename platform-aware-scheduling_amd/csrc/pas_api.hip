@@ -86,6 +86,22 @@ AuxSlot* aux_acquire(pas_ctx* ctx, hipStream_t s, size_t bytes, int* rc) {
   return slot;
 }
 
+void* slot_buf(pas_ctx* ctx, AuxSlot* slot, int which, size_t bytes, hipStream_t s, int* rc) {
+  *rc = PAS_OK;
+  if (bytes <= slot->buf_bytes[which]) return slot->buf[which];
+  if (slot->buf[which]) {  // the slot's earlier calls are ordered before s: let them finish
+    *rc = hip_status(ctx, hipStreamSynchronize(s), "slot_buf: hipStreamSynchronize");
+    if (!*rc) *rc = hip_status(ctx, hipFree(slot->buf[which]), "slot_buf: hipFree");
+    if (*rc) return nullptr;
+    slot->buf[which] = nullptr;
+    slot->buf_bytes[which] = 0;
+  }
+  *rc = hip_status(ctx, hipMalloc(&slot->buf[which], bytes), "slot_buf: hipMalloc");
+  if (*rc) return nullptr;
+  slot->buf_bytes[which] = bytes;
+  return slot->buf[which];
+}
+
 int derived_built(pas_ctx* ctx, DerivedSync& d, hipStream_t s) {
   if (!d.ev) {
     int rc = hip_status(ctx, hipEventCreateWithFlags(&d.ev, hipEventDisableTiming),
@@ -268,16 +284,16 @@ void pas_destroy(pas_ctx* ctx) {
     if (a.p) (void)hipFree(a.p);
     if (a.gas_counts) (void)hipFree(a.gas_counts);
     if (a.gas_limit) (void)hipFree(a.gas_limit);
+    if (a.gas_sync) (void)hipFree(a.gas_sync);
     if (a.ev) (void)hipEventDestroy(a.ev);
     if (a.fork) (void)hipEventDestroy(a.fork);
     if (a.join) (void)hipEventDestroy(a.join);
     if (a.side) (void)hipStreamDestroy(a.side);
     if (a.join2) (void)hipEventDestroy(a.join2);
     if (a.side2) (void)hipStreamDestroy(a.side2);
+    for (void* b : a.buf)
+      if (b) (void)hipFree(b);
   }
-  if (ctx->merge_buf) (void)hipFree(ctx->merge_buf);
-  if (ctx->label_part) (void)hipFree(ctx->label_part);
-  if (ctx->tas_gpass) (void)hipFree(ctx->tas_gpass);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->own_stream);
   delete ctx;
 }
@@ -571,9 +587,12 @@ int pas_tas_prioritize_request_device(pas_ctx* ctx, uint64_t gen, const pas_rule
   if ((rc = activate(ctx))) return rc;
   size_t ws = 0;
   if ((rc = prio_request_workspace(ctx, n_req, &ws))) return rc;
-  if ((rc = ensure_scratch(ctx, ws))) return rc;
-  return prio_request_launch(ctx, *prio, n_req, d_req_node, d_pos_out, d_len_out, ctx->scratch,
-                             ws, pick_stream(ctx, hip_stream));
+  // the workspace is the stream's aux slot (calls on other streams may run beside this one)
+  hipStream_t s = pick_stream(ctx, hip_stream);
+  SlotScope sc(ctx, s, ws, &rc);
+  if (!sc.slot) return rc;
+  return prio_request_launch(ctx, *prio, n_req, d_req_node, d_pos_out, d_len_out, sc.slot->p, ws,
+                             s);
 }
 
 int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const pas_rule* rules,

@@ -103,6 +103,14 @@ struct GasSnapshot {
   DerivedSync derived_sync;  // the derived values' build
 };
 
+// slot_buf buffers
+enum SlotBuf {
+  kBufGpass = 0,  // pass bitmaps of clusters past the LDS bitmap (tas_eval)
+  kBufMerge = 1,  // cut list and ping-pong rows of the full-list merge (tas_list_merge.hip)
+  kBufLabel = 2,  // per-workgroup partial counts of the label plan (tas_labels.hip)
+  kSlotBufs = 3
+};
+
 // Per-call device scratch of the _device entry points (TAS rule ranges and pod descriptors,
 // GAS lists, rank rows and list counts), one set per stream in use.  A call takes the slot of
 // its stream (stream order protects it), else a free slot, else the least recently used one
@@ -126,6 +134,13 @@ struct AuxSlot {
   hipEvent_t fork = nullptr, join = nullptr;
   hipStream_t side2 = nullptr;  // the sequential GAS kernel's side stream (joined per fit)
   hipEvent_t join2 = nullptr;
+  // device-side fork / join of those streams (gas_fit.hip): flags [prep done, side done,
+  // side2 done] each set to the fit's epoch (a per-slot count of fits)
+  uint32_t* gas_sync = nullptr;
+  uint32_t gas_epoch = 0;
+  // further per-stream buffers of the _device entry points (slot_buf), grown on demand
+  void* buf[kSlotBufs] = {};
+  size_t buf_bytes[kSlotBufs] = {};
 };
 constexpr int kAuxSlots = 4;
 
@@ -145,16 +160,13 @@ struct pas_ctx {
   std::string err;
   pas::TasSnapshot tas;
   pas::GasSnapshot gas;
-  // per-call scratch (grown on demand, never freed inside a launch function)
+  // per-call scratch of the host-buffer entry points, which all run on ctx->stream and
+  // synchronize it before they return (grown on demand; the _device entry points use the
+  // per-stream AuxSlot buffers instead)
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
   pas::AuxSlot aux_slot[pas::kAuxSlots];
   uint64_t aux_clock = 0;
-  int64_t* label_part = nullptr;  // per-workgroup partial counts of the label plan
-  void* tas_gpass = nullptr;  // pass bitmaps of clusters past the LDS bitmap (tas_eval)
-  size_t tas_gpass_bytes = 0;
-  void* merge_buf = nullptr;  // ping-pong rows of the full-list merge (tas_list_merge.hip)
-  size_t merge_bytes = 0;
   int gas_last_slot = -1;  // aux slot of the last GAS fit (pas_gas_limit_count)
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
@@ -183,6 +195,22 @@ int derived_wait(pas_ctx* ctx, const DerivedSync& d, hipStream_t s);
 // (records the slot's event on s).  nullptr on error (ctx->err set, *rc the status).
 AuxSlot* aux_acquire(pas_ctx* ctx, hipStream_t s, size_t bytes, int* rc);
 void aux_release(pas_ctx* ctx, AuxSlot* slot, hipStream_t s);
+// Buffer `which` (SlotBuf) of an acquired slot, at least `bytes`: grown after the slot's
+// earlier calls (ordered before s by aux_acquire) have finished.  nullptr on error (*rc).
+void* slot_buf(pas_ctx* ctx, AuxSlot* slot, int which, size_t bytes, hipStream_t s, int* rc);
+// aux_acquire + aux_release around a scope (every exit records the slot's event on s).
+struct SlotScope {
+  pas_ctx* ctx;
+  AuxSlot* slot;
+  hipStream_t s;
+  SlotScope(pas_ctx* c, hipStream_t st, size_t bytes, int* rc)
+      : ctx(c), slot(aux_acquire(c, st, bytes, rc)), s(st) {}
+  ~SlotScope() {
+    if (slot) aux_release(ctx, slot, s);
+  }
+  SlotScope(const SlotScope&) = delete;
+  SlotScope& operator=(const SlotScope&) = delete;
+};
 int activate(pas_ctx* ctx);  // hipSetDevice(ctx->device)
 hipStream_t pick_stream(pas_ctx* ctx, void* s);
 

@@ -770,21 +770,12 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   // past ~1.1M nodes the pass bitmaps move to global scratch, launched in chunks of pods
   const bool global_pass = eval_lds > 160 * 1024 || env_int("PAS_EVAL_GLOBAL_PASS", 0);
   int32_t chunk = n_pods;
+  size_t gpass_bytes = 0;
   if (global_pass) {
     eval_lds = sizeof(uint32_t) * ((size_t)kMiscWords + 4 * (size_t)kStageWords);
     const size_t row = sizeof(uint32_t) * (size_t)ep.W32p;
     chunk = (int32_t)std::max<size_t>(1, std::min<size_t>(n_pods, (256u << 20) / row));
-    const size_t need = row * (size_t)chunk;
-    if (need > ctx->tas_gpass_bytes) {
-      if (ctx->tas_gpass) {
-        PAS_HIP(ctx, hipStreamSynchronize(s));
-        PAS_HIP(ctx, hipFree(ctx->tas_gpass));
-        ctx->tas_gpass = nullptr;
-        ctx->tas_gpass_bytes = 0;
-      }
-      PAS_HIP(ctx, hipMalloc(&ctx->tas_gpass, need));
-      ctx->tas_gpass_bytes = need;
-    }
+    gpass_bytes = row * (size_t)chunk;  // the stream's slot buffer (below)
   }
   if (n_pods == 0) return PAS_OK;
 
@@ -804,6 +795,9 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
     hipStream_t s;
     ~ReleaseOnExit() { aux_release(c, a, s); }
   } done{ctx, slot, s};
+  // the global pass bitmaps are per stream too: evals on other streams may run beside this one
+  void* gpass = nullptr;
+  if (global_pass && !(gpass = slot_buf(ctx, slot, kBufGpass, gpass_bytes, s, &rc))) return rc;
   char* cur = static_cast<char*>(slot->p);
   int2* d_ranges = reinterpret_cast<int2*>(cur);
   int4* d_desc = reinterpret_cast<int4*>(cur + sizes[0]);
@@ -839,7 +833,7 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   ep.topk = topk;
   ep.out_stride = topk ? topk : N;
   ep.pos_base = 0;
-  ep.gpass = static_cast<uint32_t*>(ctx->tas_gpass);
+  ep.gpass = static_cast<uint32_t*>(gpass);
   using EvalFn = void (*)(EvalParams);
   constexpr int kA = PAS_EVAL_ABLATE;
   EvalFn fn = &tas_eval_kernel<4, 1, kA>;

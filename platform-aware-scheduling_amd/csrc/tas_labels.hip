@@ -114,16 +114,21 @@ void put_patch(JsonOut& o, const char* op, const char* name, const char* value) 
 int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
                       const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                       int64_t* d_total, hipStream_t s) {
-  if (!ctx->label_part)
-    PAS_HIP(ctx, hipMalloc(&ctx->label_part, sizeof(int64_t) * kMaxBlocks));
+  // the partial counts are the stream's slot buffer: plans on other streams may run beside
+  int rc = PAS_OK;
+  SlotScope sc(ctx, s, 0, &rc);
+  if (!sc.slot) return rc;
+  int64_t* part = static_cast<int64_t*>(
+      slot_buf(ctx, sc.slot, kBufLabel, sizeof(int64_t) * kMaxBlocks, s, &rc));
+  if (!part) return rc;
   const int64_t W = ((int64_t)n_nodes + 63) / 64;
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((W + kWaves - 1) / kWaves,
                                                                    kMaxBlocks));
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_LABELS, &tl);
   label_plan_kernel<<<blocks, kTpb, 0, s>>>(n_nodes, n_strat, W, d_viol, d_labels, d_add, d_rem,
-                                            ctx->label_part);
-  label_total_kernel<<<1, kTpb, 0, s>>>(blocks, (int64_t)n_nodes * n_strat, ctx->label_part,
+                                            part);
+  label_total_kernel<<<1, kTpb, 0, s>>>(blocks, (int64_t)n_nodes * n_strat, part,
                                         d_total);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());

@@ -205,6 +205,9 @@ int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t wi
   }
   // the tile cuts of a round, then ping-pong rows [P][sp * width] for the rounds before the
   // last.  A round has n_pairs * (tiles + 1) <= sp * width / kTile + 2 * n_pairs cuts per pod.
+  int acq = PAS_OK;
+  SlotScope sc(ctx, s, 0, &acq);
+  if (!sc.slot) return acq;
   int64_t* key_buf[2] = {nullptr, nullptr};
   int32_t* node_buf[2] = {nullptr, nullptr};
   const int64_t max_cuts = (int64_t)n_pods * ((row + kTile - 1) / kTile + 2 * sp + 2);
@@ -213,17 +216,10 @@ int list_merge_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_shards, int32_t wi
     const size_t half = rounds > 1 ? (size_t)n_pods * row : 0;
     const size_t need =
         2 * half * (sizeof(int64_t) + sizeof(int32_t)) + sizeof(int64_t) * (size_t)max_cuts;
-    if (need > ctx->merge_bytes) {
-      if (ctx->merge_buf) {
-        PAS_HIP(ctx, hipStreamSynchronize(s));
-        PAS_HIP(ctx, hipFree(ctx->merge_buf));
-        ctx->merge_buf = nullptr;
-        ctx->merge_bytes = 0;
-      }
-      PAS_HIP(ctx, hipMalloc(&ctx->merge_buf, need));
-      ctx->merge_bytes = need;
-    }
-    char* base = static_cast<char*>(ctx->merge_buf);
+    // the stream's slot buffer: merges on other streams may run beside this one
+    int rc = PAS_OK;
+    char* base = static_cast<char*>(slot_buf(ctx, sc.slot, kBufMerge, need, s, &rc));
+    if (!base) return rc;
     cut_buf = reinterpret_cast<int64_t*>(base);
     key_buf[0] = cut_buf + max_cuts;
     key_buf[1] = key_buf[0] + half;

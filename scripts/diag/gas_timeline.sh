@@ -24,7 +24,7 @@ for f in glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True):
         if m:
             rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), m.group(1), r["Queue_Id"]))
 rows.sort()
-starts = [i for i, r in enumerate(rows) if r[2] == "gas_prep_kernel"]
+starts = [i for i, r in enumerate(rows) if r[2] in ("gas_prep_kernel", "gas_prep_fused_kernel")]
 for si, ei in list(zip(starts, starts[1:]))[-3:-1]:
     t0 = rows[si][0]
     print("  step", (rows[ei][0] - t0) / 1e3, "us")
