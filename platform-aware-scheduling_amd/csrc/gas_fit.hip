@@ -40,6 +40,9 @@
 // the C3 mix the i915 kind (1 per selection against >= 30 free) goes.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include "gas_runs.h"
 #include "pas_internal.h"
 
@@ -348,6 +351,12 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
   const int32_t slot = wave_slot(counts, one_sel ? l : nl + ml);
   if (one_sel) {
     one.word = p | (steps << 24) | (one_bad ? kBadPod : 0);
+    // no selection: threshold INT64_MIN in every kind, so its group rank is 1 everywhere and
+    // the ranked kernel's mask is non-empty exactly on the nodes that fit (a node without
+    // cards has rank 0 in every card); its word is then node_ok as the reference's (:206-215)
+    if (steps == 0)
+#pragma unroll
+      for (int q = 0; q < PAS_GAS_MAX_RES; ++q) one.cmp[q] = INT64_MIN;
     single[(int64_t)l * n_pods + slot] = one;
     return;
   }
@@ -442,7 +451,8 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
     for (int jj = 0; jj < 7; ++jj)
 #pragma unroll
       for (int q = 0; q < PAS_GAS_MAX_RES; ++q) t->th[jj][q] = th[jj][q];
-    t->over = over;
+    // a bad pod's row 0 never passes (rank 0x80), so its closed-form word is 0 with no branch
+    t->over = over | (bad ? 1 : 0);
   }
   multi[(int64_t)ml * n_pods + slot] = p | (steps << 24) | (bad ? kBadPod : 0);
 }
@@ -741,7 +751,14 @@ __device__ __forceinline__ uint32_t th_mask(const int64_t (&free)[kMaxCards][Q],
   return fit_mask<kC>(need, fr, live);
 }
 
-__device__ __forceinline__ uint32_t lowest(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : 8u; }
+// v_ffbl_b32: the lowest set bit of a lane mask, 0xFFFFFFFF for none, in one instruction (the
+// C form adds a compare and a select for the zero case)
+__device__ __forceinline__ uint32_t ffbl(uint32_t m) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(m));
+  return r;
+}
+__device__ __forceinline__ uint32_t lowest(uint32_t m) { return min(ffbl(m), 8u); }  // 8: none
 
 // ---------------------------------------------------------------------------- ranked fit
 //
@@ -836,7 +853,7 @@ __device__ __forceinline__ void rank_group(
   const bool item = i < n;
   const int32_t mword = !one && item ? multi[(int64_t)ml * P + pos] : 0;
   const uint32_t over = !one && !seq && item ? (uint32_t)th->over : 0u;
-  const int32_t sword = one && item && q == 0 ? single[(int64_t)l * P + pos].word : 0;
+  const int32_t sword = one && item ? single[(int64_t)l * P + pos].word : 0;
   int64_t y = INT64_MAX;
   if (live) {
     if (one) {
@@ -864,7 +881,9 @@ __device__ __forceinline__ void rank_group(
       }
     }
     srt[(base + less + eqb) * PAS_GAS_MAX_RES + j] = y;
-    g = ((over >> row) & 1u) ? 0x80u : (uint32_t)(less + 1);
+    // 0x80 never passes: an overflowing threshold, or (one selection) a bad pod, whose word
+    // is then 0 on every node without a branch in the fit kernel
+    g = (((over >> row) & 1u) || (sword & kBadPod)) ? 0x80u : (uint32_t)(less + 1);
     if (one) {
       rsingle[(int64_t)l * P + pos].g[j] = g * 0x01010101u;
     } else if (seq) {
@@ -1114,7 +1133,7 @@ __device__ __forceinline__ uint32_t rmask(const uint32_t (&fa)[C], const uint32_
 }
 
 // lowest set bit, 0xFFFFFFFF for none (v_ffbl_b32)
-__device__ __forceinline__ uint32_t lowbit(uint32_t m) { return m ? (uint32_t)__builtin_ctz(m) : ~0u; }
+__device__ __forceinline__ uint32_t lowbit(uint32_t m) { return ffbl(m); }
 
 // Lane-private copy of the node's free values of the compared kinds (all but SKIP) in LDS,
 // [card][lane][kind], so that a lane can read its chosen card's values back with one LDS read
@@ -1512,20 +1531,22 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
     fa[j] = node_ok ? fa[j] : 0x80808080u;
     fb[j] = node_ok ? fb[j] : 0x80808080u;
   }
+  // Every pod takes one path: a pod without a selection ranks 1 in every kind and a bad pod
+  // 0x80 (gas_prep_kernel, rank_group), so m is empty exactly where its word is 0, and
+  //   word = m ? base | lowest card : 0,  base = 0x81000000 (one selection) / 0x80000000 (none)
+  // is min_i32((ffbl(m) >> 2) ^ base, 0): ffbl(0) = -1 turns base into a positive value.
   auto one_pod = [&](const GasRSingle& r, int32_t w) {
     const int64_t pod = w & 0xFFFFFF;
-    uint32_t out = node_ok;
-    if (((w >> 24) & 0xF) == 1) {
-      uint32_t g[C];
+    uint32_t g[C];
 #pragma unroll
-      for (int jj = 0; jj < C; ++jj) g[jj] = r.g[jj];
-      if (w & kBadPod) {
-        out = 0u;
-      } else {
-        const uint32_t m = rmask<C>(fa, fb, g);
-        if constexpr (kBits) out = m ? 0x80000000u : 0u;
-        else out = m ? (0x81000000u | (lowbit(m) >> 2)) : 0u;
-      }
+    for (int jj = 0; jj < C; ++jj) g[jj] = r.g[jj];
+    const uint32_t m = rmask<C>(fa, fb, g);
+    uint32_t out;
+    if constexpr (kBits) {
+      out = m ? 0x80000000u : 0u;
+    } else {
+      const int32_t base = ((w >> 24) & 0xF) == 1 ? (int32_t)0x81000000u : (int32_t)0x80000000u;
+      out = (uint32_t)min(((int32_t)ffbl(m) >> 2) ^ base, 0);
     }
     put_result<kBits>(res, fit, pod, N, n, valid, out);
   };
@@ -1731,11 +1752,9 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
           if (j0 + u >= nb) break;
           const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(wd, j0 + u);
           const int64_t pod = w & 0xFFFFFF;
-          uint32_t out = 0u;
-          if (!(w & kBadPod)) {
-            out = rclosed<C, S>(fa, fb, st[u], w, tab, lane, node_ok);
-            if constexpr (kBits) out = out ? node_ok : 0u;
-          }
+          // (a bad pod's row 0 ranks 0x80: its word comes out 0)
+          uint32_t out = rclosed<C, S>(fa, fb, st[u], w, tab, lane, node_ok);
+          if constexpr (kBits) out = out ? node_ok : 0u;
           put_result<kBits>(res, fit, pod, N, n, valid, out);
         }
       }
@@ -2019,16 +2038,36 @@ __global__ __launch_bounds__(64) void gas_signal_kernel(uint32_t* flag, uint32_t
   if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 __global__ __launch_bounds__(64) void gas_wait_kernel(const uint32_t* flags, int32_t n,
-                                                      uint32_t epoch) {
+                                                      uint32_t epoch, uint64_t limit,
+                                                      uint32_t* fault) {
   if (threadIdx.x != 0) return;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   for (int32_t i = 0; i < n; ++i)
     while ((int32_t)(__hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
                      epoch) < 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) return;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {  // reported by the next call
+        __hip_atomic_store(fault, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return;
+      }
       __builtin_amdgcn_s_sleep(2);
     }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// The fork / join mode of a context: PAS_GAS_SYNC=events|flags, else flags unless a tool that
+// runs kernels one at a time is attached (rocprofv3 counter collection or thread trace,
+// AMD_SERIALIZE_KERNEL): such a tool may start a wait kernel before the signal it waits for
+// and hold every other kernel back until the wait gives up, so events are used there.
+int gas_sync_mode() {
+  auto on = [](const char* v) { return v && *v && std::strcmp(v, "0") != 0; };
+  if (const char* m = std::getenv("PAS_GAS_SYNC")) {
+    if (!std::strcmp(m, "events")) return 0;
+    if (!std::strcmp(m, "flags")) return 1;
+  }
+  if (on(std::getenv("ROCPROF_COUNTER_COLLECTION")) ||
+      on(std::getenv("ROCPROF_ADVANCED_THREAD_TRACE")) || on(std::getenv("AMD_SERIALIZE_KERNEL")))
+    return 0;
+  return PAS_GAS_SPIN_SYNC ? 1 : 0;
 }
 
 }  // namespace
@@ -2234,7 +2273,25 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   } joins{slot, s};
   // the fork: with PAS_GAS_SPIN_SYNC the side streams start with a wait kernel on the prep's
   // flag (set by a signal kernel on s after the rank prep); else they wait on an event
-  constexpr bool kSpin = PAS_GAS_SPIN_SYNC && PAS_GAS_CONCURRENT == 3;
+  if (ctx->gas_sync_mode < 0) {
+    ctx->gas_sync_mode = gas_sync_mode();
+    if (ctx->gas_sync_mode) {
+      PAS_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->gas_sync_fault), sizeof(uint32_t),
+                                 hipHostMallocCoherent));
+      *ctx->gas_sync_fault = 0;
+    }
+  }
+  const bool kSpin = ctx->gas_sync_mode == 1 && PAS_GAS_CONCURRENT == 3;
+  // a wait that gave up (its signal never came within the limit): the fit it joined may have
+  // returned before its side streams finished, so this call fails and says so
+  if (kSpin && __atomic_load_n(ctx->gas_sync_fault, __ATOMIC_ACQUIRE)) {
+    *ctx->gas_sync_fault = 0;
+    return set_error(ctx, PAS_EDEVICE,
+                     "pas_gas_fit: a side-stream wait of an earlier fit timed out (its results "
+                     "may be incomplete); set PAS_GAS_SYNC=events under kernel-serializing tools");
+  }
+  // the waits' limit: 1 s plus 10 ns per (pod, node) pair, far past any real fit
+  const uint64_t limit = 100000000ull + (uint64_t)n_pods * (uint64_t)N / 100u;
   uint32_t* sync = nullptr;
   uint32_t epoch = 0;
   if (kSpin) {
@@ -2258,8 +2315,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   hipStream_t ss = s, ms = s, qs = s;
   if (PAS_GAS_CONCURRENT) {
     if (kSpin) {
-      gas_wait_kernel<<<1, 64, 0, slot->side>>>(sync, 1, epoch);
-      gas_wait_kernel<<<1, 64, 0, slot->side2>>>(sync, 1, epoch);
+      gas_wait_kernel<<<1, 64, 0, slot->side>>>(sync, 1, epoch, limit, ctx->gas_sync_fault);
+      gas_wait_kernel<<<1, 64, 0, slot->side2>>>(sync, 1, epoch, limit, ctx->gas_sync_fault);
       PAS_HIP(ctx, hipGetLastError());
       joins.forked = 2;
     } else {
@@ -2313,7 +2370,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     // after the signals)
     gas_signal_kernel<<<1, 64, 0, ss>>>(sync + 1, epoch);
     gas_signal_kernel<<<1, 64, 0, qs>>>(sync + 2, epoch);
-    gas_wait_kernel<<<1, 64, 0, s>>>(sync + 1, 2, epoch);
+    gas_wait_kernel<<<1, 64, 0, s>>>(sync + 1, 2, epoch, limit, ctx->gas_sync_fault);
     PAS_HIP(ctx, hipGetLastError());
     joins.forked = 0;
   } else {

@@ -280,6 +280,7 @@ void pas_destroy(pas_ctx* ctx) {
   if (ctx->tas.t_sync.ev) (void)hipEventDestroy(ctx->tas.t_sync.ev);
   if (ctx->gas.derived_sync.ev) (void)hipEventDestroy(ctx->gas.derived_sync.ev);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->gas_sync_fault) (void)hipHostFree(ctx->gas_sync_fault);
   for (AuxSlot& a : ctx->aux_slot) {
     if (a.p) (void)hipFree(a.p);
     if (a.gas_counts) (void)hipFree(a.gas_counts);

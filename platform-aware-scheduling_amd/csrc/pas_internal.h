@@ -168,6 +168,11 @@ struct pas_ctx {
   pas::AuxSlot aux_slot[pas::kAuxSlots];
   uint64_t aux_clock = 0;
   int gas_last_slot = -1;  // aux slot of the last GAS fit (pas_gas_limit_count)
+  // the GAS fit's fork / join of its side streams: -1 unresolved, 0 events, 1 device flags
+  // (gas_fit.hip gas_sync_mode), and the flags' sticky timeout report (host-pinned, written
+  // by a wait kernel that gave up)
+  int gas_sync_mode = -1;
+  uint32_t* gas_sync_fault = nullptr;
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;

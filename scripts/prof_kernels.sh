@@ -5,7 +5,7 @@ set -u
 R="$(cd "$(dirname "$0")/.." && pwd)"; W="${1:-tas}"; shift || true
 OUT="$R/gpurun_out/pk_$W"; rm -rf "$OUT"; mkdir -p "$OUT"
 export TMPDIR=/tmp; cd /tmp
-B=(python3 "$R/bench.py" --workload "$W" --no-cpu-baseline --no-request-latency --steps 5 --warmup 1)
+B=(python3 "$R/bench.py" --workload "$W" --no-cpu-baseline --no-request-latency --no-pipelined --settle 0 --steps 5 --warmup 1)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- "${B[@]}" > "$OUT/kt.log" 2>&1 || exit $?
 python3 - "$OUT/kt" <<'PY'
 import csv, glob, sys
@@ -17,7 +17,7 @@ PY
 i=0
 for C in "$@"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $C -d "$OUT/p$i" -o p --output-format csv -- "${B[@]}" > "$OUT/p$i.log" 2>&1 || exit $?
+  timeout -s KILL 150 rocprofv3 --pmc $C -d "$OUT/p$i" -o p --output-format csv -- "${B[@]}" > "$OUT/p$i.log" 2>&1 || exit $?
 done
 python3 - "$OUT" <<'PY'
 import csv, glob, sys, collections

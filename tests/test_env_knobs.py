@@ -16,9 +16,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "platform-aware-scheduling_amd", "lib", "libpas.so")
 
 # output-invariant: waves per eval workgroup, segments per wave, pod order across workgroups,
-# store cache policy, the global-scratch pass bitmap path, deschedule words per wave
+# store cache policy, the global-scratch pass bitmap path, deschedule words per wave, the GAS
+# fit's fork / join of its side streams (events or device flags)
 INVARIANT = {"PAS_EVAL_WAVES", "PAS_EVAL_SEGS", "PAS_EVAL_NOGROUP", "PAS_EVAL_AUX",
-             "PAS_EVAL_GLOBAL_PASS", "PAS_VIOL_RUN"}
+             "PAS_EVAL_GLOBAL_PASS", "PAS_VIOL_RUN", "PAS_GAS_SYNC"}
 # switches that once changed outputs (timing ablations) or picked another kernel at run time
 REMOVED = {"PAS_EVAL_ABLATE": "1", "PAS_PREP_ABLATE": "3", "PAS_VIOL_FLAT": "1",
            "PAS_VIOL_DEDUP": "1", "PAS_VIOL_PAIRS": "2", "PAS_VIOL_U": "4",
@@ -71,7 +72,8 @@ print("KNOBS-OK")
     dict(REMOVED),
     dict(REMOVED, PAS_EVAL_WAVES="8", PAS_EVAL_SEGS="2", PAS_EVAL_NOGROUP="1", PAS_VIOL_RUN="2"),
     dict(REMOVED, PAS_EVAL_WAVES="2", PAS_EVAL_AUX="0", PAS_VIOL_RUN="16",
-         PAS_EVAL_GLOBAL_PASS="1"),
+         PAS_EVAL_GLOBAL_PASS="1", PAS_GAS_SYNC="events"),
+    dict(REMOVED, AMD_SERIALIZE_KERNEL="3"),
 ])
 def test_env_knobs_change_no_result(knobs):
     env = dict(os.environ, **knobs)
