@@ -525,6 +525,8 @@ __device__ __forceinline__ int64_t free_at(const int64_t* __restrict__ free_t, i
   return (int64_t)(((uint64_t)v.y << 32) | v.x);
 }
 
+// A lane that stores nothing (past N, or a node past 8 cards with word results) reads node 0:
+// its values are never used (no store; bitmaps ballot `valid`; masks are ANDed with `live`).
 template <int Q>
 __device__ __forceinline__ void load_free_t(int32_t n, bool valid, int32_t N,
                                             const int64_t* __restrict__ free_t,
@@ -533,10 +535,7 @@ __device__ __forceinline__ void load_free_t(int32_t n, bool valid, int32_t N,
 #pragma unroll
   for (int k = 0; k < kMaxCards; ++k)
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      const int64_t f = free_at<Q>(free_t, N, k, q, off);
-      free[k][q] = valid ? f : -1;
-    }
+    for (int q = 0; q < Q; ++q) free[k][q] = free_at<Q>(free_t, N, k, q, off);
 }
 
 typedef unsigned long long lane_mask;  // one bit per lane of the wave (ballot)
@@ -1065,15 +1064,16 @@ __device__ __forceinline__ void rank_cards(const int64_t (&free)[kMaxCards][Q], 
       rank_level4(pos[4], pos[5], pos[6], pos[7], x[4], x[5], x[6], x[7], free[4][q], free[5][q],
                   free[6][q], free[7][q]);
     }
+    // bytes rank + 0x80 (ranks are at most 127: the 0x80 is one OR per word)
     uint32_t a = 0u, b = 0u;
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) {
-      const uint32_t r = min(pos[k], (uint32_t)n) + 0x80u;
+      const uint32_t r = min(pos[k], (uint32_t)n);
       if (k & 1) b |= r << (8 * (k >> 1));
       else a |= r << (8 * (k >> 1));
     }
-    fa[j] = a;
-    fb[j] = b;
+    fa[j] = a | 0x80808080u;
+    fb[j] = b | 0x80808080u;
     ++j;
   }
 }
@@ -1090,10 +1090,7 @@ __device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t,
     if (q == SKIP) continue;
     int64_t f[kMaxCards];
 #pragma unroll
-    for (int k = 0; k < kMaxCards; ++k) {
-      const int64_t x = free_at<Q>(free_t, N, k, q, off);
-      f[k] = valid ? x : -1;
-    }
+    for (int k = 0; k < kMaxCards; ++k) f[k] = free_at<Q>(free_t, N, k, q, off);  // (load_free_t)
     uint32_t pos[kMaxCards];
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) pos[k] = 0u;
@@ -1106,15 +1103,16 @@ __device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t,
       rank_level4(pos[0], pos[1], pos[2], pos[3], x[0], x[1], x[2], x[3], f[0], f[1], f[2], f[3]);
       rank_level4(pos[4], pos[5], pos[6], pos[7], x[4], x[5], x[6], x[7], f[4], f[5], f[6], f[7]);
     }
+    // bytes rank + 0x80 (ranks are at most 127: the 0x80 is one OR per word)
     uint32_t a = 0u, b = 0u;
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) {
-      const uint32_t r = min(pos[k], (uint32_t)n) + 0x80u;
+      const uint32_t r = min(pos[k], (uint32_t)n);
       if (k & 1) b |= r << (8 * (k >> 1));
       else a |= r << (8 * (k >> 1));
     }
-    fa[j] = a;
-    fb[j] = b;
+    fa[j] = a | 0x80808080u;
+    fb[j] = b | 0x80808080u;
     ++j;
   }
 }
@@ -1679,8 +1677,9 @@ __device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint3
   const uint32_t x0 = tab[min(p0 >> 2, 7u) * 64 + lane];
   const uint32_t u1 = lowbit(m1 & ~(1u << (p0 & 31u)));
   const uint32_t p1 = rpoint<C>(x0, r.pk[0]) ? min(u1, p0) : u1;
-  uint32_t word = (p0 >> 2) | ((p1 >> 2) << 3);
-  uint32_t worst = max(p0, p1);
+  // card fields as arithmetic shifts: a selection without a card (position -1) makes the
+  // word negative, whatever the other fields hold
+  int32_t word = ((int32_t)p0 >> 2) | (((int32_t)p1 >> 2) << 3);
   if constexpr (S == 3) {
     uint32_t g3[C];
 #pragma unroll
@@ -1695,10 +1694,13 @@ __device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint3
     }
     const uint32_t un = lowbit(m3 & ~(1u << (p0 & 31u)) & ~(1u << (p1 & 31u)));
     const uint32_t p2 = min(un, touched);
-    word |= (p2 >> 2) << 6;
-    worst = max(worst, p2);
+    word |= ((int32_t)p2 >> 2) << 6;
   }
-  return worst < 32u ? (node_ok | ((uint32_t)S << 24) | (word & 0xFFFFFFu)) : 0u;
+  // base = pass | S: a complete word xors to a negative value (kept by the min), a negative
+  // word to a positive one (0).  A node without cards (every free -1) has empty masks, so
+  // node_ok is not needed here; bitmap results take it at the caller.
+  (void)node_ok;
+  return (uint32_t)min(word ^ (int32_t)(0x80000000u | ((uint32_t)S << 24)), 0);
 }
 
 template <int Q, int SKIP, int S, bool kBits>
