@@ -1133,6 +1133,16 @@ __device__ __forceinline__ uint32_t rmask(const uint32_t (&fa)[C], const uint32_
 // lowest set bit, 0xFFFFFFFF for none (v_ffbl_b32)
 __device__ __forceinline__ uint32_t lowbit(uint32_t m) { return ffbl(m); }
 
+// p as a per-lane (VGPR) address: the pod loops read each pod's record from the wave's stage at
+// fixed offsets; with a uniform (SGPR) base the compiler copies the base into a VGPR before
+// every LDS read (a v_mov per read), with a VGPR base it adds the record offsets as immediates.
+template <typename T>
+__device__ __forceinline__ T* lane_ptr(T* p) {
+  uint32_t zero;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(zero));
+  return reinterpret_cast<T*>(reinterpret_cast<char*>(p) + zero);
+}
+
 // Lane-private copy of the node's free values of the compared kinds (all but SKIP) in LDS,
 // [card][lane][kind], so that a lane can read its chosen card's values back with one LDS read
 // (registers cannot be indexed per lane).
@@ -1454,6 +1464,8 @@ __device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, ch
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      const GasSel* st = lane_ptr(stage);  // (lane_ptr: record reads at immediate offsets)
+      const GasRSeq* rst = lane_ptr(rstage);
       for (int32_t j = 0; j < nb; ++j) {
         const int32_t pw = __builtin_amdgcn_readlane(wd, j);
         const int32_t pod = pw & 0xFFFFFF;
@@ -1461,9 +1473,9 @@ __device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, ch
         if (!kBits && S > kPacked) continue;  // the generic kernel's row (it runs beside this one)
         uint32_t out = 0u;
         if (!(pw & kBadPod) && S <= kPacked)  // more: the generic kernel's (bitmaps: 0 here)
-          out = multi_seq<Q, SKIP, kC, true>(nullptr, stage + j * kPacked, S, 0, node_ok, tab, lane,
+          out = multi_seq<Q, SKIP, kC, true>(nullptr, st + j * kPacked, S, 0, node_ok, tab, lane,
                                              (uint32_t)(same_m >> (32 * j)),
-                                             &rstage[j].rep[0][0], fa, fb);
+                                             &rst[j].rep[0][0], fa, fb);
         put_result<kBits>(res, fit, pod, N, n, valid, out);
       }
     }
@@ -1568,7 +1580,7 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
     // pods in pairs: both records read (broadcast LDS reads) before the first one's tests;
     // eight pods per iteration, so the records' LDS offsets are constants off one address
     for (int32_t j0 = 0; j0 < nb; j0 += 8) {
-      const GasRSingle* st = stage + j0;
+      const GasRSingle* st = lane_ptr(stage) + j0;
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
         if (j0 + u >= nb) break;
@@ -1748,7 +1760,7 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
       // four pods per iteration: their records' LDS offsets are constants off one address
       for (int32_t j0 = 0; j0 < nb; j0 += 4) {
-        const GasRMulti* st = stage + j0;
+        const GasRMulti* st = lane_ptr(stage) + j0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (j0 + u >= nb) break;

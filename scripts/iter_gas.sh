@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 240 --timeout-method threa
   tests/test_labels.py tests/test_prioritize_request.py > gpurun_out/iter_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|error" gpurun_out/iter_tests.log | tail -3
 [ $rc -ne 0 ] && { tail -40 gpurun_out/iter_tests.log; exit $rc; }
-timeout -k 10 500 bash scripts/diag/bench_ab.sh "--workload gas --steps 20 --warmup 3 --no-pipelined" 3 "$@" \
+timeout -k 10 500 bash scripts/diag/bench_ab.sh "--workload gas --steps 20 --warmup 3 --no-pipelined" ${AB_ROUNDS:-3} "$@" \
   > gpurun_out/iter_ab.log 2>&1
 rc=$?; cat gpurun_out/iter_ab.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 bash scripts/diag/gas_timeline.sh > gpurun_out/iter_timeline.log 2>&1
