@@ -100,20 +100,44 @@ __device__ __forceinline__ bool kind_fits(int64_t need, int64_t cap, int64_t use
 // 8 x 4; PAS_GAS_MAX_RES otherwise).
 template <int KMAX, int QW>
 __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
+  // every load of the node at once (card count, capacities, the usage of all its card slots):
+  // predicating the usage loads on the card count would wait for that load first
   const int32_t nc = a.n_cards[n];
-  if (nc <= 0) return false;  // FetchNode error / no cards label (:282-298)
   constexpr int kUnroll = KMAX <= 16 ? KMAX : 1;
-  const int32_t Q = a.Q;
-  const int32_t ncard = min(nc, min(a.K, KMAX));
+  const int32_t Q = a.Q, K = a.K;
   int64_t cap[kMaxRes];
   int64_t w[KMAX][QW];
 #pragma unroll
   for (int q = 0; q < kMaxRes; ++q) cap[q] = q < Q ? a.cap[(int64_t)n * Q + q] : 0;
+  if (Q == QW && ((KMAX * QW) & 1) == 0 && ((K * Q) & 1) == 0 && K <= KMAX) {
+    // the node's usage row as 16-byte loads (half the load instructions; the row starts on
+    // 16 bytes: an even number of values per node)
+    typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+    const v2i64* row = reinterpret_cast<const v2i64*>(a.used + (int64_t)n * K * Q);
+    int64_t f[KMAX * QW];
+#pragma unroll
+    for (int i = 0; i < KMAX * QW / 2; ++i) {
+      const v2i64 x = 2 * i < K * Q ? row[i] : v2i64{0, 0};
+      f[2 * i] = x.x;
+      f[2 * i + 1] = x.y;
+    }
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+      for (int q = 0; q < QW; ++q) w[k][q] = f[k * QW + q];
+  } else {
+#pragma unroll kUnroll
+    for (int k = 0; k < KMAX; ++k)
+#pragma unroll
+      for (int q = 0; q < QW; ++q)
+        w[k][q] = (k < K && q < Q) ? a.used[((int64_t)n * K + k) * Q + q] : 0;
+  }
+  if (nc <= 0) return false;  // FetchNode error / no cards label (:282-298)
+  const int32_t ncard = min(nc, min(K, KMAX));
 #pragma unroll kUnroll
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
-    for (int q = 0; q < QW; ++q)
-      w[k][q] = (k < ncard && q < Q) ? a.used[((int64_t)n * a.K + k) * Q + q] : 0;
+    for (int q = 0; q < QW; ++q) w[k][q] = k < ncard ? w[k][q] : 0;
   const int32_t nct = a.ncont[p];
   for (int32_t c = 0; c < nct; ++c) {
     const int64_t b = (int64_t)p * a.C + c;
@@ -235,8 +259,13 @@ __device__ __forceinline__ void compile_rule(const pas_rule& ru, int32_t M, int3
   out->span = (uint64_t)hi - (uint64_t)lo;
 }
 
+// (at least 4 waves per SIMD for the register-resident shapes: the gathers need waves in
+// flight)
 template <int KMAX, int QW>
-__global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
+constexpr int topk_waves() { return KMAX <= 8 && QW <= 3 ? 4 : 1; }
+template <int KMAX, int QW>
+__global__ __launch_bounds__(kTpb) __attribute__((amdgpu_waves_per_eu(topk_waves<KMAX, QW>())))
+void tas_gas_topk_kernel(LazyTopkParams a) {
   // the pods' compiled rules, kStageRules per pod (pods of at most that many rules)
   __shared__ LazyRule srule[kPodsPerBlock][kStageRules];
   __shared__ int32_t smetric[kPodsPerBlock][kStageRules];
@@ -284,10 +313,24 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
   for (int i = 0; i < kSkip; ++i) slo[i] = shi[i] = 0;
   const int ord = d0.y >= 0 ? d0.y / a.M : kOrderIndex;
   const bool sorted_row = c0 > 0 && ord != kOrderIndex;
-  for (int32_t r = r0; __ballot(sorted_row && r < r1); ++r) {
-    const pas_rule ru = a.rules[min(r, max(r1 - 1, 0))];
-    const bool same = sorted_row && r < r1 && ru.metric == pr.metric && ru.op >= 0 && ru.op <= 2;
-    if (!__ballot(same)) continue;
+  // The pod's rules are loaded one per lane (32 at a time, a single round trip) and only the
+  // ones on the prioritize metric are walked, one per half at a time (a rule by rule scan
+  // waited for a load per rule).
+  for (int32_t rc = r0; __ballot(sorted_row && rc < r1); rc += kPodLanes) {
+   const bool in_l = sorted_row && rc + sub < r1;
+   const pas_rule ru_l = a.rules[in_l ? rc + sub : 0];
+   const bool same_l = in_l && ru_l.metric == pr.metric && ru_l.op >= 0 && ru_l.op <= 2;
+   const uint64_t sm = __ballot(same_l);
+   uint32_t todo = (uint32_t)sm | (uint32_t)(sm >> 32);  // rule slots some half walks
+   while (todo) {
+    const int u = __builtin_ctz(todo);
+    todo &= todo - 1;
+    const int src = half * kPodLanes + u;  // this half's rule in slot u
+    pas_rule ru;
+    ru.metric = __shfl(ru_l.metric, src, 64);
+    ru.op = __shfl(ru_l.op, src, 64);
+    ru.target = __shfl(ru_l.target, src, 64);
+    const bool same = (sm >> src) & 1ull;
     int64_t tm = 0;
     const int sat = target_milli(ru.target, &tm);
     int32_t lb = 0, ub = 0;
@@ -309,6 +352,7 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
         ns = min(ns + 1, kSkip);
       }
     }
+   }
   }
   // Pods of at most kStageRules rules (every pod of the wave): each lane compiles one rule
   // of its pod into LDS, read back per round as broadcast LDS reads instead of a global load
@@ -357,11 +401,13 @@ __global__ __launch_bounds__(kTpb) void tas_gas_topk_kernel(LazyTopkParams a) {
         uint64_t pw[kRuleBatch];
 #pragma unroll
         for (int u = 0; u < kRuleBatch; ++u) m[u] = smetric[pslot][min(rb + u, kStageRules - 1)];
+        // (one presence word per node when the snapshot has at most 64 metrics)
+        const uint64_t pw0 = a.WM == 1 ? prow[0] : 0;
 #pragma unroll
         for (int u = 0; u < kRuleBatch; ++u) {
           const int32_t mm = m[u] >= 0 ? m[u] : 0;
           v[u] = vrow[mm];
-          pw[u] = prow[mm >> 6];
+          pw[u] = a.WM == 1 ? pw0 : prow[mm >> 6];
         }
 #pragma unroll
         for (int u = 0; u < kRuleBatch; ++u) {
