@@ -995,7 +995,11 @@ __global__ __launch_bounds__(kRankPrepTpb) void gas_rank_prep_kernel(RankArgs a)
 
 
 // The group's sorted rows of the C compared kinds into the wave's LDS slice [C][128]
-// (positions past the group's items: INT64_MAX).
+// (positions past the group's items: INT64_MAX), each in Eytzinger (breadth-first) order: the
+// i-th smallest (1-based r = i + 1 <= 127) at e(r) = 2^(6 - tz) + (r >> (tz + 1)), tz = ctz(r),
+// so that level L of the search reads entries [2^L, 2^(L+1)) — consecutive, one per bank —
+// instead of entries 2^(7-L) apart, which share banks (LDS bank conflicts of the sorted order:
+// SQ_LDS_BANK_CONFLICT, profiles/r05_gas_sq.csv).  Entry 0 is not read; the 128th is not kept.
 template <int C>
 __device__ __forceinline__ void load_sorted(const int64_t* __restrict__ srt, int64_t item0,
                                             int32_t n, int64_t* lds, int lane) {
@@ -1009,9 +1013,13 @@ __device__ __forceinline__ void load_sorted(const int64_t* __restrict__ srt, int
   }
   __builtin_amdgcn_wave_barrier();  // the previous group's reads of the slice are done
 #pragma unroll
-  for (int it = 0; it < 2; ++it)
+  for (int it = 0; it < 2; ++it) {
+    const uint32_t r = (uint32_t)(lane + 64 * it) + 1u;  // 1 .. 128
+    const uint32_t tz = (uint32_t)__builtin_ctz(r);
+    const uint32_t e = r < 128u ? (1u << (6u - tz)) + (r >> (tz + 1u)) : 0u;  // 128: entry 0
 #pragma unroll
-    for (int j = 0; j < C; ++j) lds[j * kRankItems + lane + 64 * it] = x[it][j];
+    for (int j = 0; j < C; ++j) lds[j * kRankItems + e] = x[it][j];
+  }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
@@ -1039,47 +1047,12 @@ __device__ __forceinline__ void rank_level4(uint32_t& p0, uint32_t& p1, uint32_t
 }
 
 // The node's cards ranked against the group: fa[j] = bytes rank + 0x80 of cards 0, 2, 4, 6
-// (kind j), fb[j] of cards 1, 3, 5, 7.  rank = #{group thresholds <= free}, the upper bound in
-// the sorted row found bit by bit: level L probes entry (pos << (7 - L)) + 2^(6 - L) - 1 and
-// appends the outcome (an address, a compare and an add-with-carry per level; entry 127 is
-// padding and never probed; at most n, the padding is INT64_MAX).  The 8 cards of a kind
-// go level by level together (8 LDS reads in flight).
-template <int Q, int SKIP, int C>
-__device__ __forceinline__ void rank_cards(const int64_t (&free)[kMaxCards][Q], const int64_t* lds,
-                                           int32_t n, uint32_t (&fa)[C], uint32_t (&fb)[C]) {
-#pragma unroll
-  for (int q = 0, j = 0; q < Q; ++q) {
-    if (q == SKIP) continue;
-    uint32_t pos[kMaxCards];
-#pragma unroll
-    for (int k = 0; k < kMaxCards; ++k) pos[k] = 0u;
-    const int64_t* row = lds + j * kRankItems;
-#pragma unroll
-    for (int sh = 6; sh >= 0; --sh) {
-      int64_t x[kMaxCards];
-#pragma unroll
-      for (int k = 0; k < kMaxCards; ++k) x[k] = row[(pos[k] << (sh + 1)) + (1 << sh) - 1];
-      rank_level4(pos[0], pos[1], pos[2], pos[3], x[0], x[1], x[2], x[3], free[0][q], free[1][q],
-                  free[2][q], free[3][q]);
-      rank_level4(pos[4], pos[5], pos[6], pos[7], x[4], x[5], x[6], x[7], free[4][q], free[5][q],
-                  free[6][q], free[7][q]);
-    }
-    // bytes rank + 0x80 (ranks are at most 127: the 0x80 is one OR per word)
-    uint32_t a = 0u, b = 0u;
-#pragma unroll
-    for (int k = 0; k < kMaxCards; ++k) {
-      const uint32_t r = min(pos[k], (uint32_t)n);
-      if (k & 1) b |= r << (8 * (k >> 1));
-      else a |= r << (8 * (k >> 1));
-    }
-    fa[j] = a | 0x80808080u;
-    fb[j] = b | 0x80808080u;
-    ++j;
-  }
-}
-
-// rank_cards with the free values read from the card-major copy one kind at a time (8 values
-// live instead of 8 Q).
+// (kind j), fb[j] of cards 1, 3, 5, 7.  rank = #{group thresholds <= free}, the upper bound
+// found down the Eytzinger tree of the sorted row (load_sorted): from e = 1, e = 2e + (row[e]
+// <= free) for 7 levels, then rank = e - 128 (an address, a compare and an add-with-carry per
+// level; at most n, the padding is INT64_MAX).  The 8 cards of a kind go level by level
+// together (8 LDS reads in flight).
+// (the free values read from the card-major copy one kind at a time: 8 values live, not 8 Q)
 template <int Q, int SKIP, int C>
 __device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t, int32_t n_node,
                                              bool valid, int32_t N, const int64_t* lds,
@@ -1093,13 +1066,13 @@ __device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t,
     for (int k = 0; k < kMaxCards; ++k) f[k] = free_at<Q>(free_t, N, k, q, off);  // (load_free_t)
     uint32_t pos[kMaxCards];
 #pragma unroll
-    for (int k = 0; k < kMaxCards; ++k) pos[k] = 0u;
+    for (int k = 0; k < kMaxCards; ++k) pos[k] = 1u;
     const int64_t* row = lds + j * kRankItems;
 #pragma unroll
     for (int sh = 6; sh >= 0; --sh) {
       int64_t x[kMaxCards];
 #pragma unroll
-      for (int k = 0; k < kMaxCards; ++k) x[k] = row[(pos[k] << (sh + 1)) + (1 << sh) - 1];
+      for (int k = 0; k < kMaxCards; ++k) x[k] = row[pos[k]];
       rank_level4(pos[0], pos[1], pos[2], pos[3], x[0], x[1], x[2], x[3], f[0], f[1], f[2], f[3]);
       rank_level4(pos[4], pos[5], pos[6], pos[7], x[4], x[5], x[6], x[7], f[4], f[5], f[6], f[7]);
     }
@@ -1107,7 +1080,7 @@ __device__ __forceinline__ void rank_cards_t(const int64_t* __restrict__ free_t,
     uint32_t a = 0u, b = 0u;
 #pragma unroll
     for (int k = 0; k < kMaxCards; ++k) {
-      const uint32_t r = min(pos[k], (uint32_t)n);
+      const uint32_t r = min(pos[k] - 128u, (uint32_t)n);
       if (k & 1) b |= r << (8 * (k >> 1));
       else a |= r << (8 * (k >> 1));
     }
