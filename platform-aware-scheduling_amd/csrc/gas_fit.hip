@@ -203,22 +203,27 @@ __device__ __forceinline__ int32_t skip_list(int32_t n_res, const int64_t (&cmp)
 
 // A slot in list `list` for each active lane: one atomic per distinct list in the wave (lanes
 // of different lists hit different counters, which the compiler would leave one per lane).
+// The lists are counted first (ballots only); then each list's leader lane issues its atomic,
+// all of them in one instruction: one round trip to L2 instead of one per distinct list.
 __device__ __forceinline__ int32_t wave_slot(int32_t* __restrict__ counts, int32_t list) {
   unsigned long long todo = __ballot(1);
-  int32_t slot = 0;
+  const int lane = (int)__lane_id();
+  int32_t local = 0, my_leader = 0, lead_cnt = 0;
   while (todo) {
     const int leader = __builtin_ctzll(todo);
     const int32_t l = __shfl(list, leader, 64);
     const unsigned long long m = __ballot(list == l);
-    int32_t base = 0;
-    if ((int)__lane_id() == leader) base = atomicAdd(&counts[l], __popcll(m));
-    base = __shfl(base, leader, 64);
-    if (list == l)
-      slot = base + (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    if (list == l) {
+      local = (int32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      my_leader = leader;
+    }
+    if (lane == leader) lead_cnt = __popcll(m);
     todo &= ~m;
   }
-  return slot;
+  int32_t base = 0;
+  if (lead_cnt > 0) base = atomicAdd(&counts[list], lead_cnt);  // leaders: own list
+  return __shfl(base, my_leader, 64) + local;
 }
 
 // The list a multi-selection pod is filed under: 1 + q for the lowest kind q that some
@@ -289,9 +294,12 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
   // container and pass); containers past them are loaded when reached
   constexpr int kPre = 4;
   ContainerReq pre[kPre] = {};
-  if (nc > 0) {
+  // (indexed by max_containers, not nc, so that they do not wait for n_containers[p]; entries
+  // past nc are never used)
+  if (max_containers > 0) {
 #pragma unroll
-    for (int c = 0; c < kPre; ++c) pre[c] = load_container(row + min(c, nc - 1), n_res, req, mask);
+    for (int c = 0; c < kPre; ++c)
+      pre[c] = load_container(row + min(c, max_containers - 1), n_res, req, mask);
   }
   // their steps, once; both passes below run unrolled over them (a runtime container index
   // into these arrays would put them in scratch memory), then over containers past them
