@@ -475,7 +475,9 @@ def bench_gas(args, world, rank):
         b.record(stream)
         b.synchronize()
         dense_ms = a.elapsed_time(b) / args.steps
-        assert torch.equal(dres_t, res_t[:, :N]), "dense and pitched results differ"
+        # (PAS_BENCH_ABLATED: timing runs of diagnostic builds whose outputs are wrong on purpose)
+        assert os.environ.get("PAS_BENCH_ABLATED") or torch.equal(dres_t, res_t[:, :N]), \
+            "dense and pitched results differ"
         del dres_t
     alg_bytes = N * (8 * Q + 8 * K * Q + 4) + P * (8 * C * Q + 4 * C + 4) + 4 * P * N
     kernel_s = gpu["ms_per_step"] / 1e3
