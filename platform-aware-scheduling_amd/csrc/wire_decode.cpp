@@ -793,6 +793,7 @@ bool decode_node_list(Scanner& s, NodeList* out, const char* base, ItemIndex* id
 // what the sequential path reports.
 constexpr int64_t kParBytesPerThread = 1 << 20;
 constexpr int kParMaxThreads = 16;  // the GPU box's CPU share per GPU
+constexpr int kPieces = pas::kHostPieces;
 std::atomic<int32_t> g_decode_threads{0};  // pas_decode_set_threads; 0 = automatic
 
 int decode_threads_for(int64_t len) {
@@ -816,13 +817,14 @@ class WorkerPool {
     if (!pool || pool->pid_ != getpid()) pool = new WorkerPool();  // (never freed: process-wide)
     return pool;
   }
-  // Runs f(i) for i in [0, n) on the caller and up to n - 1 workers; false if the pool is busy
-  // or cannot grow (nothing run).
-  bool run(int n, const std::function<void(int)>& f) {
+  // Runs f(i) for i in [0, n) on the caller and up to threads - 1 workers (each taking the next
+  // i until none is left); false if the pool is busy or cannot grow (nothing run).
+  bool run(int n, int threads, const std::function<void(int)>& f) {
     std::unique_lock<std::mutex> busy(busy_, std::try_to_lock);
     if (!busy.owns_lock()) return false;
+    threads = std::min(n, threads);
     try {
-      while ((int)workers_.size() < n - 1) workers_.emplace_back([this] { loop(); });
+      while ((int)workers_.size() < threads - 1) workers_.emplace_back([this] { loop(); });
     } catch (...) {
       return false;
     }
@@ -832,6 +834,7 @@ class WorkerPool {
       task_ = &f;
       n_ = n;
       pending_ = n;
+      seats_ = threads - 1;  // workers that may join this run
       ep = (uint32_t)++epoch_;
       next_.store((uint64_t)ep << 32);
     }
@@ -871,6 +874,8 @@ class WorkerPool {
         std::unique_lock<std::mutex> g(m_);
         cv_.wait(g, [&] { return epoch_ != seen && task_ != nullptr; });
         seen = epoch_;
+        if (seats_ <= 0) continue;  // the run has its threads: wait for the next one
+        --seats_;
         task = task_;
         n = n_;
       }
@@ -882,15 +887,17 @@ class WorkerPool {
   std::condition_variable cv_, done_;
   std::vector<std::thread> workers_;
   const std::function<void(int)>* task_ = nullptr;
-  int n_ = 0, pending_ = 0;
+  int n_ = 0, pending_ = 0, seats_ = 0;
   std::atomic<uint64_t> next_{0};  // {epoch (32 bits), next item (32 bits)}
   uint64_t epoch_ = 0;
 };
 
-// f(i) for i in [0, n), on the pool (or fresh threads when it is busy).  Returns false
-// (nothing run) when no thread can be started.
+// f(i) for i in [0, n) on up to `threads` threads (default n), each taking the next i until
+// none is left: the pool, or fresh threads when it is busy.  More pieces than threads balance
+// threads the host delays.  Returns false (nothing run) when no thread can be started.
 template <class F>
-bool parallel_for(int n, F&& f) {
+bool parallel_for(int n, F&& f, int threads = 0) {
+  if (threads <= 0 || threads > n) threads = n;
 #ifdef PAS_DECODE_TRACE
   std::vector<double> busy((size_t)n, 0.0);
   PAS_TRACE_T0(t_spawn);
@@ -904,17 +911,22 @@ bool parallel_for(int n, F&& f) {
   auto& g = f;
 #endif
   const std::function<void(int)> fn = [&g](int i) { g(i); };
-  bool ran = n <= 1 ? (g(0), true) : WorkerPool::get()->run(n, fn);
+  bool ran = n <= 1 ? (n == 1 ? g(0) : void(), true) : WorkerPool::get()->run(n, threads, fn);
   if (!ran) {
+    std::atomic<int> next{0};
+    auto take = [&] {
+      for (int i; (i = next.fetch_add(1)) < n;) g(i);
+    };
     std::vector<std::thread> th;
     try {
-      th.reserve((size_t)std::max(n - 1, 0));
-      for (int i = 1; i < n; ++i) th.emplace_back([&g, i] { g(i); });
+      th.reserve((size_t)std::max(threads - 1, 0));
+      for (int i = 1; i < threads; ++i) th.emplace_back(take);
     } catch (...) {
+      next.store(n);  // the started threads take nothing more
       for (auto& x : th) x.join();
       return false;
     }
-    g(0);
+    take();
     for (auto& x : th) x.join();
   }
 #ifdef PAS_DECODE_TRACE
@@ -930,7 +942,9 @@ bool parallel_for(int n, F&& f) {
 
 int pas::host_threads_for(int64_t bytes) { return decode_threads_for(bytes); }
 
-bool pas::host_parallel(int n, const std::function<void(int)>& f) { return parallel_for(n, f); }
+bool pas::host_parallel(int n, const std::function<void(int)>& f, int threads) {
+  return parallel_for(n, f, threads);
+}
 
 namespace {
 
@@ -1020,7 +1034,8 @@ struct ItemIndex {
   }
 
   void build() {
-    const int T = threads;
+    // kPieces chunks per thread, taken in turn by the threads (balances a delayed thread)
+    const int T = threads * kPieces;
     const int64_t cs = ((len + T - 1) / T + 63) & ~int64_t(63);
     std::vector<int64_t> par(T, 0), d_out(T, 0), d_in(T, 0);
     // pass 1: quote parity and depth change per chunk, for both start states
@@ -1039,7 +1054,7 @@ struct ItemIndex {
           par[t] = (int64_t)pq;
           d_out[t] = dout;
           d_in[t] = din;
-        }))
+        }, threads))
       return;
     std::vector<char> in0(T, 0);
     std::vector<int64_t> depth0(T, 0);
@@ -1074,7 +1089,7 @@ struct ItemIndex {
             }
             depth += no - nc;
           });
-        }))
+        }, threads))
       return;
     size_t total = 0;
     for (const auto& v : ev) total += v.size();
@@ -1111,7 +1126,7 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
 #ifdef PAS_DECODE_ITEMS_T1  // diagnostic: the items on one thread
   const int T = 1;
 #else
-  const int T = std::max(1, std::min<int>(idx->threads, (int)(n_items / 256)));
+  const int T = std::max(1, std::min<int>(idx->threads * kPieces, (int)(n_items / 256)));
 #endif
   PAS_TRACE_T0(t_items);
   if (!empty &&
@@ -1133,7 +1148,7 @@ bool fast_items(ItemIndex* idx, Scanner& s, NodeList* out) {
           spans[2 * i + 1] = (int64_t)(e - b);
           if (idx->table) ids[i] = idx->table->find(names[i]);
         }
-      }))
+      }, idx->threads))
     return false;
   PAS_TRACE_MS("items", t_items);
   if (!ok.load()) return false;

@@ -72,9 +72,11 @@ void encode_items(pas::JsonOut& o, int64_t n, char sep, int64_t bytes_per_item, 
     range(o, 0, n);
     return;
   }
-  std::vector<std::string> part((size_t)T);
+  // kHostPieces ranges per thread, taken in turn
+  const int R = (int)std::min<int64_t>((int64_t)T * pas::kHostPieces, n / 256);
+  std::vector<std::string> part((size_t)R);
   auto run = [&](int t) {
-    const int64_t i0 = n * t / T, i1 = n * (t + 1) / T;
+    const int64_t i0 = n * t / R, i1 = n * (t + 1) / R;
     // one pass into a buffer of twice the estimate; a range that outgrows it (long names,
     // escapes) is encoded again at its counted length
     std::string& b = part[(size_t)t];
@@ -88,7 +90,7 @@ void encode_items(pas::JsonOut& o, int64_t n, char sep, int64_t bytes_per_item, 
     }
     b.resize((size_t)w.pos);
   };
-  if (!pas::host_parallel(T, run)) {
+  if (!pas::host_parallel(R, run, T)) {
     range(o, 0, n);
     return;
   }
@@ -165,9 +167,12 @@ int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const u
     }
     const int64_t begin = o.pos, end = pos;
     const int T = (int)std::min<int64_t>(pas::host_threads_for(end - begin), (int64_t)item.size());
+    // kHostPieces byte ranges per thread, taken in turn
+    const int R = (int)std::min<int64_t>((int64_t)std::max(T, 1) * pas::kHostPieces,
+                                         std::max<int64_t>((int64_t)item.size(), 1));
     auto copy = [&](int t) {
-      const int64_t lo = begin + (end - begin) * t / T;
-      const int64_t hi = t == T - 1 ? INT64_MAX : begin + (end - begin) * (t + 1) / T;
+      const int64_t lo = begin + (end - begin) * t / R;
+      const int64_t hi = t == R - 1 ? INT64_MAX : begin + (end - begin) * (t + 1) / R;
       size_t j = std::lower_bound(at.begin(), at.end(), lo) - at.begin();
       for (; j < item.size() && at[j] < hi; ++j) {
         const int64_t a = at[j], len = node_json_len[item[j]];
@@ -175,8 +180,8 @@ int pas_encode_tas_filter_result(int32_t n_req, const int32_t* req_node, const u
         if (a < cap) std::memcpy(buf + a, node_json[item[j]], (size_t)std::min(len, cap - a));
       }
     };
-    if (T <= 1 || !pas::host_parallel(T, copy))
-      for (int t = 0; t < std::max(T, 1); ++t) copy(t);
+    if (T <= 1 || !pas::host_parallel(R, copy, T))
+      for (int t = 0; t < R; ++t) copy(t);
     o.pos = end;
     o.put(']');
   }
