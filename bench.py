@@ -583,9 +583,16 @@ def bench_deschedule(args, world, rank):
     total_t = torch.empty(1, dtype=torch.int64, device="cuda")
     gathered = {}
 
+    fused = not getattr(args, "deschedule_separate", False)
+
     def step():
-        ctx.tas_violations_device(1, S, len(rules), rules_t, off_t, viol_t, stream)
-        ctx.tas_label_plan_device(n_local, S, viol_t, labels_t, add_t, rem_t, total_t, stream)
+        if fused:  # the sweep with its label plan in one pass
+            ctx.tas_deschedule_device(1, S, len(rules), rules_t, off_t, viol_t, labels_t, add_t,
+                                      rem_t, total_t, stream)
+        else:
+            ctx.tas_violations_device(1, S, len(rules), rules_t, off_t, viol_t, stream)
+            ctx.tas_label_plan_device(n_local, S, viol_t, labels_t, add_t, rem_t, total_t,
+                                      stream)
         gathered["v"] = shard.gather_violations(viol_t, world, N)
 
     settle_steps = distrib.settle(step, args.settle, world=world)
@@ -599,6 +606,8 @@ def bench_deschedule(args, world, rank):
     l_ms, l_n = ctx.kernel_time(_lib.PAS_K_TAS_LABELS)
     w = pas_amd.w64(n_local)
     alg_bytes = 8 * M * n_local + 8 * M * w + 8 * S * w
+    if fused:  # the plan's label words read and add / remove masks written by the same kernel
+        alg_bytes += 8 * S * w + 16 * n_local
     kernel_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = alg_bytes / kernel_s / 1e9
     out = {
@@ -611,10 +620,12 @@ def bench_deschedule(args, world, rank):
         "data": "synthetic (SURVEY.md §8(d) C4)",
         "config": {"settle_steps": settle_steps, "workload": "tas_deschedule_sweep (BASELINE configs[3])", "nodes": N,
                    "nodes_per_gpu": n_local, "metrics": M, "strategies": S, "rules": len(rules),
-                   "step": "sweep + label plan (add/remove masks per node) + all-gather",
+                   "step": ("sweep with its label plan fused (add/remove masks per node)"
+                            if fused else "sweep, then label plan (add/remove masks per node)")
+                           + " + all-gather",
                    "snapshot_build_ms": snapshot_ms, "snapshot_refresh_ms": refresh,
                    "parallelism": f"node-sharded x{world}, violation bitmaps all-gathered"},
-        "label_plan_ms": l_ms / max(l_n, 1),
+        "label_plan_ms": None if fused else l_ms / max(l_n, 1),
         "roofline": {"bound": "hbm", "kernel": "tas_violations_run_kernel", "achieved": achieved,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": load_traffic("tas_violations_kernel"),
@@ -824,6 +835,9 @@ def main():
                          "the launch stream only)")
     ap.add_argument("--no-pipelined", action="store_true",
                     help="skip the pipelined sub-record (kernel profiles of the D = 1 line)")
+    ap.add_argument("--deschedule-separate", action="store_true",
+                    help="deschedule: the sweep and the label plan as two calls (default: "
+                         "pas_tas_deschedule_device, one pass)")
     ap.add_argument("--no-request-latency", action="store_true",
                     help="skip the f2 request-latency leg of the TAS workload")
     args = ap.parse_args()

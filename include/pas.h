@@ -236,6 +236,17 @@ int pas_tas_label_plan_device(pas_ctx* ctx, int32_t n_nodes, int32_t n_strategie
                               uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
                               void* hip_stream);
 
+/* The deschedule sweep and its label plan in one pass (Deschedule.Cleanup's violation lists,
+ * deschedule/strategy.go:31-50, then updateNodeLabels, enforce.go:99-151): outputs as
+ * pas_tas_violations_device (viol_out) followed by pas_tas_label_plan_device on those
+ * bitmaps for the snapshot's n_nodes (labels / add_out / remove_out / total_out), without
+ * re-reading the bitmaps.  n_strategies <= 64. */
+int pas_tas_deschedule_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
+                              int32_t n_rules, const pas_rule* d_rules,
+                              const int32_t* d_rule_off, uint64_t* d_viol_out,
+                              const uint64_t* d_labels, uint64_t* d_add_out,
+                              uint64_t* d_remove_out, int64_t* d_total_out, void* hip_stream);
+
 /* json.Marshal of the node's []patchValue (enforce.go:21-25, 74-86) for the masks of
  * pas_tas_label_plan: adds in strategy order, then a remove + add "null" pair per removed
  * label in strategy order (the reference emits these in Go-map order).  names[s] = policy

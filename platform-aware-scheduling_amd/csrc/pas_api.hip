@@ -1204,6 +1204,25 @@ int pas_tas_label_plan_device(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat,
                            d_total_out, pick_stream(ctx, hip_stream));
 }
 
+int pas_tas_deschedule_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
+                              int32_t n_rules, const pas_rule* d_rules,
+                              const int32_t* d_rule_off, uint64_t* d_viol_out,
+                              const uint64_t* d_labels, uint64_t* d_add_out,
+                              uint64_t* d_remove_out, int64_t* d_total_out, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  if (n_rules < 0) return set_error(ctx, PAS_EINVAL, "negative count");
+  if ((rc = check_label_plan(ctx, ctx->tas.n_nodes, n_strategies, d_viol_out, d_add_out,
+                             d_remove_out, d_total_out, "pas_tas_deschedule_device")))
+    return rc;
+  if (n_strategies > 0 && (!d_rule_off || (n_rules > 0 && !d_rules)))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_deschedule_device: null input");
+  if ((rc = activate(ctx))) return rc;
+  return tas_deschedule_launch(ctx, n_strategies, d_rules, d_rule_off, d_viol_out, d_labels,
+                               d_add_out, d_remove_out, d_total_out, pick_stream(ctx, hip_stream));
+}
+
 // --------------------------------------------------------------------------- node shards
 
 int pas_tas_topk_device(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t n_rules,

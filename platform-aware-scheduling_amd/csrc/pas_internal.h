@@ -286,5 +286,13 @@ int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_con
 int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
                       const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                       int64_t* d_total, hipStream_t s);
+// totalViolations from per-block counts of violated pairs: *d_total = pairs - sum(d_part).
+int label_total_launch(pas_ctx* ctx, int32_t n_parts, int64_t pairs, const int64_t* d_part,
+                       int64_t* d_total, hipStream_t s);
+// The deschedule sweep with the label plan fused in (pas_tas_deschedule_device): viol as
+// tas_violations_launch, add / rem / total as label_plan_launch on those bitmaps.
+int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
+                          const int32_t* d_rule_off, uint64_t* d_viol, const uint64_t* d_labels,
+                          uint64_t* d_add, uint64_t* d_rem, int64_t* d_total, hipStream_t s);
 
 }  // namespace pas

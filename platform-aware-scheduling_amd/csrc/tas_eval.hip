@@ -639,22 +639,59 @@ constexpr int kWaves = kTpb / 64;
 #ifndef PAS_VIOL_NT
 #define PAS_VIOL_NT 1  // non-temporal column loads: each column byte is read once per sweep
 #endif
-template <int kRun>
+// The label plan fused into the sweep (pas_tas_deschedule_device, deschedule/enforce.go:99-151,
+// as label_plan_kernel in tas_labels.hip): the wave's carried-label words [S][kRun] are read
+// into its LDS slice before the walk, a strategy's completed words go next to them, and after
+// the walk lane l turns both into the masks of nodes (gw0 + k) * 64 + l, one word k at a time
+// (bit s = bit l of word (s, k), from broadcast LDS reads; the block stores its count of
+// violated pairs).
+static_assert(kWaves == 4, "the plan's per-block count sums four waves");
+struct PlanOut {
+  const uint64_t* labels;  // [S][W64] or null
+  uint64_t* add;           // [N]
+  uint64_t* rem;           // [N]
+  int64_t* part;           // [gridDim.x] violated pairs per block
+};
+
+template <int kRun, bool kPlan = false>
 __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
     const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
-    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out) {
+    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out, PlanOut plan) {
   static_assert(kRun <= 64, "one word per lane");
+  __shared__ int64_t red[kPlan ? kWaves : 1];
+  __shared__ uint64_t vws[kPlan ? kWaves : 1][kPlan ? 64 : 1][kPlan ? kRun : 1];
+  __shared__ uint64_t lws[kPlan ? kWaves : 1][kPlan ? 64 : 1][kPlan ? kRun : 1];
   const int32_t gw0 = (blockIdx.x * kWaves + (threadIdx.x >> 6)) * kRun;
-  if (gw0 >= W64) return;
   const int lane = threadIdx.x & 63;
+  if (gw0 >= W64) {
+    if constexpr (kPlan) {  // (a block's waves past the end still take part in its count)
+      if (lane == 0) red[threadIdx.x >> 6] = 0;
+      __syncthreads();
+      if (threadIdx.x == 0) plan.part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+    }
+    return;
+  }
   const int32_t pw_lane = min(gw0 + lane, W64 - 1);
   const int32_t r_begin = rule_off[0], r_end = rule_off[n_strat];
   int32_t s = 0;
   int32_t s_end = n_strat > 0 ? rule_off[1] : 0;
   uint64_t acc = 0;  // lane k: word gw0 + k
+  int64_t violated = 0;
+  if constexpr (kPlan) {  // lane t: strategy t's carried-label words of this wave's run
+    if (lane < n_strat) {
+      const uint64_t* lrow = plan.labels + (int64_t)lane * W64;
+#pragma unroll
+      for (int k = 0; k < kRun; ++k)
+        lws[threadIdx.x >> 6][lane][k] = plan.labels ? lrow[min(gw0 + k, W64 - 1)] : 0ull;
+    }
+  }
   auto flush = [&]() {
     if (lane < kRun && gw0 + lane < W64) viol_out[(int64_t)s * W64 + gw0 + lane] = acc;
+    if constexpr (kPlan) {
+      violated += __popcll(acc);  // (lanes past kRun hold 0)
+      if (lane < kRun) vws[threadIdx.x >> 6][s][lane] = acc;
+    }
     acc = 0;
   };
   // rule records arrive two rules ahead (scalar loads), so the column loads of the next rule
@@ -708,6 +745,36 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     for (int k = 0; k < kRun; ++k) v[k] = nv[k];
   }
   for (; s < n_strat; ++s) flush();  // the last strategy with rules, then those without
+  if constexpr (kPlan) {
+    const uint64_t(*ws)[kRun] = vws[threadIdx.x >> 6];
+    const uint64_t(*ls)[kRun] = lws[threadIdx.x >> 6];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    // bit l of a word: bit (l & 31) of its half l >> 5
+    const bool hi = lane >= 32;
+    const uint32_t sh = (uint32_t)lane & 31u;
+    auto bit = [&](uint64_t w) { return ((hi ? (uint32_t)(w >> 32) : (uint32_t)w) >> sh) & 1u; };
+    for (int k = 0; k < kRun; ++k) {
+      uint32_t a[2] = {0u, 0u}, r[2] = {0u, 0u};
+      for (int32_t t = 0; t < n_strat; ++t) {
+        const int h = t >> 5;
+        const uint32_t b = (uint32_t)t & 31u;
+        a[h] |= bit(ws[t][k]) << b;
+        r[h] |= bit(ls[t][k]) << b;
+      }
+      const int64_t n = (int64_t)(gw0 + k) * 64 + lane;
+      if (n < N) {
+        const uint64_t av = (uint64_t)a[1] << 32 | a[0], rv = (uint64_t)r[1] << 32 | r[0];
+        plan.add[n] = av;
+        plan.rem[n] = rv & ~av;
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) violated += __shfl_xor(violated, off, 64);
+    if (lane == 0) red[threadIdx.x >> 6] = violated;
+    __syncthreads();
+    if (threadIdx.x == 0) plan.part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  }
 }
 
 size_t align256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -901,10 +968,43 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   const int32_t per = (run == 2 || run == 4 || run == 16) ? run : 8;
   const int32_t rwaves = (W64 + per - 1) / per;
   rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
-      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol);
+      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol,
+      PlanOut{});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
+}
+
+int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
+                          const int32_t* d_rule_off, uint64_t* d_viol, const uint64_t* d_labels,
+                          uint64_t* d_add, uint64_t* d_rem, int64_t* d_total, hipStream_t s) {
+  const TasSnapshot& t = ctx->tas;
+  const int32_t N = t.n_nodes, W64 = (int32_t)w64(N);
+  if (W64 == 0 || n_strat == 0) {  // no pairs: every mask 0, total 0
+    if (N > 0) {
+      PAS_HIP(ctx, hipMemsetAsync(d_add, 0, sizeof(uint64_t) * (size_t)N, s));
+      PAS_HIP(ctx, hipMemsetAsync(d_rem, 0, sizeof(uint64_t) * (size_t)N, s));
+    }
+    return label_total_launch(ctx, 0, 0, nullptr, d_total, s);
+  }
+  constexpr int kRun = 8;
+  const int32_t rwaves = (W64 + kRun - 1) / kRun;
+  const int32_t blocks = (rwaves + kWaves - 1) / kWaves;
+  // the per-block counts are the stream's slot buffer: sweeps on other streams may run beside
+  int rc = PAS_OK;
+  SlotScope sc(ctx, s, 0, &rc);
+  if (!sc.slot) return rc;
+  int64_t* part = static_cast<int64_t*>(
+      slot_buf(ctx, sc.slot, kBufLabel, sizeof(int64_t) * (size_t)blocks, s, &rc));
+  if (!part) return rc;
+  TimedLaunch tl;
+  timing_begin(ctx, s, PAS_K_TAS_VIOLATIONS, &tl);
+  tas_violations_run_kernel<kRun, true><<<blocks, kTpb, 0, s>>>(
+      N, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol,
+      PlanOut{d_labels, d_add, d_rem, part});
+  timing_end(ctx, s, &tl);
+  PAS_HIP(ctx, hipGetLastError());
+  return label_total_launch(ctx, blocks, (int64_t)N * n_strat, part, d_total, s);
 }
 
 }  // namespace pas

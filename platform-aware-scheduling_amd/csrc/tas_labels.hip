@@ -111,6 +111,13 @@ void put_patch(JsonOut& o, const char* op, const char* name, const char* value) 
 
 }  // namespace
 
+int label_total_launch(pas_ctx* ctx, int32_t n_parts, int64_t pairs, const int64_t* d_part,
+                       int64_t* d_total, hipStream_t s) {
+  label_total_kernel<<<1, kTpb, 0, s>>>(n_parts, pairs, d_part, d_total);
+  PAS_HIP(ctx, hipGetLastError());
+  return PAS_OK;
+}
+
 int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
                       const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                       int64_t* d_total, hipStream_t s) {

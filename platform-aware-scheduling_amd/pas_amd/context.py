@@ -294,6 +294,16 @@ class Context:
                                                _dptr(total_t), _stream(stream))
         self._check(rc, "pas_tas_label_plan_device")
 
+    def tas_deschedule_device(self, gen: int, n_strat: int, n_rules: int, rules_t, rule_off_t,
+                              viol_t, labels_t, add_t, rem_t, total_t, stream=None):
+        """The sweep and its label plan in one pass (pas_tas_deschedule_device): viol_t as
+        tas_violations_device, add_t / rem_t / total_t as tas_label_plan_device on it."""
+        rc = self._l.pas_tas_deschedule_device(self._h, gen, n_strat, n_rules, _dptr(rules_t),
+                                               _dptr(rule_off_t), _dptr(viol_t),
+                                               _dptr(labels_t), _dptr(add_t), _dptr(rem_t),
+                                               _dptr(total_t), _stream(stream))
+        self._check(rc, "pas_tas_deschedule_device")
+
     # ------------------------------------------------------------------ GAS
     def gas_snapshot_set(self, gen: int, n_cards: np.ndarray, cap_per_gpu: np.ndarray,
                          used: np.ndarray):

@@ -152,6 +152,95 @@ def test_label_plan_device_after_sweep(ctx, oracle):
     a = add_t.cpu().numpy().view(np.uint64)
     assert not np.any(a & rem_t.cpu().numpy().view(np.uint64))
     assert want[2] == n * s - int(unpack_bits(viol, n).sum())
+    # the fused sweep + plan at the same shape: the same bitmaps, masks and count
+    f_viol_t = torch.empty_like(viol_t)
+    f_add_t, f_rem_t, f_total_t = (torch.empty_like(add_t), torch.empty_like(rem_t),
+                                   torch.empty_like(total_t))
+    ctx.tas_deschedule_device(gen, s, len(rules), rules_t, off_t, f_viol_t, labels_t, f_add_t,
+                              f_rem_t, f_total_t)
+    torch.cuda.synchronize()
+    assert torch.equal(f_viol_t, viol_t) and torch.equal(f_add_t, add_t)
+    assert torch.equal(f_rem_t, rem_t) and torch.equal(f_total_t, total_t)
+
+
+def _fused_and_separate(ctx, gen, n, s, rules, off, labels):
+    """pas_tas_deschedule_device and the sweep + plan pair on the same resident inputs."""
+    import torch
+    dev = torch.device("cuda", 0)
+    w = (n + 63) // 64
+    rules_t = torch.from_numpy(rules.view(np.uint8).copy()).to(dev)
+    off_t = torch.from_numpy(off).to(dev)
+    labels_t = None if labels is None else torch.from_numpy(labels.view(np.int64).copy()).to(dev)
+    out = {}
+    for name in ("fused", "separate"):
+        viol_t = torch.full((max(s, 1), max(w, 1)), -1, dtype=torch.int64, device=dev)
+        add_t = torch.full((max(n, 1),), -1, dtype=torch.int64, device=dev)
+        rem_t = torch.full((max(n, 1),), -1, dtype=torch.int64, device=dev)
+        total_t = torch.full((1,), -7, dtype=torch.int64, device=dev)
+        if name == "fused":
+            ctx.tas_deschedule_device(gen, s, len(rules), rules_t, off_t, viol_t, labels_t, add_t,
+                                      rem_t, total_t)
+        else:
+            ctx.tas_violations_device(gen, s, len(rules), rules_t, off_t, viol_t)
+            ctx.tas_label_plan_device(n, s, viol_t, labels_t, add_t, rem_t, total_t)
+        torch.cuda.synchronize()
+        out[name] = (viol_t.cpu().numpy().view(np.uint64)[:s, :w],
+                     add_t.cpu().numpy().view(np.uint64)[:n],
+                     rem_t.cpu().numpy().view(np.uint64)[:n], int(total_t.item()))
+    return out["fused"], out["separate"]
+
+
+@pytest.mark.gpu
+def test_deschedule_fused_parity(ctx, oracle):
+    # the sweep with its label plan in one pass equals the two calls and the oracle, for node
+    # counts off the 64-node words and the waves' 8-word runs, 1..64 strategies, with and
+    # without carried labels, and strategies without rules
+    rng = np.random.default_rng(14)
+    gen = 7200
+    for n in (1, 63, 64, 65, 511, 513, 4097, 70_001):
+        snap = wl.make_tas_snapshot(n, 8, seed=n)
+        ctx.tas_snapshot_set(gen, snap.v_milli, snap.present)
+        for s in (1, 5, 16, 64):
+            rules, off = wl.make_deschedule_rules(snap, s, 2, seed=n + s)
+            if s >= 5:  # strategies 1 and 3 without rules
+                cnt = np.diff(off).copy()
+                cnt[1] = cnt[3] = 0
+                keep = np.concatenate([np.arange(off[i], off[i] + cnt[i]) for i in range(s)])
+                rules = rules[keep]
+                off = np.concatenate([[0], np.cumsum(cnt)]).astype(np.int32)
+            want_v = oracle.tas_violations(snap.v_milli, snap.present, rules, off)
+            labels = wl.pack_bits(rng.random((s, n)) < 0.4)
+            for lab in (labels, None):
+                f, sep = _fused_and_separate(ctx, gen, n, s, rules, off, lab)
+                np.testing.assert_array_equal(f[0], want_v, err_msg=f"viol n={n} s={s}")
+                want = oracle.label_plan(want_v, lab, n)
+                for i, what in ((1, "add"), (2, "rem")):
+                    np.testing.assert_array_equal(f[i], want[i - 1], err_msg=f"{what} n={n} s={s}")
+                    np.testing.assert_array_equal(f[i], sep[i], err_msg=f"{what} n={n} s={s}")
+                assert f[3] == want[2] == sep[3], (n, s)
+        gen += 1
+
+
+@pytest.mark.gpu
+def test_deschedule_fused_no_strategies_and_errors(ctx):
+    import torch
+    n = 1000
+    snap = wl.make_tas_snapshot(n, 4, seed=3)
+    ctx.tas_snapshot_set(7300, snap.v_milli, snap.present)
+    dev = torch.device("cuda", 0)
+    add_t = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    rem_t = torch.full((n,), -1, dtype=torch.int64, device=dev)
+    total_t = torch.full((1,), -7, dtype=torch.int64, device=dev)
+    off_t = torch.zeros(1, dtype=torch.int32, device=dev)
+    viol_t = torch.zeros(1, dtype=torch.int64, device=dev)
+    ctx.tas_deschedule_device(7300, 0, 0, None, off_t, viol_t, None, add_t, rem_t, total_t)
+    torch.cuda.synchronize()
+    assert not add_t.any() and not rem_t.any() and int(total_t.item()) == 0
+    with pytest.raises(pas_amd.PasError) as e:  # more than 64 strategies
+        ctx.tas_deschedule_device(7300, 65, 0, None, off_t, viol_t, None, add_t, rem_t, total_t)
+    assert e.value.code == pas_amd._lib.PAS_EINVAL
+    with pytest.raises(pas_amd.PasError) as e:  # stale generation
+        ctx.tas_deschedule_device(7299, 1, 0, None, off_t, viol_t, None, add_t, rem_t, total_t)
 
 
 @pytest.mark.gpu
