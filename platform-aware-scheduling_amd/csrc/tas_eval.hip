@@ -680,10 +680,10 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
   int64_t violated = 0;
   if constexpr (kPlan) {  // lane t: strategy t's carried-label words of this wave's run
     if (lane < n_strat) {
-      const uint64_t* lrow = plan.labels + (int64_t)lane * W64;
 #pragma unroll
       for (int k = 0; k < kRun; ++k)
-        lws[threadIdx.x >> 6][lane][k] = plan.labels ? lrow[min(gw0 + k, W64 - 1)] : 0ull;
+        lws[threadIdx.x >> 6][lane][k] =
+            plan.labels ? plan.labels[(int64_t)lane * W64 + min(gw0 + k, W64 - 1)] : 0ull;
     }
   }
   auto flush = [&]() {
