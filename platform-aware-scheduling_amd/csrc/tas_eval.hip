@@ -101,6 +101,9 @@ __device__ void block_exclusive_scan(int32_t* a, int32_t n) {
 }
 
 // ---------------------------------------------------------------------------- prep
+#ifndef PAS_PREP_STAMPS
+#define PAS_PREP_STAMPS 0  // diagnostic builds: phase times of the prep (printf, 100 MHz ticks)
+#endif
 //
 // One launch, two roles: block 0 groups the pods (below); blocks 1.. map every rule to its
 // range (a3).  The two are independent, so the binary searches run beside the grouping.
@@ -219,6 +222,13 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
   const bool prio = (g.flags & PAS_TAS_PRIORITIZE) != 0 && g.M > 0;
   for (int32_t i = tid; i <= G; i += kGroupTpb) hist[i] = 0;
   const bool filt = (g.flags & PAS_TAS_FILTER) != 0;
+#if PAS_PREP_STAMPS
+  uint64_t st[6];
+  st[0] = __builtin_amdgcn_s_memrealtime();
+#define PAS_STAMP(i) st[i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PAS_STAMP(i)
+#endif
   if (g.P > 0 && g.P <= kGroupTpb * kGU && g.M <= kGroupTpb) {
     // one round: every load of the pods (prioritize rule, rule offsets) in flight together,
     // the keys kept in registers between the histogram and the scatter
@@ -235,6 +245,7 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
     }
     if (tid < g.M) cnt[tid] = g.cnt[tid];
     __syncthreads();
+    PAS_STAMP(1);
 #pragma unroll
     for (int u = 0; u < kGU; ++u) c[u] = prio ? cnt[min(max(r[u].metric, 0), g.M - 1)] : 0;
 #pragma unroll
@@ -245,7 +256,9 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
       if (tid + u * kGroupTpb < g.P) atomicAdd(&hist[key[u]], 1);
     }
     __syncthreads();
+    PAS_STAMP(2);
     block_exclusive_scan(hist, G + 1);
+    PAS_STAMP(3);
 #pragma unroll
     for (int u = 0; u < kGU; ++u) {
       const int32_t p = tid + u * kGroupTpb;
@@ -255,6 +268,16 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
       g.desc[2 * pos] = make_int4(p, key[u] < G ? key[u] : -1, c[u], 0);
       g.desc[2 * pos + 1] = make_int4(r0[u], r1[u], 0, 0);
     }
+#if PAS_PREP_STAMPS
+    PAS_STAMP(4);
+    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0);
+    PAS_STAMP(5);
+    if (tid == 0)
+      printf("STAMP group load %d hist %d scan %d scatter %d drain %d\n", (int)(st[1] - st[0]),
+             (int)(st[2] - st[1]), (int)(st[3] - st[2]), (int)(st[4] - st[3]),
+             (int)(st[5] - st[4]));
+#endif
     return;
   }
   __syncthreads();
@@ -315,6 +338,11 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
 #endif
 __global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, RangesParams R) {
   extern __shared__ __attribute__((aligned(16))) int32_t sh[];
+#if PAS_PREP_STAMPS
+  const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 1 || blockIdx.x == gridDim.x - 1))
+    printf("STAMP start block %d t %llu\n", (int)blockIdx.x, (unsigned long long)t_start);
+#endif
   if (blockIdx.x == 0) {
     if (!(PAS_PREP_ABLATE & 2)) group_body(g, sh);
     return;
@@ -323,6 +351,13 @@ __global__ __launch_bounds__(kGroupTpb) void tas_prep_kernel(GroupParams g, Rang
   const int32_t r =
       (int32_t)(blockIdx.x - 1) * (kGroupTpb / kRuleLanes) + (int32_t)(threadIdx.x / kRuleLanes);
   if (r < R.n_rules) ranges_group(R, r);
+#if PAS_PREP_STAMPS
+  __syncthreads();
+  if (threadIdx.x == 0 && (blockIdx.x == 1 || blockIdx.x == gridDim.x - 1))
+    printf("STAMP ranges block %d took %d end %llu\n", (int)blockIdx.x,
+           (int)(__builtin_amdgcn_s_memrealtime() - t_start),
+           (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#endif
 }
 
 // ---------------------------------------------------------------------------- eval
