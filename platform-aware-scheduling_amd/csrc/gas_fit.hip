@@ -2364,7 +2364,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     // the join: each side stream sets its flag after its work; s waits for both (enqueued
     // after the signals)
     gas_signal_kernel<<<1, 64, 0, ss>>>(sync + 1, epoch);
-    gas_signal_kernel<<<1, 64, 0, qs>>>(sync + 2, epoch);
+    gas_signal_kernel<<<1, 64, 0, slot->side2>>>(sync + 2, epoch);
     gas_wait_kernel<<<1, 64, 0, s>>>(sync + 1, 2, epoch, limit, ctx->gas_sync_fault);
     PAS_HIP(ctx, hipGetLastError());
     joins.forked = 0;
