@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define PAS_ABI_VERSION 2
+#define PAS_ABI_VERSION 3
 
 typedef enum pas_status {
   PAS_OK = 0,
@@ -220,37 +220,51 @@ int pas_tas_violations_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
                               void* hip_stream);
 
 /* Deschedule label plan (Deschedule.updateNodeLabels, deschedule/enforce.go:99-151) for
- * n_strategies <= 64 strategies from a sweep's viol[s][W64(n_nodes)] and the nodes' labels:
+ * n_strategies <= 64 strategies from a sweep's viol[s][W64(n_nodes)] and the nodes' labels.
+ * The reference keys its non-violated set by policy NAME (allPolicies, :89-95), and two
+ * registered strategies may share a name (SetPolicyName drops the namespace,
+ * controller/controller.go:80; AddStrategy drops only Equals duplicates,
+ * core/enforcer.go:84-103):
+ *   name_id      [s] host array: strategies s and t share a policy name iff
+ *                name_id[s] == name_id[t] (any int32 values); NULL = all names distinct.
+ *                A name is represented by its first strategy k (lowest index).
  *   labels       [s][W64] bit set = the node carries label <policy name of s> (any value);
- *                NULL = no node carries any
- *   add_out      [n_nodes] bit s = add "<policy>": "violating" (:108-117)
- *   remove_out   [n_nodes] bit s = remove the label, then add it as "null" (:118-132)
- *   total_out    the function's int result: the count of NON-violated (node, strategy)
- *                pairs (totalViolations++ sits in the non-violated loop, :133)
- * pas_label_patch_json renders one node's masks as the PATCH body. */
+ *                only the rows of each name's first strategy are read; NULL = no node
+ *                carries any
+ *   add_out      [n_nodes] bit s = strategy s violated at the node: add "<name>":
+ *                "violating", one entry per violating strategy (:108-117)
+ *   remove_out   [n_nodes] bit k = name k (its first strategy) violated by none of its
+ *                strategies and carried: remove it, then add it as "null" (:118-132)
+ *   total_out    the function's int result: the count of NON-violated (node, name) pairs
+ *                (totalViolations++ sits in the non-violated loop, :133)
+ * More than 64 strategies: call per group of <= 64 that keeps every name's strategies
+ * together, OR the masks' strategy offsets back in and sum the totals (DescheduleEnforcer).
+ * pas_label_patch_json renders one node's masks as the PATCH body.  The _device forms take
+ * device viol / labels / outputs and a host name_id, and are asynchronous on hip_stream. */
 int pas_tas_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strategies,
-                       const uint64_t* viol, const uint64_t* labels, uint64_t* add_out,
-                       uint64_t* remove_out, int64_t* total_out);
+                       const uint64_t* viol, const int32_t* name_id, const uint64_t* labels,
+                       uint64_t* add_out, uint64_t* remove_out, int64_t* total_out);
 int pas_tas_label_plan_device(pas_ctx* ctx, int32_t n_nodes, int32_t n_strategies,
-                              const uint64_t* d_viol, const uint64_t* d_labels,
-                              uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
-                              void* hip_stream);
+                              const uint64_t* d_viol, const int32_t* name_id,
+                              const uint64_t* d_labels, uint64_t* d_add_out,
+                              uint64_t* d_remove_out, int64_t* d_total_out, void* hip_stream);
 
 /* The deschedule sweep and its label plan in one pass (Deschedule.Cleanup's violation lists,
  * deschedule/strategy.go:31-50, then updateNodeLabels, enforce.go:99-151): outputs as
  * pas_tas_violations_device (viol_out) followed by pas_tas_label_plan_device on those
- * bitmaps for the snapshot's n_nodes (labels / add_out / remove_out / total_out), without
- * re-reading the bitmaps.  n_strategies <= 64. */
+ * bitmaps for the snapshot's n_nodes (name_id / labels / add_out / remove_out / total_out),
+ * without re-reading the bitmaps.  n_strategies <= 64. */
 int pas_tas_deschedule_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
                               int32_t n_rules, const pas_rule* d_rules,
                               const int32_t* d_rule_off, uint64_t* d_viol_out,
-                              const uint64_t* d_labels, uint64_t* d_add_out,
-                              uint64_t* d_remove_out, int64_t* d_total_out, void* hip_stream);
+                              const int32_t* name_id, const uint64_t* d_labels,
+                              uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
+                              void* hip_stream);
 
 /* json.Marshal of the node's []patchValue (enforce.go:21-25, 74-86) for the masks of
  * pas_tas_label_plan: adds in strategy order, then a remove + add "null" pair per removed
- * label in strategy order (the reference emits these in Go-map order).  names[s] = policy
- * name of strategy s.  Writes at most cap bytes (no terminator); *len = full length;
+ * label in the order of the names' first strategies (the reference emits these in Go-map
+ * order).  names[s] = policy name of strategy s.  Writes at most cap bytes (no terminator); *len = full length;
  * PAS_ECAPACITY if it exceeds cap.  Host-only. */
 int pas_label_patch_json(int32_t n_strategies, const char* const* names, uint64_t add_mask,
                          uint64_t remove_mask, char* buf, int64_t cap, int64_t* len);

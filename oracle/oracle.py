@@ -64,7 +64,7 @@ def load():
                                           c_int32, P, P, P, P, P]),
         "or_gas_release": (c_int, [c_int32, c_int32, c_int32, P, P, c_int32, P, P, c_int32,
                                    P, P, P, P, P, c_int32, P]),
-        "or_label_plan": (c_int, [c_int32, c_int32, P, P, P, P, P]),
+        "or_label_plan": (c_int, [c_int32, c_int32, P, P, P, P, P, P]),
         "or_label_patch_json": (c_int64, [c_int32, P, ctypes.c_uint64, ctypes.c_uint64,
                                           ctypes.c_char_p, c_int64]),
     }
@@ -245,16 +245,22 @@ def gas_release_counts(n_cards, used, req, req_mask, n_containers, pods, nodes, 
     return used, st
 
 
-def label_plan(viol, labels, n_nodes):
-    """updateNodeLabels per node: (add masks, remove masks, totalViolations)."""
+def label_plan(viol, labels, n_nodes, names=None):
+    """updateNodeLabels per node: (add masks, remove masks, totalViolations).  names[s] =
+    policy name of strategy s (None: all distinct); a name's remove bit and labels row are
+    those of its first strategy."""
     viol = np.ascontiguousarray(viol, np.uint64)
     s = viol.shape[0]
     labels = None if labels is None else np.ascontiguousarray(labels, np.uint64)
+    arr = None
+    if names is not None:
+        assert len(names) == s
+        arr = (ctypes.c_char_p * max(s, 1))(*[n.encode() for n in names])
     add = np.zeros(n_nodes, np.uint64)
     rem = np.zeros(n_nodes, np.uint64)
     total = c_int64(0)
-    rc = load().or_label_plan(n_nodes, s, _p(viol), _p(labels), _p(add), _p(rem),
-                              ctypes.byref(total))
+    rc = load().or_label_plan(n_nodes, s, None if arr is None else ctypes.cast(arr, c_void_p),
+                              _p(viol), _p(labels), _p(add), _p(rem), ctypes.byref(total))
     if rc != 0:
         raise ValueError("oracle label_plan: more than 64 strategies")
     return add, rem, total.value

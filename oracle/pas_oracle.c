@@ -233,21 +233,36 @@ int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli
 
 /* ---- deschedule label payloads ------------------------------------------- */
 
-int or_label_plan(int32_t n_nodes, int32_t n_strat, const uint64_t* viol, const uint64_t* labels,
-                  uint64_t* add, uint64_t* rem, int64_t* total_violations) {
+int or_label_plan(int32_t n_nodes, int32_t n_strat, const char* const* names,
+                  const uint64_t* viol, const uint64_t* labels, uint64_t* add, uint64_t* rem,
+                  int64_t* total_violations) {
   if (n_strat < 0 || n_strat > 64) return -1;
   const int64_t w = w64(n_nodes);
+  /* allPolicies (enforce.go:89-95): the registered strategies' policy NAMES as a set.  A
+   * name is represented by its first strategy (first[s] = lowest t with names[t] == names[s]);
+   * that strategy's labels row says whether a node carries the label <name>. */
+  int32_t first[64];
+  for (int32_t s = 0; s < n_strat; ++s) {
+    first[s] = s;
+    if (names)
+      for (int32_t t = 0; t < s; ++t)
+        if (strcmp(names[t], names[s]) == 0) { first[s] = t; break; }
+  }
   int64_t total = 0;
   for (int32_t n = 0; n < n_nodes; ++n) {          /* for _, node := range allNodes.Items */
     uint64_t a = 0, r = 0;
-    for (int32_t s = 0; s < n_strat; ++s) {
-      if (has_bit(viol + s * w, n)) {                /* viols[node.Name] (:108-117) */
-        a |= 1ull << s;
-      } else {                                       /* nonViolatedPolicies (:118-134) */
-        if (labels && has_bit(labels + s * w, n)) r |= 1ull << s;
-        ++total;                                     /* totalViolations++ for every one */
+    uint8_t non_violated[64];                      /* nonViolatedPolicies = allPolicies(...) */
+    for (int32_t s = 0; s < n_strat; ++s) non_violated[s] = first[s] == s;
+    for (int32_t s = 0; s < n_strat; ++s)          /* for _, policyName := range viols[node] */
+      if (has_bit(viol + s * w, n)) {
+        non_violated[first[s]] = 0;                /* delete(nonViolatedPolicies, name) */
+        a |= 1ull << s;                            /* one "add" per violating strategy */
       }
-    }
+    for (int32_t k = 0; k < n_strat; ++k)          /* for policyName := range nonViolated... */
+      if (non_violated[k]) {
+        if (labels && has_bit(labels + k * w, n)) r |= 1ull << k;  /* remove + add "null" */
+        ++total;                                   /* totalViolations++ per name (:133) */
+      }
     add[n] = a;
     rem[n] = r;
   }

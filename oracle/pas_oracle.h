@@ -75,12 +75,18 @@ int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli
                       const int32_t* rule_off, uint64_t* viol_out);
 
 /* Deschedule.updateNodeLabels (deschedule/enforce.go:99-151) per node, for S <= 64
- * registered strategies: add[n] = strategies violated at node n (their label is added as
- * "violating"), rem[n] = not violated but labelled (label removed, then added as "null").
- * *total_violations counts, as the reference does, the NON-violated (node, strategy)
- * pairs (enforce.go:118-134). */
-int or_label_plan(int32_t n_nodes, int32_t n_strat, const uint64_t* viol, const uint64_t* labels,
-                  uint64_t* add, uint64_t* rem, int64_t* total_violations);
+ * registered strategies with policy names names[s] (NULL = all distinct).  The reference
+ * keys the non-violated set by policy NAME (allPolicies, :89-95; delete per violating
+ * strategy, :109), and two registered strategies can share one (AddStrategy drops only
+ * Equals duplicates, core/enforcer.go:84-103).  A name is represented by its first
+ * strategy k; labels[k] row = the nodes carrying the label <name>.
+ *   add[n] bit s = strategy s violated at node n (one "violating" add per strategy, :108-117)
+ *   rem[n] bit k = name k violated by none of its strategies and carried (remove + add
+ *                  "null", :118-132)
+ *   *total_violations = the NON-violated (node, name) pairs (totalViolations++, :133). */
+int or_label_plan(int32_t n_nodes, int32_t n_strat, const char* const* names,
+                  const uint64_t* viol, const uint64_t* labels, uint64_t* add, uint64_t* rem,
+                  int64_t* total_violations);
 /* json.Marshal of the node's []patchValue (enforce.go:20-24, 76-83): adds in strategy
  * order, then remove + add-null pairs in strategy order (the reference's order is map
  * iteration).  Returns the length, or -1 if cap is too small. */

@@ -1156,8 +1156,8 @@ static int check_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, cons
 }
 
 int pas_tas_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* viol,
-                       const uint64_t* labels, uint64_t* add_out, uint64_t* remove_out,
-                       int64_t* total_out) {
+                       const int32_t* name_id, const uint64_t* labels, uint64_t* add_out,
+                       uint64_t* remove_out, int64_t* total_out) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_label_plan(ctx, n_nodes, n_strat, viol, add_out, remove_out, total_out,
                             "pas_tas_label_plan");
@@ -1179,8 +1179,8 @@ int pas_tas_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uin
     PAS_HIP(ctx, hipMemcpyAsync(d_viol, viol, b_bits, hipMemcpyHostToDevice, s));
     if (labels) PAS_HIP(ctx, hipMemcpyAsync(d_labels, labels, b_bits, hipMemcpyHostToDevice, s));
   }
-  rc = label_plan_launch(ctx, n_nodes, n_strat, d_viol, labels ? d_labels : nullptr, d_add,
-                         d_rem, d_total, s);
+  rc = label_plan_launch(ctx, n_nodes, n_strat, make_name_plan(n_strat, name_id), d_viol,
+                         labels ? d_labels : nullptr, d_add, d_rem, d_total, s);
   if (rc) return rc;
   if (b_mask) {
     PAS_HIP(ctx, hipMemcpyAsync(add_out, d_add, b_mask, hipMemcpyDeviceToHost, s));
@@ -1192,23 +1192,25 @@ int pas_tas_label_plan(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uin
 }
 
 int pas_tas_label_plan_device(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat,
-                              const uint64_t* d_viol, const uint64_t* d_labels,
-                              uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
-                              void* hip_stream) {
+                              const uint64_t* d_viol, const int32_t* name_id,
+                              const uint64_t* d_labels, uint64_t* d_add_out,
+                              uint64_t* d_remove_out, int64_t* d_total_out, void* hip_stream) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_label_plan(ctx, n_nodes, n_strat, d_viol, d_add_out, d_remove_out,
                             d_total_out, "pas_tas_label_plan_device");
   if (rc) return rc;
   if ((rc = activate(ctx))) return rc;
-  return label_plan_launch(ctx, n_nodes, n_strat, d_viol, d_labels, d_add_out, d_remove_out,
-                           d_total_out, pick_stream(ctx, hip_stream));
+  return label_plan_launch(ctx, n_nodes, n_strat, make_name_plan(n_strat, name_id), d_viol,
+                           d_labels, d_add_out, d_remove_out, d_total_out,
+                           pick_stream(ctx, hip_stream));
 }
 
 int pas_tas_deschedule_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
                               int32_t n_rules, const pas_rule* d_rules,
                               const int32_t* d_rule_off, uint64_t* d_viol_out,
-                              const uint64_t* d_labels, uint64_t* d_add_out,
-                              uint64_t* d_remove_out, int64_t* d_total_out, void* hip_stream) {
+                              const int32_t* name_id, const uint64_t* d_labels,
+                              uint64_t* d_add_out, uint64_t* d_remove_out, int64_t* d_total_out,
+                              void* hip_stream) {
   if (!ctx) return PAS_EINVAL;
   int rc = check_tas_gen(ctx, gen);
   if (rc) return rc;
@@ -1219,8 +1221,9 @@ int pas_tas_deschedule_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
   if (n_strategies > 0 && (!d_rule_off || (n_rules > 0 && !d_rules)))
     return set_error(ctx, PAS_EINVAL, "pas_tas_deschedule_device: null input");
   if ((rc = activate(ctx))) return rc;
-  return tas_deschedule_launch(ctx, n_strategies, d_rules, d_rule_off, d_viol_out, d_labels,
-                               d_add_out, d_remove_out, d_total_out, pick_stream(ctx, hip_stream));
+  return tas_deschedule_launch(ctx, n_strategies, d_rules, d_rule_off, d_viol_out,
+                               make_name_plan(n_strategies, name_id), d_labels, d_add_out,
+                               d_remove_out, d_total_out, pick_stream(ctx, hip_stream));
 }
 
 // --------------------------------------------------------------------------- node shards

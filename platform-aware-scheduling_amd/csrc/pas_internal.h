@@ -283,16 +283,37 @@ int gas_commit_launch(pas_ctx* ctx, bool release, int32_t n_seg, int32_t max_con
                       const int32_t* d_cards, int32_t cards_stride, uint32_t* d_res,
                       int32_t* d_status, uint8_t* d_cards_out, int32_t* d_nsel_out,
                       int64_t* d_counts_out, const int64_t* d_counts, hipStream_t s);
-int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
-                      const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
-                      int64_t* d_total, hipStream_t s);
+// Policy names of the deschedule strategies (updateNodeLabels keys its non-violated set by
+// name, deschedule/enforce.go:89-134).  A name is represented by its first strategy k
+// (canonical); bit k of canon marks those.  Names held by one strategy are the bits of single;
+// each name held by two or more strategies is a group: its member strategies and its k.  A
+// node's violated names: (add & single) | {key[g] : add & group[g] != 0}.
+struct NamePlan {
+  uint64_t canon = 0;
+  uint64_t single = 0;
+  int32_t n_groups = 0;
+  uint8_t key[32] = {};
+  uint64_t group[32] = {};
+};
+// The plan of name_id[0 .. n_strat) (NULL = all distinct); n_strat <= 64.
+NamePlan make_name_plan(int32_t n_strat, const int32_t* name_id);
+__device__ __forceinline__ uint64_t violated_names(const NamePlan& np, uint64_t add) {
+  uint64_t vn = add & np.single;
+  for (int32_t g = 0; g < np.n_groups; ++g)
+    vn |= (add & np.group[g]) ? 1ull << np.key[g] : 0ull;
+  return vn;
+}
+int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const NamePlan& names,
+                      const uint64_t* d_viol, const uint64_t* d_labels, uint64_t* d_add,
+                      uint64_t* d_rem, int64_t* d_total, hipStream_t s);
 // totalViolations from per-block counts of violated pairs: *d_total = pairs - sum(d_part).
 int label_total_launch(pas_ctx* ctx, int32_t n_parts, int64_t pairs, const int64_t* d_part,
                        int64_t* d_total, hipStream_t s);
 // The deschedule sweep with the label plan fused in (pas_tas_deschedule_device): viol as
 // tas_violations_launch, add / rem / total as label_plan_launch on those bitmaps.
 int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
-                          const int32_t* d_rule_off, uint64_t* d_viol, const uint64_t* d_labels,
-                          uint64_t* d_add, uint64_t* d_rem, int64_t* d_total, hipStream_t s);
+                          const int32_t* d_rule_off, uint64_t* d_viol, const NamePlan& names,
+                          const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
+                          int64_t* d_total, hipStream_t s);
 
 }  // namespace pas

@@ -678,10 +678,12 @@ constexpr int kWaves = kTpb / 64;
 // as label_plan_kernel in tas_labels.hip): the wave's carried-label words [S][kRun] are read
 // into its LDS slice before the walk, a strategy's completed words go next to them, and after
 // the walk lane l turns both into the masks of nodes (gw0 + k) * 64 + l, one word k at a time
-// (bit s = bit l of word (s, k), from broadcast LDS reads; the block stores its count of
-// violated pairs).
+// (bit s = bit l of word (s, k), from broadcast LDS reads; removes and the count are by policy
+// name, NamePlan; the block stores its count of violated (node, name) pairs).  The run length
+// is fixed at 8 words per wave here (PAS_VIOL_RUN tunes only the unfused sweep).
 static_assert(kWaves == 4, "the plan's per-block count sums four waves");
 struct PlanOut {
+  NamePlan names;
   const uint64_t* labels;  // [S][W64] or null
   uint64_t* add;           // [N]
   uint64_t* rem;           // [N]
@@ -724,7 +726,6 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
   auto flush = [&]() {
     if (lane < kRun && gw0 + lane < W64) viol_out[(int64_t)s * W64 + gw0 + lane] = acc;
     if constexpr (kPlan) {
-      violated += __popcll(acc);  // (lanes past kRun hold 0)
       if (lane < kRun) vws[threadIdx.x >> 6][s][lane] = acc;
     }
     acc = 0;
@@ -801,8 +802,10 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
       const int64_t n = (int64_t)(gw0 + k) * 64 + lane;
       if (n < N) {
         const uint64_t av = (uint64_t)a[1] << 32 | a[0], rv = (uint64_t)r[1] << 32 | r[0];
+        const uint64_t vn = violated_names(plan.names, av);
+        violated += __popcll(vn);
         plan.add[n] = av;
-        plan.rem[n] = rv & ~av;
+        plan.rem[n] = rv & plan.names.canon & ~vn;
       }
     }
     for (int off = 32; off > 0; off >>= 1) violated += __shfl_xor(violated, off, 64);
@@ -1004,15 +1007,16 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   const int32_t rwaves = (W64 + per - 1) / per;
   rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
       t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol,
-      PlanOut{});
+      PlanOut{NamePlan{}, nullptr, nullptr, nullptr, nullptr});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
 }
 
 int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
-                          const int32_t* d_rule_off, uint64_t* d_viol, const uint64_t* d_labels,
-                          uint64_t* d_add, uint64_t* d_rem, int64_t* d_total, hipStream_t s) {
+                          const int32_t* d_rule_off, uint64_t* d_viol, const NamePlan& names,
+                          const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
+                          int64_t* d_total, hipStream_t s) {
   const TasSnapshot& t = ctx->tas;
   const int32_t N = t.n_nodes, W64 = (int32_t)w64(N);
   if (W64 == 0 || n_strat == 0) {  // no pairs: every mask 0, total 0
@@ -1036,10 +1040,11 @@ int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   timing_begin(ctx, s, PAS_K_TAS_VIOLATIONS, &tl);
   tas_violations_run_kernel<kRun, true><<<blocks, kTpb, 0, s>>>(
       N, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol,
-      PlanOut{d_labels, d_add, d_rem, part});
+      PlanOut{names, d_labels, d_add, d_rem, part});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
-  return label_total_launch(ctx, blocks, (int64_t)N * n_strat, part, d_total, s);
+  return label_total_launch(ctx, blocks, (int64_t)N * __builtin_popcountll(names.canon), part,
+                            d_total, s);
 }
 
 }  // namespace pas

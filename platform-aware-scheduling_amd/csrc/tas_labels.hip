@@ -3,18 +3,21 @@
 //
 // Deschedule.updateNodeLabels (deschedule/enforce.go:99-151) walks every node: for each
 // strategy whose violation list holds the node it adds the strategy's label with value
-// "violating" (:108-117); for every other registered strategy it counts a "violation"
-// (totalViolations++, :118-134 — the reference counts the non-violated pairs) and, when the
-// node carries that label, removes it and re-adds it as "null" (:119-132).  Per node that is
-// two 64-bit masks over <= 64 strategies.  The sweep's output is [S][W64] bitmaps (a word =
-// 64 nodes of one strategy), so the plan is a 64 x S bit transpose per word: one wave per
-// word, lane s loads word w of strategy row s (violations and labels), the S words are
-// broadcast with readlane and each lane (node) collects bit s of each.  HBM-bound byte work:
-// 2 * S * 8 bytes read per 64 nodes, 16 bytes written per node.
+// "violating" (:108-117); for every registered policy NAME none of whose strategies is
+// violated it counts a "violation" (totalViolations++, :118-134 — the reference counts the
+// non-violated names) and, when the node carries that label, removes it and re-adds it as
+// "null" (:119-132).  The non-violated set is keyed by name (allPolicies, :89-95), and two
+// strategies can share one (NamePlan, pas_internal.h).  Per node that is two 64-bit masks
+// over <= 64 strategies: add by strategy, remove by the name's first strategy.  The sweep's
+// output is [S][W64] bitmaps (a word = 64 nodes of one strategy), so the plan is a 64 x S
+// bit transpose per word: one wave per word, lane s loads word w of strategy row s
+// (violations and labels), the S words are broadcast with readlane and each lane (node)
+// collects bit s of each.  HBM-bound byte work: 2 * S * 8 bytes read per 64 nodes, 16 bytes
+// written per node.
 //
 // totalViolations is a count over the whole node list, so the kernel writes one partial
-// count of violated pairs per workgroup and a one-workgroup kernel finishes the sum (device-
-// scope atomics on one address serialise across the 8 XCDs).
+// count of violated (node, name) pairs per workgroup and a one-workgroup kernel finishes the
+// sum (device-scope atomics on one address serialise across the 8 XCDs).
 //
 // The JSON body of one node's patch (enforce.go:21-25, 74-86) is host work on the two masks:
 // pas_label_patch_json below.
@@ -41,7 +44,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int s) {
 }
 
 __global__ __launch_bounds__(kTpb) void label_plan_kernel(int32_t n_nodes, int32_t n_strat,
-                                                          int64_t W,
+                                                          int64_t W, NamePlan names,
                                                           const uint64_t* __restrict__ viol,
                                                           const uint64_t* __restrict__ labels,
                                                           uint64_t* __restrict__ add,
@@ -51,7 +54,7 @@ __global__ __launch_bounds__(kTpb) void label_plan_kernel(int32_t n_nodes, int32
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int64_t stride = (int64_t)gridDim.x * kWaves;
-  int64_t violated = 0;  // violated pairs of this lane's strategy row
+  int64_t violated = 0;  // violated (node, name) pairs of this lane's nodes
   for (int64_t w = (int64_t)blockIdx.x * kWaves + wave; w < W; w += stride) {
     uint64_t vw = 0, lw = 0;
     if (lane < n_strat) {
@@ -59,15 +62,15 @@ __global__ __launch_bounds__(kTpb) void label_plan_kernel(int32_t n_nodes, int32
       if (labels) lw = labels[lane * W + w];
     }
     const int64_t valid = min((int64_t)64, (int64_t)n_nodes - w * 64);
-    vw &= valid == 64 ? ~0ull : ((1ull << valid) - 1);
-    violated += __popcll(vw);
     uint64_t a = 0, r = 0;
     for (int s = 0; s < n_strat; ++s) a |= ((readlane64(vw, s) >> lane) & 1ull) << s;
     if (labels)
       for (int s = 0; s < n_strat; ++s) r |= ((readlane64(lw, s) >> lane) & 1ull) << s;
     if (lane < valid) {
+      const uint64_t vn = violated_names(names, a);
+      violated += __popcll(vn);
       add[w * 64 + lane] = a;
-      rem[w * 64 + lane] = r & ~a;
+      rem[w * 64 + lane] = r & names.canon & ~vn;
     }
   }
   for (int off = 32; off > 0; off >>= 1) violated += __shfl_xor(violated, off, 64);
@@ -80,7 +83,7 @@ __global__ __launch_bounds__(kTpb) void label_plan_kernel(int32_t n_nodes, int32
   }
 }
 
-// totalViolations = the non-violated pairs = n_nodes * S - violated pairs.
+// totalViolations = the non-violated pairs = n_nodes * names - violated pairs.
 __global__ __launch_bounds__(kTpb) void label_total_kernel(int32_t n_parts, int64_t pairs,
                                                            const int64_t* __restrict__ part,
                                                            int64_t* __restrict__ total) {
@@ -118,9 +121,35 @@ int label_total_launch(pas_ctx* ctx, int32_t n_parts, int64_t pairs, const int64
   return PAS_OK;
 }
 
-int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint64_t* d_viol,
-                      const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
-                      int64_t* d_total, hipStream_t s) {
+NamePlan make_name_plan(int32_t n_strat, const int32_t* name_id) {
+  NamePlan np;
+  uint64_t member[64] = {};
+  for (int32_t s = 0; s < n_strat; ++s) {
+    int32_t k = s;  // the name's first strategy
+    if (name_id)
+      for (int32_t t = 0; t < s; ++t)
+        if (name_id[t] == name_id[s]) {
+          k = t;
+          break;
+        }
+    member[k] |= 1ull << s;
+  }
+  for (int32_t k = 0; k < n_strat; ++k) {
+    if (!member[k]) continue;
+    np.canon |= 1ull << k;
+    if (member[k] == 1ull << k) {
+      np.single |= 1ull << k;
+    } else {
+      np.key[np.n_groups] = (uint8_t)k;
+      np.group[np.n_groups++] = member[k];
+    }
+  }
+  return np;
+}
+
+int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const NamePlan& names,
+                      const uint64_t* d_viol, const uint64_t* d_labels, uint64_t* d_add,
+                      uint64_t* d_rem, int64_t* d_total, hipStream_t s) {
   // the partial counts are the stream's slot buffer: plans on other streams may run beside
   int rc = PAS_OK;
   SlotScope sc(ctx, s, 0, &rc);
@@ -133,10 +162,10 @@ int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint
                                                                    kMaxBlocks));
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_LABELS, &tl);
-  label_plan_kernel<<<blocks, kTpb, 0, s>>>(n_nodes, n_strat, W, d_viol, d_labels, d_add, d_rem,
-                                            part);
-  label_total_kernel<<<1, kTpb, 0, s>>>(blocks, (int64_t)n_nodes * n_strat, part,
-                                        d_total);
+  label_plan_kernel<<<blocks, kTpb, 0, s>>>(n_nodes, n_strat, W, names, d_viol, d_labels, d_add,
+                                            d_rem, part);
+  const int64_t pairs = (int64_t)n_nodes * __builtin_popcountll(names.canon);
+  label_total_kernel<<<1, kTpb, 0, s>>>(blocks, pairs, part, d_total);
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
@@ -145,8 +174,9 @@ int label_plan_launch(pas_ctx* ctx, int32_t n_nodes, int32_t n_strat, const uint
 }  // namespace pas
 
 // json.Marshal([]patchValue) of one node's label patch: the adds in strategy order, then a
-// remove + add-"null" pair per removed label in strategy order (the reference iterates a
-// Go map there, whose order is unspecified; the set of operations is the same).
+// remove + add-"null" pair per removed label in the order of the names' first strategies
+// (the reference iterates a Go map there, whose order is unspecified; the set of operations
+// is the same).
 extern "C" int pas_label_patch_json(int32_t n_strat, const char* const* names, uint64_t add_mask,
                                     uint64_t remove_mask, char* buf, int64_t cap, int64_t* len) {
   if (n_strat < 0 || n_strat > 64 || !names || !len || cap < 0 || (cap > 0 && !buf))

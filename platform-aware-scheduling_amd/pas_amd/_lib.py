@@ -132,10 +132,10 @@ SIGNATURES = {
     ),
     "pas_tas_violations": (c_int, [_P, c_uint64, c_int32, _P, _P, _P]),
     "pas_tas_violations_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P]),
-    "pas_tas_label_plan": (c_int, [_P, c_int32, c_int32, _P, _P, _P, _P, _P]),
-    "pas_tas_label_plan_device": (c_int, [_P, c_int32, c_int32, _P, _P, _P, _P, _P, _P]),
+    "pas_tas_label_plan": (c_int, [_P, c_int32, c_int32, _P, _P, _P, _P, _P, _P]),
+    "pas_tas_label_plan_device": (c_int, [_P, c_int32, c_int32, _P, _P, _P, _P, _P, _P, _P]),
     "pas_tas_deschedule_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P, _P, _P, _P,
-                                          _P, _P]),
+                                          _P, _P, _P]),
     "pas_label_patch_json": (
         c_int,
         [c_int32, POINTER(c_char_p), c_uint64, c_uint64, c_char_p, c_int64, POINTER(c_int64)],

@@ -270,36 +270,52 @@ class Context:
                                                _stream(stream))
         self._check(rc, "pas_tas_violations_device")
 
-    def tas_label_plan(self, n_nodes: int, viol: np.ndarray, labels: Optional[np.ndarray] = None):
+    @staticmethod
+    def _name_ids(names, n_strat: int):
+        """int32 name ids of policy names (None: all distinct) as pas_tas_label_plan takes
+        them: equal names, equal ids."""
+        if names is None:
+            return None
+        assert len(names) == n_strat, "one policy name per strategy"
+        ids = {}
+        return np.array([ids.setdefault(n, len(ids)) for n in names], np.int32)
+
+    def tas_label_plan(self, n_nodes: int, viol: np.ndarray, labels: Optional[np.ndarray] = None,
+                       names=None):
         """(add [n_nodes] u64, remove [n_nodes] u64, total) of updateNodeLabels
-        (deschedule/enforce.go:99-151) from viol[S][W64] and labels[S][W64] (or None)."""
+        (deschedule/enforce.go:99-151) from viol[S][W64] and labels[S][W64] (or None);
+        names[s] = policy name of strategy s (None: all distinct)."""
         viol = np.ascontiguousarray(viol, dtype=np.uint64)
         s = viol.shape[0]
         if labels is not None:
             labels = np.ascontiguousarray(labels, dtype=np.uint64)
             assert labels.shape == viol.shape, "labels must have the shape of viol"
+        ids = self._name_ids(names, s)
         add = np.zeros(n_nodes, np.uint64)
         rem = np.zeros(n_nodes, np.uint64)
         total = c_int64()
         rc = self._l.pas_tas_label_plan(self._h, n_nodes, s, _ptr(viol) if viol.size else None,
-                                        _ptr(labels) if labels is not None and labels.size
-                                        else None, _ptr(add), _ptr(rem), byref(total))
+                                        _ptr(ids), _ptr(labels) if labels is not None and
+                                        labels.size else None, _ptr(add), _ptr(rem),
+                                        byref(total))
         self._check(rc, "pas_tas_label_plan")
         return add, rem, total.value
 
     def tas_label_plan_device(self, n_nodes: int, n_strat: int, viol_t, labels_t, add_t, rem_t,
-                              total_t, stream=None):
+                              total_t, stream=None, names=None):
+        ids = self._name_ids(names, n_strat)
         rc = self._l.pas_tas_label_plan_device(self._h, n_nodes, n_strat, _dptr(viol_t),
-                                               _dptr(labels_t), _dptr(add_t), _dptr(rem_t),
-                                               _dptr(total_t), _stream(stream))
+                                               _ptr(ids), _dptr(labels_t), _dptr(add_t),
+                                               _dptr(rem_t), _dptr(total_t), _stream(stream))
         self._check(rc, "pas_tas_label_plan_device")
 
     def tas_deschedule_device(self, gen: int, n_strat: int, n_rules: int, rules_t, rule_off_t,
-                              viol_t, labels_t, add_t, rem_t, total_t, stream=None):
+                              viol_t, labels_t, add_t, rem_t, total_t, stream=None, names=None):
         """The sweep and its label plan in one pass (pas_tas_deschedule_device): viol_t as
         tas_violations_device, add_t / rem_t / total_t as tas_label_plan_device on it."""
+        ids = self._name_ids(names, n_strat)
         rc = self._l.pas_tas_deschedule_device(self._h, gen, n_strat, n_rules, _dptr(rules_t),
-                                               _dptr(rule_off_t), _dptr(viol_t),
+                                               _dptr(rule_off_t), _dptr(viol_t), _ptr(ids),
                                                _dptr(labels_t), _dptr(add_t), _dptr(rem_t),
                                                _dptr(total_t), _stream(stream))
         self._check(rc, "pas_tas_deschedule_device")

@@ -14,7 +14,7 @@ tests, with the same names and error behaviour.
 from __future__ import annotations
 
 import json
-from typing import Dict, Mapping, Optional, Sequence, Tuple
+from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -297,22 +297,41 @@ class GASExtender:
         return wire.binding_result(msg)
 
 
+def _strategy_equals(a: Tuple[str, list], b: Tuple[str, list]) -> bool:
+    """deschedule.Strategy.Equals (deschedule/strategy.go:60-78): same policy name and the
+    same non-empty rule list (metric, target, operator per position)."""
+    (na, ra), (nb, rb) = a, b
+    if na != nb or not ra or len(ra) != len(rb):
+        return False
+    return all(x[0] == y[0] and int(x[2]) == int(y[2]) and x[1] == y[1] for x, y in zip(ra, rb))
+
+
 class DescheduleEnforcer:
     """deschedule.Strategy.Enforce over the registered deschedule strategies
     (telemetry-aware-scheduling/pkg/strategies/deschedule/enforce.go:57-164):
     nodeStatusForStrategy (pas_tas_violations), updateNodeLabels (pas_tas_label_plan) and
     the PATCH bodies (pas_label_patch_json).
 
-    strategies: [(policy name, [(metric, op, target), ...])] in registration order."""
+    strategies: [(policy name, [(metric, op, target), ...])] in registration order.  As
+    MetricEnforcer.AddStrategy (core/enforcer.go:84-103) a strategy Equals to one already
+    registered is dropped; strategies that only share a policy name stay, and the label plan
+    keys removes and totalViolations by name (enforce.go:89-134).  More than 64 strategies
+    are planned in groups of <= 64 that keep each name's strategies together."""
+
+    MAX_PLAN = 64  # strategies per pas_tas_label_plan call
 
     def __init__(self, ctx: Context, gen: int, node_names: Sequence[str],
                  metric_names: Sequence[str], strategies: Sequence[Tuple[str, list]]):
         self.ctx, self.gen = ctx, gen
         self.node_names = list(node_names)
         self.metric_index = {m: i for i, m in enumerate(metric_names)}
-        self.names = [s[0] for s in strategies]
+        registered: List[Tuple[str, list]] = []
+        for st in strategies:
+            if not any(_strategy_equals(r, st) for r in registered):
+                registered.append(st)
+        self.names = [s[0] for s in registered]
         metric, op, target, off = [], [], [], [0]
-        for _, rules in strategies:
+        for _, rules in registered:
             for m, o, t in rules:
                 metric.append(self.metric_index.get(m, -1))
                 op.append(_op_code(o))  # unknown: skipped or the panic, as in filter
@@ -320,6 +339,18 @@ class DescheduleEnforcer:
             off.append(len(metric))
         self.rules = make_rules(metric, op, target)
         self.rule_off = np.array(off, np.int32)
+        # plan groups: whole names, first-registration order, <= 64 strategies per group
+        by_name: Dict[str, List[int]] = {}
+        for i, n in enumerate(self.names):
+            by_name.setdefault(n, []).append(i)
+        self.groups: List[List[int]] = [[]]
+        for members in by_name.values():
+            if len(members) > self.MAX_PLAN:
+                raise ValueError(f"policy name {self.names[members[0]]!r}: more than "
+                                 f"{self.MAX_PLAN} registered deschedule strategies")
+            if len(self.groups[-1]) + len(members) > self.MAX_PLAN:
+                self.groups.append([])
+            self.groups[-1].extend(members)
 
     def enforce(self, node_labels: Sequence[Mapping[str, str]]):
         """(totalViolations, {node name: PATCH body}) for the listed nodes' current labels;
@@ -334,8 +365,22 @@ class DescheduleEnforcer:
             for j, name in enumerate(self.names):
                 if name in lab:
                     labels[j, i >> 6] |= np.uint64(1 << (i & 63))
-        add, rem, total = self.ctx.tas_label_plan(n, viol, labels)
         from .context import label_patch_json
-        bodies = {self.node_names[i]: label_patch_json(self.names, int(add[i]), int(rem[i]))
+        total = 0
+        adds: List[List[bytes]] = [[] for _ in range(n)]
+        rems: List[List[bytes]] = [[] for _ in range(n)]
+        for g in self.groups:
+            if not g:
+                continue
+            names = [self.names[j] for j in g]
+            add, rem, t = self.ctx.tas_label_plan(n, viol[g], labels[g], names)
+            total += t
+            for i in range(n):
+                a, r = int(add[i]), int(rem[i])
+                if a:
+                    adds[i].append(label_patch_json(names, a, 0)[1:-1])
+                if r:
+                    rems[i].append(label_patch_json(names, 0, r)[1:-1])
+        bodies = {self.node_names[i]: b"[" + b",".join(adds[i] + rems[i]) + b"]"
                   for i in range(n)}
         return total, bodies

@@ -76,6 +76,55 @@ V["G4_deschedule_enforce"] = {
     ],
 }
 
+# G4n deschedule strategies that share a policy name (derived; no reference test covers it).
+# SetPolicyName takes ObjectMeta.Name without the namespace (controller/controller.go:80), and
+# AddStrategy drops only Equals duplicates: same name AND the same non-empty rules
+# (core/enforcer.go:84-103, deschedule/strategy.go:60-78).  So policies "p" in two namespaces
+# with different rules are two registered strategies named "p".  updateNodeLabels keys the
+# non-violated set by NAME (allPolicies, enforce.go:89-95; delete(nonViolatedPolicies, name)
+# per violating strategy, :108-109): a name is removed / counted once, and only when none of
+# its strategies is violated (:118-134); each violating strategy appends its own "add" (:110-115).
+# "strategies" lists (name, rules) in registration order; outcomes read off enforce.go:99-151.
+_ADD_P = '{"op":"add","path":"/metadata/labels/p","value":"violating"}'
+_REM_P = ('{"op":"remove","path":"/metadata/labels/p","value":""},'
+          '{"op":"add","path":"/metadata/labels/p","value":"null"}')
+V["G4n_shared_policy_name"] = {
+    "source": ["telemetry-aware-scheduling/pkg/strategies/deschedule/enforce.go:89-134",
+               "telemetry-aware-scheduling/pkg/strategies/core/enforcer.go:84-103",
+               "telemetry-aware-scheduling/pkg/controller/controller.go:80"],
+    "derived": True,
+    "metrics": {"memory": {"node-1": 100}},
+    "nodes": ["node-1"],
+    "cases": [
+        {"name": "one of two same-name strategies violating, node labelled",
+         "strategies": [["p", [["memory", "GreaterThan", 1]]],
+                        ["p", [["memory", "GreaterThan", 1000]]]],
+         "labels": {"p": "violating"},
+         "add": [0], "remove": [], "total": 0, "patch": "[" + _ADD_P + "]"},
+        {"name": "violating strategy registered second",
+         "strategies": [["p", [["memory", "GreaterThan", 1000]]],
+                        ["p", [["memory", "GreaterThan", 1]]]],
+         "labels": {"p": "null"},
+         "add": [1], "remove": [], "total": 0, "patch": "[" + _ADD_P + "]"},
+        {"name": "both same-name strategies violating: one add each",
+         "strategies": [["p", [["memory", "GreaterThan", 1]]],
+                        ["p", [["memory", "LessThan", 1000]]]],
+         "labels": {},
+         "add": [0, 1], "remove": [], "total": 0, "patch": "[" + _ADD_P + "," + _ADD_P + "]"},
+        {"name": "neither violating: one remove pair, counted once",
+         "strategies": [["p", [["memory", "GreaterThan", 1000]]],
+                        ["p", [["memory", "LessThan", 1]]]],
+         "labels": {"p": "violating"},
+         "add": [], "remove": [0], "total": 1, "patch": "[" + _REM_P + "]"},
+        {"name": "a second name, not violated and not carried, is counted",
+         "strategies": [["p", [["memory", "GreaterThan", 1]]],
+                        ["p", [["memory", "GreaterThan", 1000]]],
+                        ["q", [["memory", "Equals", 7]]]],
+         "labels": {"p": "violating"},
+         "add": [0], "remove": [], "total": 1, "patch": "[" + _ADD_P + "]"},
+    ],
+}
+
 # testPolicy1 (telemetryscheduler/scheduler_test.go:44-62)
 TEST_POLICY1 = {
     "name": "test-policy", "namespace": "default",

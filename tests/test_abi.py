@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert pas_amd.LIB.pas_abi_version() == 2
+    assert pas_amd.LIB.pas_abi_version() == 3
 
 
 @pytest.mark.parametrize("op,want", [("LessThan", 0), ("GreaterThan", 1), ("Equals", 2),

@@ -173,6 +173,102 @@ def test_deschedule_enforce_g4(ctx):
         assert [n for n in g["nodes"] if after.get(g["policy"]) == "violating"] == c["want"]
 
 
+def test_deschedule_enforce_shared_names(ctx):
+    """G4n (derived): registered strategies that share a policy name, through the Enforce
+    mirror: one remove / count per name (enforce.go:89-134)."""
+    from test_oracle_golden import apply_label_patch
+    g = G["G4n_shared_policy_name"]
+    v, pres, _ = sn.tas_snapshot_from_metrics(
+        {m: {k: str(x) for k, x in vals.items()} for m, vals in g["metrics"].items()},
+        g["nodes"], ["memory"])
+    ctx.tas_snapshot_set(8310, v, pres)
+    for c in g["cases"]:
+        e = ext.DescheduleEnforcer(ctx, 8310, g["nodes"], ["memory"],
+                                   [(nm, [tuple(r) for r in rules])
+                                    for nm, rules in c["strategies"]])
+        total, bodies = e.enforce([c["labels"]])
+        assert total == c["total"], c["name"]
+        assert bodies["node-1"].decode() == c["patch"], c["name"]
+        after = apply_label_patch(c["labels"], bodies["node-1"])
+        assert (after.get("p") == "violating") == bool(c["add"])
+
+
+def test_deschedule_enforce_registry_dedupe(ctx):
+    """AddStrategy (core/enforcer.go:84-103) drops a strategy Equals to a registered one
+    (deschedule/strategy.go:60-78: same name, same non-empty rules); same name with other
+    rules, or empty rules, stays."""
+    names = ["node A", "node B"]
+    v, pres, _ = sn.tas_snapshot_from_metrics({"m": {"node A": "50", "node B": "30"}}, names,
+                                              ["m"])
+    ctx.tas_snapshot_set(8320, v, pres)
+    r1 = [("m", "GreaterThan", 40)]
+    e = ext.DescheduleEnforcer(ctx, 8320, names, ["m"],
+                               [("p", r1), ("p", list(r1)), ("p", [("m", "GreaterThan", 41)]),
+                                ("q", []), ("q", [])])
+    assert e.names == ["p", "p", "q", "q"]
+    total, bodies = e.enforce([{}, {"p": "violating"}])
+    # node A: p violated (twice: r1 and GreaterThan 41), q not -> 1; node B: p, q not -> 2
+    assert total == 3
+    assert json.loads(bodies["node A"]) == [
+        {"op": "add", "path": "/metadata/labels/p", "value": "violating"}] * 2
+    assert json.loads(bodies["node B"]) == [
+        {"op": "remove", "path": "/metadata/labels/p", "value": ""},
+        {"op": "add", "path": "/metadata/labels/p", "value": "null"}]
+
+
+def _update_node_labels(names, viol_bits, node_labels):
+    """updateNodeLabels (enforce.go:99-151) literally: per node, allPolicies by name, delete
+    per violating strategy, remove + null / count per remaining name.  Returns (total,
+    [sorted ops per node])."""
+    total, out = 0, []
+    for i, lab in enumerate(node_labels):
+        non_violated = dict.fromkeys(names)
+        ops = []
+        for j, nm in enumerate(names):
+            if viol_bits[j, i]:
+                non_violated.pop(nm, None)
+                ops.append(("add", nm, "violating"))
+        for nm in non_violated:
+            if nm in lab:
+                ops += [("remove", nm, ""), ("add", nm, "null")]
+            total += 1
+        out.append(sorted(ops))
+    return total, out
+
+
+def test_deschedule_enforce_more_than_64_strategies(ctx, oracle):
+    """150 strategies under 40 policy names: planned in groups of <= 64 whole names; the
+    total and every node's set of operations equal the literal restatement."""
+    from helpers import unpack_bits
+    rng = np.random.default_rng(21)
+    n_nodes, metrics = 300, ["m0", "m1", "m2"]
+    nodes = [f"node-{i}" for i in range(n_nodes)]
+    vals = {m: {nd: str(int(rng.integers(0, 100))) for nd in nodes if rng.random() > 0.05}
+            for m in metrics}
+    v, pres, _ = sn.tas_snapshot_from_metrics(vals, nodes, metrics)
+    ctx.tas_snapshot_set(8330, v, pres)
+    strategies = []
+    for j in range(150):
+        rules = [(metrics[int(rng.integers(0, 3))], ["LessThan", "GreaterThan", "Equals"][
+            int(rng.integers(0, 3))], int(rng.integers(0, 100))) for _ in range(2)]
+        strategies.append((f"pol-{int(rng.integers(0, 40))}", rules))
+    e = ext.DescheduleEnforcer(ctx, 8330, nodes, metrics, strategies)
+    assert len(e.groups) >= 3 and all(len(g) <= 64 for g in e.groups)
+    for g in e.groups:  # whole names per group
+        assert not ({e.names[j] for j in g} & {e.names[j] for h in e.groups if h is not g
+                                                 for j in h})
+    node_labels = [{nm: "violating" for nm in set(e.names) if rng.random() < 0.3}
+                   for _ in nodes]
+    total, bodies = e.enforce(node_labels)
+    viol = oracle.tas_violations(v, pres, e.rules, e.rule_off)
+    want_total, want_ops = _update_node_labels(e.names, unpack_bits(viol, n_nodes), node_labels)
+    assert total == want_total
+    for i, nd in enumerate(nodes):
+        got = sorted((o["op"], o["path"][len("/metadata/labels/"):], o["value"])
+                     for o in json.loads(bodies[nd]))
+        assert got == want_ops[i], nd
+
+
 def test_gas_filter_unknown_kind(ctx):
     # a request for a gpu.intel.com/ kind no node has (scheduler.go:206-215, 349-354): with
     # an i915 in the same container every node fails; without one it fits with no cards

@@ -163,7 +163,7 @@ def test_label_plan_device_after_sweep(ctx, oracle):
     assert torch.equal(f_rem_t, rem_t) and torch.equal(f_total_t, total_t)
 
 
-def _fused_and_separate(ctx, gen, n, s, rules, off, labels):
+def _fused_and_separate(ctx, gen, n, s, rules, off, labels, names=None):
     """pas_tas_deschedule_device and the sweep + plan pair on the same resident inputs."""
     import torch
     dev = torch.device("cuda", 0)
@@ -179,10 +179,10 @@ def _fused_and_separate(ctx, gen, n, s, rules, off, labels):
         total_t = torch.full((1,), -7, dtype=torch.int64, device=dev)
         if name == "fused":
             ctx.tas_deschedule_device(gen, s, len(rules), rules_t, off_t, viol_t, labels_t, add_t,
-                                      rem_t, total_t)
+                                      rem_t, total_t, names=names)
         else:
             ctx.tas_violations_device(gen, s, len(rules), rules_t, off_t, viol_t)
-            ctx.tas_label_plan_device(n, s, viol_t, labels_t, add_t, rem_t, total_t)
+            ctx.tas_label_plan_device(n, s, viol_t, labels_t, add_t, rem_t, total_t, names=names)
         torch.cuda.synchronize()
         out[name] = (viol_t.cpu().numpy().view(np.uint64)[:s, :w],
                      add_t.cpu().numpy().view(np.uint64)[:n],
@@ -248,3 +248,118 @@ def test_label_plan_errors(ctx):
     with pytest.raises(pas_amd.PasError) as e:
         ctx.tas_label_plan(10, np.zeros((65, 1), np.uint64))
     assert e.value.code == pas_amd._lib.PAS_EINVAL
+
+
+# ---------------------------------------------------------------- shared policy names (GPU)
+# updateNodeLabels keys its non-violated set by policy NAME (enforce.go:89-134): a name is
+# removed / counted once, and only when none of its strategies is violated.
+
+def random_shared_names(rng, s, pool):
+    """s policy names drawn from `pool` distinct ones (repeats likely)."""
+    return [f"pol-{int(i)}" for i in rng.integers(0, pool, size=s)]
+
+
+def name_labels(rng, names, n, density=0.5):
+    """Labels rows [S][W64] that agree within a name (the label is the node's)."""
+    uniq = sorted(set(names))
+    rows = {u: wl.pack_bits(rng.random((1, n)) < density)[0] for u in uniq}
+    return np.stack([rows[x] for x in names]) if names else np.zeros((0, (n + 63) // 64),
+                                                                      np.uint64)
+
+
+@pytest.mark.gpu
+def test_label_plan_golden_g4n(ctx, oracle):
+    """The derived G4n cases through the GPU sweep and both plan paths (two calls, fused)."""
+    from helpers import NamedSnapshot
+    from test_oracle_golden import g4n_inputs
+    g = G["G4n_shared_policy_name"]
+    snap = NamedSnapshot(g["metrics"], g["nodes"])
+    for gen, c in enumerate(g["cases"], start=7400):
+        ctx.tas_snapshot_set(gen, snap.v_milli, snap.present)
+        names, rules, off, viol_o, labels = g4n_inputs(oracle, c, snap, g["nodes"])
+        viol = ctx.tas_violations(gen, rules, off)
+        np.testing.assert_array_equal(viol, viol_o)
+        add, rem, total = ctx.tas_label_plan(1, viol, labels, names)
+        bits = lambda m: [j for j in range(len(names)) if int(m) >> j & 1]  # noqa: E731
+        assert bits(add[0]) == c["add"] and bits(rem[0]) == c["remove"], c["name"]
+        assert total == c["total"], c["name"]
+        assert pas_amd.label_patch_json(names, int(add[0]), int(rem[0])).decode() == c["patch"]
+        f, sep = _fused_and_separate(ctx, gen, 1, len(names), rules, off, labels, names)
+        assert (int(f[1][0]), int(f[2][0]), f[3]) == (int(add[0]), int(rem[0]), total), c["name"]
+        assert (int(sep[1][0]), int(sep[2][0]), sep[3]) == (int(add[0]), int(rem[0]), total)
+
+
+@pytest.mark.gpu
+def test_label_plan_shared_names_parity(ctx, oracle):
+    """Random plans with repeated names (and rows of non-first strategies that disagree with
+    their name's first row: only the first is read) equal the oracle's name-keyed plan."""
+    rng = np.random.default_rng(15)
+    for n in (1, 63, 64, 65, 1000, 4097):
+        for s in (2, 5, 16, 33, 64):
+            for pool in (1, 3, max(s // 2, 1)):
+                names = random_shared_names(rng, s, pool)
+                viol, _ = _plan_case(rng, n, s, density=0.05)
+                labels = name_labels(rng, names, n)
+                noisy = labels.copy()
+                noisy[1:] ^= wl.pack_bits(rng.random((s - 1, n)) < 0.3)
+                for lab in (labels, noisy, None):
+                    got = ctx.tas_label_plan(n, viol, lab, names)
+                    want = oracle.label_plan(viol, lab, n, names)
+                    np.testing.assert_array_equal(got[0], want[0], err_msg=f"add {n} {s} {pool}")
+                    np.testing.assert_array_equal(got[1], want[1], err_msg=f"rem {n} {s} {pool}")
+                    assert got[2] == want[2], (n, s, pool)
+                # distinct names given explicitly = names omitted
+                uniq = [f"u{j}" for j in range(s)]
+                a = ctx.tas_label_plan(n, viol, labels, uniq)
+                b = ctx.tas_label_plan(n, viol, labels)
+                assert all(np.array_equal(x, y) for x, y in zip(a[:2], b[:2])) and a[2] == b[2]
+
+
+@pytest.mark.gpu
+def test_deschedule_fused_shared_names_parity(ctx, oracle):
+    rng = np.random.default_rng(16)
+    gen = 7500
+    for n in (65, 513, 70_001):
+        snap = wl.make_tas_snapshot(n, 8, seed=n + 1)
+        ctx.tas_snapshot_set(gen, snap.v_milli, snap.present)
+        for s, pool in ((2, 1), (16, 4), (64, 9)):
+            rules, off = wl.make_deschedule_rules(snap, s, 2, seed=n + s + 1)
+            names = random_shared_names(rng, s, pool)
+            want_v = oracle.tas_violations(snap.v_milli, snap.present, rules, off)
+            labels = name_labels(rng, names, n, 0.4)
+            for lab in (labels, None):
+                f, sep = _fused_and_separate(ctx, gen, n, s, rules, off, lab, names)
+                want = oracle.label_plan(want_v, lab, n, names)
+                np.testing.assert_array_equal(f[0], want_v)
+                for i, what in ((1, "add"), (2, "rem")):
+                    np.testing.assert_array_equal(f[i], want[i - 1], err_msg=f"{what} {n} {s}")
+                    np.testing.assert_array_equal(sep[i], want[i - 1], err_msg=f"{what} {n} {s}")
+                assert f[3] == want[2] == sep[3], (n, s)
+        gen += 1
+
+
+@pytest.mark.gpu
+def test_deschedule_shared_names_1m(ctx, oracle):
+    """C4 shape (1M nodes x 16 strategies x 4 rules) with the 16 strategies under 5 policy
+    names: fused and two-call plans equal the oracle; totals obey the per-name identity."""
+    n, s = 1_000_000, 16
+    snap = wl.make_tas_snapshot(n, 64, seed=0xC4)
+    rules, off = wl.make_deschedule_rules(snap, s, 4, seed=0xC4)
+    gen = 7600
+    ctx.tas_snapshot_set(gen, snap.v_milli, snap.present)
+    rng = np.random.default_rng(17)
+    names = [f"pol-{j % 5}" for j in range(s)]
+    labels = name_labels(rng, names, n, 0.1)
+    f, sep = _fused_and_separate(ctx, gen, n, s, rules, off, labels, names)
+    want_v = oracle.tas_violations(snap.v_milli, snap.present, rules, off)
+    np.testing.assert_array_equal(f[0], want_v)
+    want = oracle.label_plan(want_v, labels, n, names)
+    for i in (1, 2):
+        np.testing.assert_array_equal(f[i], want[i - 1])
+        np.testing.assert_array_equal(sep[i], want[i - 1])
+    assert f[3] == sep[3] == want[2]
+    # size-independent: total = sum over names of nodes where no strategy of the name violates
+    bits = unpack_bits(want_v, n)
+    expect = sum(int((~bits[[j for j in range(s) if names[j] == u]].any(axis=0)).sum())
+                 for u in set(names))
+    assert want[2] == expect

@@ -105,6 +105,42 @@ def test_g4_deschedule_enforce(oracle):
         assert got == c["want"], c["name"]
 
 
+def g4n_inputs(oracle, case, snap, nodes):
+    """(names, viol [S][W64], labels [S][W64]) of one G4n case: every strategy's labels row
+    says whether the node carries the label of the strategy's policy name."""
+    names = [s[0] for s in case["strategies"]]
+    rules, off = [], [0]
+    for _, named in case["strategies"]:
+        rules.extend(snap.rules(named).tolist())
+        off.append(len(rules))
+    rules = np.array(rules, dtype=snap.rules([]).dtype)
+    off = np.array(off, np.int32)
+    viol = oracle.tas_violations(snap.v_milli, snap.present, rules, off)
+    labels = np.zeros_like(viol)
+    for j, name in enumerate(names):
+        for i in range(len(nodes)):
+            if name in case["labels"]:
+                labels[j, i >> 6] |= np.uint64(1 << (i & 63))
+    return names, rules, off, viol, labels
+
+
+def test_g4n_shared_policy_name(oracle):
+    """Strategies that share a policy name: remove / null and totalViolations per distinct
+    name (enforce.go:89-134), one add per violating strategy (:108-117)."""
+    g = G["G4n_shared_policy_name"]
+    snap = NamedSnapshot(g["metrics"], g["nodes"])
+    for c in g["cases"]:
+        names, _, _, viol, labels = g4n_inputs(oracle, c, snap, g["nodes"])
+        add, rem, total = oracle.label_plan(viol, labels, len(g["nodes"]), names)
+        bits = lambda m: [s for s in range(len(names)) if int(m) >> s & 1]  # noqa: E731
+        assert bits(add[0]) == c["add"] and bits(rem[0]) == c["remove"], c["name"]
+        assert total == c["total"], c["name"]
+        assert oracle.label_patch_json(names, add[0], rem[0]).decode() == c["patch"], c["name"]
+        # the label ends "violating" exactly when some strategy of the name is violated
+        after = apply_label_patch(c["labels"], oracle.label_patch_json(names, add[0], rem[0]))
+        assert (after.get("p") == "violating") == bool(c["add"]), c["name"]
+
+
 def _filter(oracle, snap, named_rules, nodes):
     rules = snap.rules(named_rules)
     off = np.array([0, len(rules)], np.int32)
