@@ -90,6 +90,11 @@ int pas_set_stream(pas_ctx* ctx, void* hip_stream); /* NULL = the context's own 
  * (snapshot_set, snapshot_update, gas_bind, gas_release) must be ordered by the caller after
  * the calls on other streams that still read it. */
 #define PAS_STREAM_NULL ((void*)1)
+/* Waits for the context's stream and for the last calls on every other stream the context
+ * ran on (and the GAS fits' internal side streams).  Returns PAS_EDEVICE when a GAS fit
+ * enqueued since the last report could not complete: one of its internal stream waits gave
+ * up (pas_gas_fit_device: its outputs are not to be used); the report is cleared, so the
+ * next call starts clean.  The host-pointer GAS forms report this themselves. */
 int pas_synchronize(pas_ctx* ctx);
 
 /* Operator string -> pas_op ("LessThan", "GreaterThan", "Equals"), else PAS_EINVAL.

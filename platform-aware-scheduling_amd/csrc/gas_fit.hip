@@ -72,12 +72,6 @@ constexpr int kSingleTpb = PAS_GAS_SINGLE_TPB;
 #ifndef PAS_GAS_SEQ_FIRST
 #define PAS_GAS_SEQ_FIRST 0  // 1: the sequential kernel before the closed-form one (diagnostic)
 #endif
-#ifndef PAS_GAS_CONCURRENT
-// 1: multi-selection kernels on a side stream; 2: the single-selection one; 3: the single- and
-// the sequential-selection kernels each on a side stream of their own, the closed-form one on
-// the caller's (same-box C3 A/B: 2 -> 3, 0.733-0.737 -> 0.719-0.725 ms)
-#define PAS_GAS_CONCURRENT 3
-#endif
 #ifndef PAS_GAS_BLOCKS_SINGLE
 #define PAS_GAS_BLOCKS_SINGLE 8192  // target blocks of a fit grid: (node block, pod chunk) pairs
 #endif
@@ -243,6 +237,12 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
 // and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
 // go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
 // PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
+// A fit kernel whose fork wait gave up returns at entry: its prep lists may be unwritten (the
+// call reports PAS_EDEVICE, gas_fault_check).
+__device__ __forceinline__ bool fit_aborted(const uint32_t* abort, uint32_t epoch) {
+  return abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
+}
+
 struct PrepArgs {
   int32_t n_pods, max_containers, n_res, i915;
   const int64_t* req;
@@ -260,6 +260,8 @@ struct PrepArgs {
   int32_t n_counts;
   int64_t* limit_count;
   int64_t* side_count;
+  uint32_t* start;  // device flags: set to the fit's epoch when the prep starts (null: events)
+  uint32_t epoch;
 };
 
 // Block 0 of the prep zeroes the next fit's counts and this fit's generic-kernel counters
@@ -468,6 +470,8 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
 // One thread per pod.
 __global__ __launch_bounds__(kPrepTpb) void gas_prep_kernel(PrepArgs a) {
   if (blockIdx.x == 0) prep_zero<kPrepTpb>(a);
+  if (a.start && blockIdx.x == 0 && threadIdx.x == 0)  // the side streams' waits start timing
+    __hip_atomic_store(a.start, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   prep_pod(a, blockIdx.x * kPrepTpb + threadIdx.x);
 }
 
@@ -561,7 +565,10 @@ typedef unsigned long long lane_mask;  // one bit per lane of the wave (ballot)
 struct ResOut {
   uint32_t* w;
   int64_t ld;
+  const uint32_t* abort;  // device flags: a wait of this fit timed out if *abort == epoch
+  uint32_t epoch;
 };
+
 template <bool kBits>
 __device__ __forceinline__ void put_result(ResOut res, uint64_t* __restrict__ fit, int64_t p,
                                            int32_t N, int32_t n, bool valid, uint32_t out) {
@@ -1629,6 +1636,7 @@ __global__ __launch_bounds__(kSingleTpb) void gas_rfit_single_kernel(
     const int32_t* __restrict__ counts, int32_t chunks, ResOut res,
     uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kSingleTpb / 64][SingleLds<Q>::kBytes / 16];  // a slice per wave
+  if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_single_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
                              n_cards, free_t, rs, srt, counts, res, fit);
@@ -1836,6 +1844,7 @@ __global__ __launch_bounds__(kClosedTpb) __attribute__((amdgpu_waves_per_eu(clos
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ counts, int32_t chunks, ResOut res, uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kClosedTpb / 64][MultiLds<Q>::kRanked / 16];
+  if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_closed_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
                              n_cards, free_t, rm, rw, srt, counts, res, fit);
@@ -1872,6 +1881,7 @@ __global__ __launch_bounds__(kSeqTpb) void gas_rfit_seq_kernel(
     const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
     ResOut res, uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kSeqTpb / 64][MultiLds<Q>::kSeq / 16];
+  if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P, n_cards,
                           free_t, rq, srt, multi, sels, counts, res, fit);
@@ -1910,6 +1920,8 @@ struct GenericArgs {
   int64_t side_cap;
   unsigned long long* side_count;
   unsigned long long* limit_count;
+  const uint32_t* abort;  // as ResOut
+  uint32_t epoch;
 };
 
 __device__ __forceinline__ bool kind_fits(int64_t need, int64_t cap, int64_t used) {
@@ -2003,6 +2015,7 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
 
 template <int KMAX>
 __global__ __launch_bounds__(64) void gas_fit_generic_kernel(GenericArgs a) {
+  if (fit_aborted(a.abort, a.epoch)) return;
   const int64_t nbp = *a.n_big_pods, nbn = *a.n_big_nodes;
   const int64_t seg_a = nbp * a.N, total = seg_a + (int64_t)a.n_pods * nbn;
   for (int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x; i < total;
@@ -2026,22 +2039,55 @@ __global__ __launch_bounds__(64) void gas_fit_generic_kernel(GenericArgs a) {
 // Device-side fork / join of the fit's streams (PAS_GAS_SPIN_SYNC): a one-thread kernel
 // sets a flag to the fit's epoch after the work before it on its stream; another waits on
 // flags before the work after it on its stream.  Host order is the deadlock guard: every
-// wait is enqueued after the signal it waits for, so streams that share a hardware queue
-// still reach the signal first.  A wait gives up after ~2 s of the 100 MHz clock (a signal
-// that never comes is an enqueue failure the host already reported) rather than hang.
+// wait is enqueued after the signal it waits for (so is every event wait), so streams that
+// share a hardware queue still reach the signal first.  A wait gives up rather than hang: a
+// fork wait first waits for the fit's prep to start on the caller's stream (start; up to
+// limit_start, the caller's earlier work on that stream), then for the prep's signal (up to
+// limit); the join wait for the side streams' signals (limit).  A wait that gives up aborts
+// the fit (its fit kernels return at entry, fit_aborted) and sets the context's fault word,
+// which the call's synchronization reports as PAS_EDEVICE (gas_fault_check).  force: a
+// debug-forced timeout (PAS_GAS_FORCE_TIMEOUT).
 __global__ __launch_bounds__(64) void gas_signal_kernel(uint32_t* flag, uint32_t epoch) {
   if (threadIdx.x == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
-__global__ __launch_bounds__(64) void gas_wait_kernel(const uint32_t* flags, int32_t n,
-                                                      uint32_t epoch, uint64_t limit,
-                                                      uint32_t* fault) {
+struct WaitArgs {
+  const uint32_t* flags;  // [n]
+  int32_t n;
+  const uint32_t* start;  // fork waits: the prep-started flag, else null
+  uint32_t epoch;
+  uint64_t limit, limit_start;  // 100 MHz ticks
+  uint32_t* abort;
+  uint32_t* fault;  // host-pinned
+  int32_t force;
+};
+__global__ __launch_bounds__(64) void gas_wait_kernel(WaitArgs a) {
   if (threadIdx.x != 0) return;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (int32_t i = 0; i < n; ++i)
-    while ((int32_t)(__hip_atomic_load(flags + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                     epoch) < 0) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {  // reported by the next call
-        __hip_atomic_store(fault, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  auto give_up = [&]() {
+    __hip_atomic_store(a.abort, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.fault, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  };
+  if (a.force) {
+    give_up();
+    return;
+  }
+  auto reached = [&](const uint32_t* f) {
+    return (int32_t)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.epoch) >=
+           0;
+  };
+  uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  if (a.start)
+    while (!reached(a.start)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.limit_start) {
+        give_up();
+        return;
+      }
+      __builtin_amdgcn_s_sleep(8);
+    }
+  t0 = __builtin_amdgcn_s_memrealtime();
+  for (int32_t i = 0; i < a.n; ++i)
+    while (!reached(a.flags + i)) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > a.limit) {
+        give_up();
         return;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -2066,6 +2112,20 @@ int gas_sync_mode() {
 }
 
 }  // namespace
+
+int gas_fault_check(pas_ctx* ctx) {
+  if (!ctx->gas_sync_fault || !__atomic_load_n(ctx->gas_sync_fault, __ATOMIC_ACQUIRE))
+    return PAS_OK;
+  // the fit kernels of a fit whose join gave up may still be running on its side streams
+  for (AuxSlot& a : ctx->aux_slot) {
+    if (a.side) (void)hipStreamSynchronize(a.side);
+    if (a.side2) (void)hipStreamSynchronize(a.side2);
+  }
+  __atomic_store_n(ctx->gas_sync_fault, 0u, __ATOMIC_RELEASE);
+  return set_error(ctx, PAS_EDEVICE,
+                   "pas_gas_fit: a side-stream wait of a fit timed out, so that fit's results "
+                   "are incomplete (set PAS_GAS_SYNC=events under kernel-serializing tools)");
+}
 
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
@@ -2162,6 +2222,59 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   unsigned long long* gflip = static_cast<unsigned long long*>(g.derived);
   int32_t* n_big_nodes = reinterpret_cast<int32_t*>(gflip + PAS_GAS_MAX_RES);
   int32_t* big_nodes = reinterpret_cast<int32_t*>(static_cast<char*>(g.derived) + 64);
+  // The fit forks two side streams of its slot after its prep launches (the one-selection
+  // and generic kernels on one, the sequential kernel on the other; the closed-form kernel
+  // stays on s) and joins them at the end.  Fork / join: device flags (per slot, set to the
+  // slot's fit epoch), else events (gas_sync_mode).
+  if (ctx->gas_sync_mode < 0) {
+    ctx->gas_sync_mode = gas_sync_mode();
+    if (ctx->gas_sync_mode) {
+      PAS_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->gas_sync_fault), sizeof(uint32_t),
+                                 hipHostMallocCoherent));
+      *ctx->gas_sync_fault = 0;
+      if (const char* f = std::getenv("PAS_GAS_FORCE_TIMEOUT"))
+        ctx->gas_force_timeouts = std::atoi(f);
+    }
+  }
+  // a wait of an earlier fit that gave up and was not reported by a synchronization yet
+  if (int e = gas_fault_check(ctx)) return e;
+  // side streams and events exist before the fork, and every exit after the fork joins them
+  // (Joins), so a later user of the slot never waits on an event that does not cover
+  // side-stream work
+  if (!slot->side) {
+    PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side, hipStreamNonBlocking));
+    PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side2, hipStreamNonBlocking));
+    PAS_HIP(ctx, hipEventCreateWithFlags(&slot->fork, hipEventDisableTiming));
+    PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join, hipEventDisableTiming));
+    PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join2, hipEventDisableTiming));
+  }
+  hipStream_t const ss = slot->side, qs = slot->side2;
+  const bool kFlags = ctx->gas_sync_mode == 1;
+  // limits (100 MHz ticks): a side-stream wait for the prep to START, up to 30 s (it may sit
+  // behind the caller's earlier work on s); then for the prep's signal, and the join's wait
+  // for the side streams, 1 s plus 1 ns per (pod, node) pair, far past any fit
+  const uint64_t limit = 100000000ull + (uint64_t)n_pods * (uint64_t)N / 10u;
+  const uint64_t limit_start = 3000000000ull;
+  uint32_t* sync = nullptr;  // [prep done, side done, side2 done, abort, prep started]
+  uint32_t epoch = 0;
+  if (kFlags) {
+    if (!slot->gas_sync) {
+      uint32_t* f = nullptr;
+      PAS_HIP(ctx, hipMalloc(&f, 8 * sizeof(uint32_t)));
+      // zero before any side stream can read them (once per slot)
+      if (hipMemsetAsync(f, 0, 8 * sizeof(uint32_t), s) != hipSuccess ||
+          hipStreamSynchronize(s) != hipSuccess) {
+        (void)hipFree(f);
+        return set_error(ctx, PAS_EDEVICE, "pas_gas_fit: sync flags init failed");
+      }
+      slot->gas_sync = f;
+      slot->gas_epoch = 0;
+    }
+    sync = slot->gas_sync;
+    epoch = ++slot->gas_epoch;
+    if (epoch == 0) epoch = ++slot->gas_epoch;  // flags start at 0: never wait for epoch 0
+  }
+  uint32_t* const abort_flag = kFlags ? sync + 3 : nullptr;
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_GAS_PREP, &tl);
   if (ctx->gas.derived_epoch != ctx->gas.epoch) {
@@ -2177,7 +2290,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   }
   const PrepArgs pa{n_pods, max_containers, Q, i915_index, d_req, d_req_mask, d_n_containers,
                     gflip, single, multi, sels, counts, big_pods, n_big_pods, pod_steps,
-                    counts_next, kCounts, slot->gas_limit, d_side_count};
+                    counts_next, kCounts, slot->gas_limit, d_side_count,
+                    kFlags ? sync + 4 : nullptr, epoch};
   const RankArgs ra{n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword,
                     rseq};
   gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(pa);
@@ -2224,6 +2338,9 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   ga.side_cap = d_side ? side_cap : 0;
   ga.side_count = reinterpret_cast<unsigned long long*>(d_side_count);
   ga.limit_count = reinterpret_cast<unsigned long long*>(slot->gas_limit);
+  ga.abort = abort_flag;
+  ga.epoch = epoch;
+  const ResOut ro{d_res, ld_res, abort_flag, epoch};
   auto generic = [&](hipStream_t st) {
     constexpr int kGenericBlocks = 512;
     if (K <= 8)
@@ -2233,126 +2350,64 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     else
       gas_fit_generic_kernel<PAS_GAS_MAX_CARDS><<<kGenericBlocks, 64, 0, st>>>(ga);
   };
-  // streams of the single-selection (ss), closed-form (ms) and sequential (qs) kernels:
-  // disjoint pods, disjoint result rows; the side streams are forked from s here and joined
-  // at the end.  They and their events exist before the fork is recorded, and every exit after
-  // the fork joins them (Joins), so a later user of the slot never waits on an event that
-  // does not cover side-stream work.
-  if (PAS_GAS_CONCURRENT) {
-    if (!slot->side) {
-      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side, hipStreamNonBlocking));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->fork, hipEventDisableTiming));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join, hipEventDisableTiming));
-    }
-    if (PAS_GAS_CONCURRENT == 3 && !slot->side2) {
-      PAS_HIP(ctx, hipStreamCreateWithFlags(&slot->side2, hipStreamNonBlocking));
-      PAS_HIP(ctx, hipEventCreateWithFlags(&slot->join2, hipEventDisableTiming));
-    }
-  }
   struct Joins {
     AuxSlot* a;
     hipStream_t s;
-    int forked = 0;  // side streams forked and not yet joined
+    bool forked = false;  // side streams forked and not yet joined
     hipError_t join() {
-      hipError_t e = hipSuccess;
-      if (forked >= 1 && e == hipSuccess) e = hipEventRecord(a->join, a->side);
-      if (forked >= 1 && e == hipSuccess) e = hipStreamWaitEvent(s, a->join, 0);
-      if (forked >= 2 && e == hipSuccess) e = hipEventRecord(a->join2, a->side2);
-      if (forked >= 2 && e == hipSuccess) e = hipStreamWaitEvent(s, a->join2, 0);
-      forked = 0;
+      hipError_t e = hipEventRecord(a->join, a->side);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, a->join, 0);
+      if (e == hipSuccess) e = hipEventRecord(a->join2, a->side2);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, a->join2, 0);
+      forked = false;
       return e;
     }
     ~Joins() {
       if (forked) (void)join();  // an error exit: runs before ReleaseOnExit records the slot
     }
   } joins{slot, s};
-  // the fork: with PAS_GAS_SPIN_SYNC the side streams start with a wait kernel on the prep's
-  // flag (set by a signal kernel on s after the rank prep); else they wait on an event
-  if (ctx->gas_sync_mode < 0) {
-    ctx->gas_sync_mode = gas_sync_mode();
-    if (ctx->gas_sync_mode) {
-      PAS_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->gas_sync_fault), sizeof(uint32_t),
-                                 hipHostMallocCoherent));
-      *ctx->gas_sync_fault = 0;
+  // the fork, after the rank prep: flags — a signal kernel on s, a wait kernel at the head of
+  // each side stream (enqueued after the signal); else events
+  if (kFlags) {
+    int32_t force = 0;  // PAS_GAS_FORCE_TIMEOUT: the side streams' waits give up at once
+    if (ctx->gas_force_timeouts > 0) {
+      force = 1;
+      --ctx->gas_force_timeouts;
     }
-  }
-  const bool kSpin = ctx->gas_sync_mode == 1 && PAS_GAS_CONCURRENT == 3;
-  // a wait that gave up (its signal never came within the limit): the fit it joined may have
-  // returned before its side streams finished, so this call fails and says so
-  if (kSpin && __atomic_load_n(ctx->gas_sync_fault, __ATOMIC_ACQUIRE)) {
-    *ctx->gas_sync_fault = 0;
-    return set_error(ctx, PAS_EDEVICE,
-                     "pas_gas_fit: a side-stream wait of an earlier fit timed out (its results "
-                     "may be incomplete); set PAS_GAS_SYNC=events under kernel-serializing tools");
-  }
-  // the waits' limit: 1 s plus 10 ns per (pod, node) pair, far past any real fit
-  const uint64_t limit = 100000000ull + (uint64_t)n_pods * (uint64_t)N / 100u;
-  uint32_t* sync = nullptr;
-  uint32_t epoch = 0;
-  if (kSpin) {
-    if (!slot->gas_sync) {
-      uint32_t* f = nullptr;
-      PAS_HIP(ctx, hipMalloc(&f, 4 * sizeof(uint32_t)));
-      // zero before any side stream can read them (once per slot)
-      if (hipMemsetAsync(f, 0, 4 * sizeof(uint32_t), s) != hipSuccess ||
-          hipStreamSynchronize(s) != hipSuccess) {
-        (void)hipFree(f);
-        return set_error(ctx, PAS_EDEVICE, "pas_gas_fit: sync flags init failed");
-      }
-      slot->gas_sync = f;
-      slot->gas_epoch = 0;
-    }
-    sync = slot->gas_sync;
-    epoch = ++slot->gas_epoch;
-    if (epoch == 0) epoch = ++slot->gas_epoch;  // flags start at 0: never wait for epoch 0
     gas_signal_kernel<<<1, 64, 0, s>>>(sync, epoch);
+    const WaitArgs fw{sync, 1, sync + 4, epoch, limit, limit_start, abort_flag,
+                      ctx->gas_sync_fault, force};
+    gas_wait_kernel<<<1, 64, 0, ss>>>(fw);
+    gas_wait_kernel<<<1, 64, 0, qs>>>(fw);
+  } else {
+    PAS_HIP(ctx, hipEventRecord(slot->fork, s));
+    PAS_HIP(ctx, hipStreamWaitEvent(ss, slot->fork, 0));
+    PAS_HIP(ctx, hipStreamWaitEvent(qs, slot->fork, 0));
   }
-  hipStream_t ss = s, ms = s, qs = s;
-  if (PAS_GAS_CONCURRENT) {
-    if (kSpin) {
-      gas_wait_kernel<<<1, 64, 0, slot->side>>>(sync, 1, epoch, limit, ctx->gas_sync_fault);
-      gas_wait_kernel<<<1, 64, 0, slot->side2>>>(sync, 1, epoch, limit, ctx->gas_sync_fault);
-      PAS_HIP(ctx, hipGetLastError());
-      joins.forked = 2;
-    } else {
-      PAS_HIP(ctx, hipEventRecord(slot->fork, s));
-      PAS_HIP(ctx, hipStreamWaitEvent(slot->side, slot->fork, 0));
-      joins.forked = 1;
-      if (PAS_GAS_CONCURRENT == 3) {
-        PAS_HIP(ctx, hipStreamWaitEvent(slot->side2, slot->fork, 0));
-        joins.forked = 2;
-      }
-    }
-    (PAS_GAS_CONCURRENT == 1 ? ms : ss) = slot->side;
-    qs = ms;
-    if (PAS_GAS_CONCURRENT == 3) qs = slot->side2;
-  }
-  // word results: the generic kernel writes its (pod, node) words alone (the fast kernels
-  // skip pods past 8 selections and nodes past 8 cards), so it runs beside them, after the
-  // single-selection kernel on that stream; bitmap rows are or-ed into the fast kernels'
-  // words, so it runs after the join
+  joins.forked = true;
+  PAS_HIP(ctx, hipGetLastError());
+  // streams of the single-selection (ss), closed-form (s) and sequential (qs) kernels:
+  // disjoint pods, disjoint result rows.  Word results: the generic kernel writes its (pod,
+  // node) words alone (the fast kernels skip pods past 8 selections and nodes past 8 cards),
+  // so it runs beside them, after the single-selection kernel on ss; bitmap rows are or-ed
+  // into the fast kernels' words, so it runs after the join
   switch (Q * 2 + (bits ? 1 : 0)) {
 #define PAS_GAS_CASE(QQ, B)                                                                    \
   case QQ * 2 + B:                                                                             \
-    if (PAS_GAS_CONCURRENT != 2 && PAS_GAS_CONCURRENT != 3)                                    \
-      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                       \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
-          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
     if (PAS_GAS_SEQ_FIRST)                                                                     \
       gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                     \
-    gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, ms>>>(                         \
+          counts + NL, ch_q, ro, d_fit);                                                        \
+    gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, s>>>(                          \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
-        counts + NL, ch_c, ResOut{d_res, ld_res}, d_fit);                                       \
+        counts + NL, ch_c, ro, d_fit);                                                          \
     if (!PAS_GAS_SEQ_FIRST)                                                                    \
       gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_q, ResOut{d_res, ld_res}, d_fit);                                     \
-    if (PAS_GAS_CONCURRENT == 2 || PAS_GAS_CONCURRENT == 3)                                    \
-      gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                       \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,     \
-          ch_s, ResOut{d_res, ld_res}, d_fit);                                                  \
+          counts + NL, ch_q, ro, d_fit);                                                        \
+    gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                         \
+        N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,       \
+        ch_s, ro, d_fit);                                                                       \
     break;
     PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
     PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
@@ -2360,14 +2415,15 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
     default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   }
   if (!bits) generic(ss);
-  if (kSpin) {
+  if (kFlags) {
     // the join: each side stream sets its flag after its work; s waits for both (enqueued
     // after the signals)
     gas_signal_kernel<<<1, 64, 0, ss>>>(sync + 1, epoch);
-    gas_signal_kernel<<<1, 64, 0, slot->side2>>>(sync + 2, epoch);
-    gas_wait_kernel<<<1, 64, 0, s>>>(sync + 1, 2, epoch, limit, ctx->gas_sync_fault);
+    gas_signal_kernel<<<1, 64, 0, qs>>>(sync + 2, epoch);
+    gas_wait_kernel<<<1, 64, 0, s>>>(
+        WaitArgs{sync + 1, 2, nullptr, epoch, limit, 0, abort_flag, ctx->gas_sync_fault, 0});
     PAS_HIP(ctx, hipGetLastError());
-    joins.forked = 0;
+    joins.forked = false;
   } else {
     PAS_HIP(ctx, joins.join());
   }

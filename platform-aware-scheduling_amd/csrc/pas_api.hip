@@ -289,8 +289,8 @@ void pas_destroy(pas_ctx* ctx) {
     if (a.ev) (void)hipEventDestroy(a.ev);
     if (a.fork) (void)hipEventDestroy(a.fork);
     if (a.join) (void)hipEventDestroy(a.join);
-    if (a.side) (void)hipStreamDestroy(a.side);
     if (a.join2) (void)hipEventDestroy(a.join2);
+    if (a.side) (void)hipStreamDestroy(a.side);
     if (a.side2) (void)hipStreamDestroy(a.side2);
     for (void* b : a.buf)
       if (b) (void)hipFree(b);
@@ -313,7 +313,14 @@ int pas_synchronize(pas_ctx* ctx) {
   if (!ctx) return PAS_EINVAL;
   PAS_HIP(ctx, hipSetDevice(ctx->device));
   PAS_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return PAS_OK;
+  // every stream's calls: the slots' last users and the GAS fits' side streams
+  for (AuxSlot& a : ctx->aux_slot) {
+    if (a.used && a.ev) PAS_HIP(ctx, hipEventSynchronize(a.ev));
+    if (a.side) PAS_HIP(ctx, hipStreamSynchronize(a.side));
+    if (a.side2) PAS_HIP(ctx, hipStreamSynchronize(a.side2));
+  }
+  // a GAS fit whose side-stream wait gave up (device flags): its results are incomplete
+  return gas_fault_check(ctx);
 }
 
 int pas_parse_operator(const char* op) {
@@ -1028,6 +1035,8 @@ static int gas_fit_host(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_
   if (side_count)
     PAS_HIP(ctx, hipMemcpyAsync(&count, d_count, sizeof(int64_t), hipMemcpyDeviceToHost, s));
   PAS_HIP(ctx, hipStreamSynchronize(s));
+  // a side-stream wait of this fit that gave up: its words are incomplete
+  if ((rc = gas_fault_check(ctx))) return rc;
   if (side_count) {
     *side_count = count;
     const int64_t got = std::min(count, side_cap);

@@ -129,13 +129,13 @@ struct AuxSlot {
   int32_t* gas_counts = nullptr;
   int gas_counts_set = 0;
   int64_t* gas_limit = nullptr;  // pods of the slot's last GAS fit past PAS_GAS_MAX_SELECTIONS
-  // a side stream for fit kernels running beside each other (forked / joined per fit)
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  hipStream_t side2 = nullptr;  // the sequential GAS kernel's side stream (joined per fit)
-  hipEvent_t join2 = nullptr;
-  // device-side fork / join of those streams (gas_fit.hip): flags [prep done, side done,
-  // side2 done] each set to the fit's epoch (a per-slot count of fits)
+  // the GAS fit's side streams (one-selection + generic kernels; sequential kernel), forked
+  // from and joined to the caller's stream per fit, and their events (events mode)
+  hipStream_t side = nullptr, side2 = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr, join2 = nullptr;
+  // device-side fork / join (gas_fit.hip): flags [prep done, side done, side2 done, abort,
+  // prep started] each set to the fit's epoch (a per-slot count of fits); abort = the epoch of
+  // a fit whose wait timed out (its fit kernels return at entry)
   uint32_t* gas_sync = nullptr;
   uint32_t gas_epoch = 0;
   // further per-stream buffers of the _device entry points (slot_buf), grown on demand
@@ -173,6 +173,7 @@ struct pas_ctx {
   // by a wait kernel that gave up)
   int gas_sync_mode = -1;
   uint32_t* gas_sync_fault = nullptr;
+  int gas_force_timeouts = 0;  // PAS_GAS_FORCE_TIMEOUT: the next n flag-mode fits time out
   // timing
   int timing = 0;  // 0 off, PAS_TIMING_SPAN, PAS_TIMING_KERNELS (pas_set_timing)
   std::vector<pas::TimedLaunch> pending;
@@ -245,6 +246,10 @@ int prio_request_launch(pas_ctx* ctx, const pas_rule& rule, int32_t n_req, const
                         hipStream_t s);
 int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
                           const int32_t* d_rule_off, uint64_t* d_viol, hipStream_t s);
+// A GAS fit whose side-stream wait timed out (device flags) reports here: after the fit's
+// stream was synchronized, PAS_EDEVICE (and the side streams drained) if a wait gave up since
+// the last report, else PAS_OK.
+int gas_fault_check(pas_ctx* ctx);
 int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t i915_index,
                    const int64_t* d_req, const uint32_t* d_req_mask,
                    const int32_t* d_n_containers, uint32_t* d_res, int64_t ld_res,
