@@ -69,6 +69,11 @@ constexpr int kSingleTpb = PAS_GAS_SINGLE_TPB;
 #ifndef PAS_GAS_SPIN_SYNC
 #define PAS_GAS_SPIN_SYNC 1  // 1: fork / join the fit's side streams with device flags (0: events)
 #endif
+#ifndef PAS_GAS_FAULT_INJECTION
+// 1: the fault-injection build (lib/libpas_fault.so): PAS_GAS_FORCE_TIMEOUT=n makes the next
+// n fits' side-stream waits give up at once, to test that the call then fails loudly
+#define PAS_GAS_FAULT_INJECTION 0
+#endif
 #ifndef PAS_GAS_SEQ_FIRST
 #define PAS_GAS_SEQ_FIRST 0  // 1: the sequential kernel before the closed-form one (diagnostic)
 #endif
@@ -2232,8 +2237,10 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
       PAS_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->gas_sync_fault), sizeof(uint32_t),
                                  hipHostMallocCoherent));
       *ctx->gas_sync_fault = 0;
+#if PAS_GAS_FAULT_INJECTION  // lib/libpas_fault.so only (tests/test_gas_sync.py)
       if (const char* f = std::getenv("PAS_GAS_FORCE_TIMEOUT"))
         ctx->gas_force_timeouts = std::atoi(f);
+#endif
     }
   }
   // a wait of an earlier fit that gave up and was not reported by a synchronization yet

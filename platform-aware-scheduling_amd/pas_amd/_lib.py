@@ -14,6 +14,8 @@ from ctypes import POINTER, c_char_p, c_double, c_int, c_int32, c_int64, c_uint3
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpas.so")
+# the same library built with the GAS fault-injection knob (test tooling only)
+FAULT_LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "lib", "libpas_fault.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_PKG_DIR)), "include", "pas.h")
 
 PAS_OK = 0
@@ -284,4 +286,27 @@ def load() -> ctypes.CDLL:
         fn.restype = restype
         fn.argtypes = argtypes
     _lib = lib
+    return lib
+
+
+_fault = None
+
+
+def load_fault() -> ctypes.CDLL:
+    """lib/libpas_fault.so: libpas.so compiled with PAS_GAS_FAULT_INJECTION=1, whose GAS fits
+    read PAS_GAS_FORCE_TIMEOUT=n (the next n fits' side-stream waits give up at once).  Test
+    tooling for the fail-loud path of the fork / join; the product library has no such knob."""
+    global _fault
+    if _fault is not None:
+        return _fault
+    load()  # torch's HIP runtime first (see load)
+    if not os.path.exists(FAULT_LIB_PATH):
+        raise ImportError(f"{FAULT_LIB_PATH} not found: build it with "
+                          "`make -C platform-aware-scheduling_amd`")
+    lib = ctypes.CDLL(FAULT_LIB_PATH)
+    for name, (restype, argtypes) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
+    _fault = lib
     return lib

@@ -100,8 +100,8 @@ def label_patch_json(names, add_mask: int, remove_mask: int) -> bytes:
 class Context:
     """One pas_ctx bound to a HIP device."""
 
-    def __init__(self, device: int = -1):
-        self._l = _lib.load()
+    def __init__(self, device: int = -1, lib=None):
+        self._l = lib if lib is not None else _lib.load()
         h = c_void_p()
         cfg = _lib.PasConfig(device, 0)
         rc = self._l.pas_create(byref(cfg), byref(h))

@@ -3,8 +3,9 @@ reference's filter answer is (gpu-aware-scheduling/pkg/gpuscheduler/scheduler.go
 
 With device flags a side-stream wait that gives up aborts its fit (the fit kernels return at
 entry) and the call's synchronization reports PAS_EDEVICE: the host forms themselves, the
-_device forms through pas_synchronize.  PAS_GAS_FORCE_TIMEOUT=n (read when a context resolves
-its sync mode) makes the next n flag-mode fits' waits give up at once.  A fit behind more
+_device forms through pas_synchronize.  The fault-injection build lib/libpas_fault.so reads
+PAS_GAS_FORCE_TIMEOUT=n when a context resolves its sync mode: the next n flag-mode fits'
+waits give up at once (the product library has no such knob).  A fit behind more
 than a second of the caller's own work on its stream still completes (the waits start
 timing when the fit's prep starts)."""
 import os
@@ -19,12 +20,14 @@ pytestmark = pytest.mark.gpu
 
 
 def _new_ctx(monkeypatch, force=None):
+    """A flag-mode context: of the product library, or (force=n) of the fault-injection
+    build with its next n fits' waits forced to give up."""
     monkeypatch.setenv("PAS_GAS_SYNC", "flags")
     if force is None:
         monkeypatch.delenv("PAS_GAS_FORCE_TIMEOUT", raising=False)
-    else:
-        monkeypatch.setenv("PAS_GAS_FORCE_TIMEOUT", str(force))
-    return pas_amd.Context(0)
+        return pas_amd.Context(0)
+    monkeypatch.setenv("PAS_GAS_FORCE_TIMEOUT", str(force))
+    return pas_amd.Context(0, lib=pas_amd._lib.load_fault())
 
 
 def _case(oracle, n=3000, p=64, seed=0xC3):
