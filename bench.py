@@ -637,15 +637,17 @@ def bench_deschedule(args, world, rank):
 
 # ------------------------------------------------------------------------------- C5
 
-def c5_setup(args, world, rank, whole=False, host=None):
-    """The C5 workload on this rank: its node range of the cluster (whole: every node, for
-    the pod-sharded split) as resident TAS and GAS snapshots (generations 1 and 2), the pod
-    batch on the device.  host: a dict that receives the host batches (tbatch, gbatch)."""
+def c5_setup(args, world, rank, node_shards=None, host=None):
+    """The C5 workload on this rank: its node range of the cluster -- node shard rank % s of
+    s = node_shards (default world: one shard per rank; 1: every node) -- as resident TAS and
+    GAS snapshots (generations 1 and 2), the pod batch on the device.  host: a dict that
+    receives the host batches (tbatch, gbatch)."""
     P, N, M, R = args.pods, args.nodes, args.metrics, args.rules - 1
     ctx = pas_amd.Context(torch.cuda.current_device())
     stream = torch.cuda.current_stream()
     ctx.set_stream(stream)
-    n0, n1 = (0, N) if whole else shard.node_range(N, world, rank)
+    s = world if node_shards is None else node_shards
+    n0, n1 = shard.node_range(N, s, rank % s)
     tsnap = wl.make_tas_snapshot(N, M, seed=0xC5)
     v, pres = shard_tas(tsnap, n0, n1)
     ctx.tas_snapshot_set_device(1, n1 - n0, M, dev(v), dev(pres.view(np.int64)), stream)
@@ -726,14 +728,50 @@ def bench_c5(args, world, rank):
     return out
 
 
+def grid_c5_record(a, world, rank, node_shards):
+    """The C5 step over a node_shards x (world / node_shards) grid (shard.GridTopK), timed with
+    the barrier / max-over-ranks protocol; returns (record, every pod's lists gathered)."""
+    host = {}
+    ctx, stream, n0, n1, t = c5_setup(a, world, rank, node_shards, host=host)
+    del t
+    tb, gb = host["tbatch"], host["gbatch"]
+    grid = shard.GridTopK(ctx, a.topk, world, rank, node_shards, a.pods, a.nodes, tb.rules,
+                          tb.rule_off, tb.prio, gb.req, gb.req_mask, gb.n_containers)
+    for _ in range(a.warmup):
+        grid.run(1, 2, wl.I915, stream)
+    el = timed_steps(lambda: grid.run(1, 2, wl.I915, stream), a.steps, 0, world)
+    # the combined kernel alone (extra untimed steps, events around the launch)
+    ctx.reset_timing()
+    ctx.set_timing(2)
+    for _ in range(3):
+        grid.run(1, 2, wl.I915, stream)
+    ctx.set_timing(0)
+    k_ms, k_n = ctx.kernel_time(_lib.PAS_K_TAS_GAS_TOPK)
+    lists = grid.gather()
+    g = world // node_shards
+    rec = {"split": f"{node_shards} node shard(s) x {g} pod group(s)",
+           "node_shards": node_shards, "pod_groups": g, "pods_per_gpu": grid.p1 - grid.p0,
+           "nodes_per_gpu": n1 - n0, "topk": a.topk,
+           "step_collective": ("all-gather of records within each pod group + merge"
+                               if node_shards > 1 else "none (lists gathered once at the end)"),
+           "ms_per_step": el / a.steps * 1e3, "pods_per_s": a.pods * a.steps / el,
+           "topk_kernel_ms": k_ms / max(k_n, 1), "scaling": "strong"}
+    ctx.close()
+    del grid
+    torch.cuda.empty_cache()
+    return rec, (lists[0].cpu(), lists[1].cpu())
+
+
 def node_sharded_record(args, world, rank):
     """The north_star's 1M-node scaling point, run inside a multi-GPU bench.py call: the C5
-    step (64k pods x 1M nodes) split two ways -- node-sharded over the ranks (RCCL all-gather
-    + merge every step; the path for clusters past one GPU's memory) and pod-sharded over a
-    replicated snapshot (no collective in the step; lists gathered once at the end) -- and
-    the C4 deschedule sweep (1M nodes x 64 rules + all-gather of the violation bitmaps), each
-    timed with the same barrier / max-over-ranks protocol.  The driver's 1/2/4/8 runs of
-    bench.py then carry both curves without a --workload flag (DESIGN.md §6 cost model)."""
+    step (64k pods x 1M nodes) over the 2-D split of shard.GridTopK -- s node shards x
+    world / s pod groups -- at s = the fewest shards the snapshot memory needs
+    (shard.min_node_shards: 1 at 1M nodes, pure pod sharding), at s = world (pure node
+    sharding, the path for clusters past one GPU's memory) and, from 4 ranks, at s = 2; plus
+    the C4 deschedule sweep (1M nodes x 64 rules + all-gather of the violation bitmaps).  Each
+    is timed with the same barrier / max-over-ranks protocol, and every split's lists are
+    checked equal.  The driver's 1/2/4/8 runs of bench.py then carry the curves without a
+    --workload flag (DESIGN.md §6 cost model: per-rank kernel work (P / g) x (N / s))."""
     import argparse as _ap
     import torch.distributed as dist
     rec = {"nodes": 1_000_000, "world_size": world,
@@ -741,45 +779,19 @@ def node_sharded_record(args, world, rank):
     a = _ap.Namespace(**vars(args))
     a.pods, a.nodes, a.steps, a.warmup, a.settle = args.ns_pods, args.ns_nodes, 10, 2, 0.1
     rec["nodes"] = a.nodes
-    ctx, stream, n0, n1, t = c5_setup(a, world, rank)
-    topk = shard.ShardedTopK(ctx, a.topk, world, rank, n0)
-    step, result = c5_step_fn(ctx, stream, topk, a.pods, t)
-    for _ in range(a.warmup):
-        step()
-    el = timed_steps(step, a.steps, 0, world)
-    # every rank ends the step with the same merged lists (all-gather + identical merge)
-    digest = (int(result["nodes"].to(torch.int64).sum().item()),
-              int(result["len"].to(torch.int64).sum().item()))
-    rec["c5_topk"] = {"pods": a.pods, "nodes_per_gpu": n1 - n0, "topk": a.topk,
-                      "split": "node-sharded", "ms_per_step": el / a.steps * 1e3,
-                      "pods_per_s": a.pods * a.steps / el, "scaling": "strong",
-                      "entries": digest[1],
-                      "ranks_agree": len(set(distrib.gather_objects(digest, world))) == 1}
-    node_lists = (result["nodes"].clone(), result["len"].clone())
-    ctx.close()
-    del topk, t, result
-    torch.cuda.empty_cache()
-    # the same step split by pod over the whole cluster on every rank
-    host = {}
-    ctx, stream, _, _, t = c5_setup(a, world, rank, whole=True, host=host)
-    tb, gb = host["tbatch"], host["gbatch"]
-    ps = shard.PodShardedTopK(ctx, a.topk, world, rank, a.pods, tb.rules, tb.rule_off, tb.prio,
-                              gb.req, gb.req_mask, gb.n_containers)
-    del t
-    for _ in range(a.warmup):
-        ps.run(1, 2, wl.I915, stream)
-    el = timed_steps(lambda: ps.run(1, 2, wl.I915, stream), a.steps, 0, world)
-    pods_nodes, pods_lens = ps.gather()
-    same = bool(torch.equal(pods_nodes, node_lists[0]) and torch.equal(pods_lens, node_lists[1]))
-    rec["c5_topk_pod_sharded"] = {
-        "pods": a.pods, "pods_per_gpu": ps.p1 - ps.p0, "nodes_per_gpu": a.nodes, "topk": a.topk,
-        "split": "pod-sharded (snapshot replicated, lists gathered once after the timed steps)",
-        "ms_per_step": el / a.steps * 1e3, "pods_per_s": a.pods * a.steps / el,
-        "scaling": "strong",
-        "equals_node_sharded": all(distrib.gather_objects(same, world))}
-    ctx.close()
-    del ps
-    torch.cuda.empty_cache()
+    s_mem = shard.min_node_shards(world, a.nodes, a.metrics)
+    splits = [("c5_topk", s_mem), ("c5_topk_node_sharded", world)]
+    if world >= 4 and world % 2 == 0:
+        splits.append(("c5_topk_grid_2", 2))
+    lists = {}
+    for name, s in splits:
+        if any(s == s2 for s2 in lists):
+            continue
+        rec[name], lists[s] = grid_c5_record(a, world, rank, s)
+    ref = lists[s_mem]
+    same = all(torch.equal(v[0], ref[0]) and torch.equal(v[1], ref[1]) for v in lists.values())
+    rec["splits_agree"] = all(distrib.gather_objects(same, world))
+    rec["c5_topk"]["entries"] = int(ref[1].to(torch.int64).sum().item())
     d = bench_deschedule(a, world, rank)
     rec["c4_deschedule"] = {"nodes_per_gpu": d["config"]["nodes_per_gpu"],
                             "ms_per_step": d["ms_per_step"],

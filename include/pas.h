@@ -19,10 +19,13 @@
  *     gpu-aware-scheduling/pkg/gpuscheduler/scheduler.go:463-465).
  *   - Bitmaps are little-endian uint64 words, node n at bit (n & 63) of word n >> 6;
  *     W64(n) = (n + 63) / 64 words per row, bits >= n_nodes are zero.
- *   - Metric values are int64 "milli" units: value * 1000 of the reference's
- *     resource.Quantity (telemetry-aware-scheduling/pkg/metrics/client.go:25-29).
- *     pas_quantity_to_milli() converts a Quantity string and reports
- *     non-milli-exact values (PAS_ENOTEXACT) — those must not reach the device.
+ *   - Metric values are int64 fixed-point columns: column m holds value * 10^scale[m] of
+ *     the reference's resource.Quantity (telemetry-aware-scheduling/pkg/metrics/
+ *     client.go:25-29), scale 3 ("milli") unless pas_tas_snapshot_set_scale says otherwise.
+ *     ParseQuantity keeps at most 9 fractional digits (it rounds to 1e-9), so a column with
+ *     scale = the most decimal places of its values (pas_quantity_decimals, 0..9) is exact;
+ *     pas_quantity_to_scaled() converts a Quantity string and reports PAS_ENOTEXACT only
+ *     when value * 10^scale is outside int64.
  */
 #ifndef PAS_H_
 #define PAS_H_
@@ -109,6 +112,13 @@ int pas_parse_operator(const char* op);
  * PAS_ENOTEXACT if that value has sub-milli precision or is outside int64 milli range;
  * PAS_EINVAL if ParseQuantity would fail. */
 int pas_quantity_to_milli(const char* quantity, int64_t* milli_out);
+/* The same at any decimal scale: value * 10^places exactly, 0 <= places <= 9 (EINVAL
+ * otherwise); PAS_ENOTEXACT if that is not an integer or is outside int64.
+ * pas_quantity_to_milli is places = 3. */
+int pas_quantity_to_scaled(const char* quantity, int32_t places, int64_t* out);
+/* The fewest decimal places (0..9) that hold the parsed value exactly: "1500u" -> 4,
+ * "0.0005" -> 4, "1e-7" -> 7, "2k" -> 0, "1.5" -> 1. */
+int pas_quantity_decimals(const char* quantity, int32_t* places);
 
 /* resource.ParseQuantity(quantity).AsInt64() with `ok` ignored, as the reference uses it
  * (gpuscheduler/utils.go:23, scheduler.go:155).  That is 0 — even for integral values —
@@ -126,7 +136,8 @@ int pas_quantity_as_int64(const char* quantity, int64_t* out);
 
 /* Upload a node-metric snapshot: the content of AutoUpdatingCache's
  * "metrics/<name>" entries (cache/autoupdating.go:76-85) as SoA columns.
- *   v_milli [n_metrics][n_nodes]      value * 1000 (ignored where not present)
+ *   v_milli [n_metrics][n_nodes]      value * 1000 (ignored where not present), or
+ *                                     value * 10^scale[m] with pas_tas_snapshot_set_scale
  *   present [n_metrics][W64(n_nodes)] node has this metric (NodeMetricsInfo key set)
  * The device builds per-metric sorted orders once here, so that per-request
  * evaluation never sorts (core.OrderedList, operator.go:30-42, sorts per request).
@@ -138,6 +149,19 @@ int pas_tas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
                                 void* hip_stream);
 int pas_tas_snapshot_info(const pas_ctx* ctx, uint64_t* gen, int32_t* n_nodes,
                           int32_t* n_metrics);
+
+/* Decimal scale of each column of the resident snapshot generation gen: column m holds
+ * value * 10^col_scale[m] (0 <= col_scale[m] <= 9, host array of n_metrics = the snapshot's
+ * metric count).  Every column is 3 (milli) after pas_tas_snapshot_set[_device]; a column
+ * refresh keeps the column's scale.  Rule targets are integers (TASPolicyRule.Target,
+ * telemetrypolicy/api/v1alpha1/types.go:31-35), so core.EvaluateRule's CmpInt64
+ * (operator.go:16-22) is exact against target * 10^scale (saturated past int64), and
+ * OrderedList's Cmp (:37,39) is the integer order of one column: sub-milli metric values
+ * evaluate on the device exactly.  Order this call after evaluations on
+ * other streams that still read the snapshot, as a snapshot change; it is synchronous on
+ * hip_stream (NULL: the context's stream). */
+int pas_tas_snapshot_set_scale(pas_ctx* ctx, uint64_t gen, int32_t n_metrics,
+                               const int32_t* col_scale, void* hip_stream);
 
 /* Column refresh: AutoUpdatingCache.updateMetric replaces one metric's whole node map
  * (cache/autoupdating.go:45-73, WriteMetric :100-112).  Replaces the resident snapshot's

@@ -48,6 +48,12 @@ def load():
         "or_ordered_list_request": (c_int32, [c_int32, c_int32, P, P, P, c_int32, P, P]),
         "or_tas_eval": (c_int, [c_int32, c_int32, P, P, c_int32, P, P, P, P, c_uint32, P, P, P]),
         "or_tas_violations": (c_int, [c_int32, c_int32, P, P, c_int32, P, P, P]),
+        "or_evaluate_rule_dec": (c_int, [c_int64, c_int32, c_int32, c_int64]),
+        "or_cmp_dec": (c_int, [c_int64, c_int32, c_int64, c_int32]),
+        "or_tas_eval_dec": (c_int, [c_int32, c_int32, P, P, P, c_int32, P, P, P, P, c_uint32,
+                                    P, P, P]),
+        "or_ordered_list_request_dec": (c_int32, [c_int32, c_int32, P, P, P, P, c_int32, P, P]),
+        "or_tas_violations_dec": (c_int, [c_int32, c_int32, P, P, P, c_int32, P, P, P]),
         "or_rm_add": (c_int, [POINTER(OrRm), c_int32, c_int64]),
         "or_rm_subtract": (c_int, [POINTER(OrRm), c_int32, c_int64]),
         "or_rm_add_rm": (c_int, [POINTER(OrRm), POINTER(OrRm)]),
@@ -91,7 +97,25 @@ def evaluate_rule(v_milli: int, op: int, target: int) -> int:
     return load().or_evaluate_rule(v_milli, op, target)
 
 
-def tas_eval(v_milli, present, rules, rule_off, prio, cand=None, flags=3):
+def _scale(v_scale, shape):
+    """Per-value decimal places [M][N] (int8; value = v * 10^-scale) or None (milli)."""
+    if v_scale is None:
+        return None
+    sc = np.ascontiguousarray(v_scale, np.int8)
+    assert sc.shape == shape and sc.min(initial=0) >= 0 and sc.max(initial=0) <= 9
+    return sc
+
+
+def evaluate_rule_dec(u: int, s: int, op: int, target: int) -> int:
+    return load().or_evaluate_rule_dec(u, s, op, target)
+
+
+def cmp_dec(u1: int, s1: int, u2: int, s2: int) -> int:
+    return load().or_cmp_dec(u1, s1, u2, s2)
+
+
+def tas_eval(v_milli, present, rules, rule_off, prio, cand=None, flags=3, v_scale=None):
+    """v_scale: per-value decimal places (value = v * 10^-v_scale), None = milli."""
     v = np.ascontiguousarray(v_milli, np.int64)
     m, n = v.shape
     p = np.ascontiguousarray(present, np.uint64)
@@ -104,15 +128,16 @@ def tas_eval(v_milli, present, rules, rule_off, prio, cand=None, flags=3):
     pass_out = np.zeros((n_pods, w64(n)), np.uint64) if flags & 1 else None
     order = np.zeros((n_pods, max(n, 1)), np.int32) if flags & 2 else None
     lens = np.zeros(n_pods, np.int32) if flags & 2 else None
-    rc = load().or_tas_eval(n, m, _p(v), _p(p), n_pods, _p(rules) if rules.size else None,
-                            _p(rule_off), _p(prio), _p(cand), flags, _p(pass_out), _p(order),
-                            _p(lens))
+    sc = _scale(v_scale, v.shape)
+    rc = load().or_tas_eval_dec(n, m, _p(v), _p(sc), _p(p), n_pods,
+                                _p(rules) if rules.size else None, _p(rule_off), _p(prio),
+                                _p(cand), flags, _p(pass_out), _p(order), _p(lens))
     if rc != 0:
         raise ValueError("oracle: invalid operator (the reference panics)")
     return pass_out, order, lens
 
 
-def prioritize_request(v_milli, present, prio, req_node):
+def prioritize_request(v_milli, present, prio, req_node, v_scale=None):
     """Request positions best-first for one request (SURVEY.md A.3 tie order)."""
     v = np.ascontiguousarray(v_milli, np.int64)
     m, n = v.shape
@@ -120,11 +145,13 @@ def prioritize_request(v_milli, present, prio, req_node):
     rule = np.ascontiguousarray(np.asarray(prio, RULE_DTYPE).reshape(1))
     req = np.ascontiguousarray(req_node, np.int32)
     out = np.zeros(max(len(req), 1), np.int32)
-    k = load().or_ordered_list_request(n, m, _p(v), _p(p), _p(rule), len(req), _p(req), _p(out))
+    sc = _scale(v_scale, v.shape)
+    k = load().or_ordered_list_request_dec(n, m, _p(v), _p(sc), _p(p), _p(rule), len(req),
+                                           _p(req), _p(out))
     return out[:k]
 
 
-def tas_violations(v_milli, present, rules, rule_off):
+def tas_violations(v_milli, present, rules, rule_off, v_scale=None):
     v = np.ascontiguousarray(v_milli, np.int64)
     m, n = v.shape
     p = np.ascontiguousarray(present, np.uint64)
@@ -132,8 +159,9 @@ def tas_violations(v_milli, present, rules, rule_off):
     rule_off = np.ascontiguousarray(rule_off, np.int32)
     s = rule_off.shape[0] - 1
     out = np.zeros((s, w64(n)), np.uint64)
-    rc = load().or_tas_violations(n, m, _p(v), _p(p), s, _p(rules) if rules.size else None,
-                                  _p(rule_off), _p(out))
+    sc = _scale(v_scale, v.shape)
+    rc = load().or_tas_violations_dec(n, m, _p(v), _p(sc), _p(p), s,
+                                      _p(rules) if rules.size else None, _p(rule_off), _p(out))
     if rc != 0:
         raise ValueError("oracle: invalid operator (the reference panics)")
     return out

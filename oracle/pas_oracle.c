@@ -30,13 +30,30 @@ static int metric_in_cache(int32_t n_nodes, int32_t n_metrics, const uint64_t* p
   return 0;
 }
 
-/* operator.go:13-26.  The reference compares the exact decimal Quantity with the int64
- * target; here value = v_milli / 1000 exactly, so the comparison is v_milli against
- * target * 1000 in 128-bit arithmetic (no saturation needed). */
-int or_evaluate_rule(int64_t v_milli, int32_t op, int64_t target) {
-  const __int128 v = (__int128)v_milli;
-  const __int128 t = (__int128)target * 1000;
-  const int cmp = v < t ? -1 : (v > t ? 1 : 0); /* Quantity.CmpInt64 */
+/* A metric value as the exact decimal the reference holds: unscaled u and decimal places s,
+ * value = u * 10^-s (inf.Dec's {unscaled, scale}; an int64Amount{value, scale} is the same
+ * with s = -scale).  resource.ParseQuantity rounds every value to 9 fractional digits
+ * (inf.RoundUp at Nano) and caps it at 2^63 - 1, so 0 <= s <= 9 covers every Quantity a
+ * metric can hold.  Comparisons align both operands to 10^-9 (u * 10^(9 - s)) in 128-bit
+ * integers, as inf.Dec.Cmp aligns scales before comparing unscaled values: exact, no
+ * rounding, no saturation.  vs == NULL: every value is milli (s = 3). */
+static const __int128 kPow10[10] = {1, 10, 100, 1000, 10000, 100000, 1000000, 10000000,
+                                    100000000, 1000000000};
+
+static inline __int128 nano_of(const int64_t* v, const int8_t* vs, int64_t i) {
+  const int s = vs ? vs[i] : 3;
+  return (__int128)v[i] * kPow10[9 - s];
+}
+
+/* Quantity.CmpInt64(target) on a value in units of 1e-9. */
+static int cmp_int64_nano(__int128 v, int64_t target) {
+  const __int128 t = (__int128)target * kPow10[9];
+  return v < t ? -1 : (v > t ? 1 : 0);
+}
+
+/* operator.go:13-26 on an aligned value. */
+static int evaluate_rule_nano(__int128 v, int32_t op, int64_t target) {
+  const int cmp = cmp_int64_nano(v, target); /* Quantity.CmpInt64 */
   switch (op) {
     case 0: return cmp == -1; /* "LessThan"    operator.go:15-17 */
     case 1: return cmp == 1;  /* "GreaterThan" operator.go:18-20 */
@@ -45,10 +62,24 @@ int or_evaluate_rule(int64_t v_milli, int32_t op, int64_t target) {
   }
 }
 
+int or_evaluate_rule(int64_t v_milli, int32_t op, int64_t target) {
+  return evaluate_rule_nano((__int128)v_milli * kPow10[6], op, target);
+}
+
+int or_evaluate_rule_dec(int64_t u, int32_t s, int32_t op, int64_t target) {
+  if (s < 0 || s > 9) return -2;
+  return evaluate_rule_nano((__int128)u * kPow10[9 - s], op, target);
+}
+
+int or_cmp_dec(int64_t u1, int32_t s1, int64_t u2, int32_t s2) {
+  const __int128 a = (__int128)u1 * kPow10[9 - s1], b = (__int128)u2 * kPow10[9 - s2];
+  return a < b ? -1 : (a > b ? 1 : 0);
+}
+
 /* dontschedule/strategy.go:25-44 (deschedule/strategy.go:31-50 is the same loop). */
-int or_violated(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
-                const uint64_t* present, const or_rule* rules, int32_t n_rules,
-                uint8_t* violating) {
+static int violated_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                        const int8_t* v_scale, const uint64_t* present, const or_rule* rules,
+                        int32_t n_rules, uint8_t* violating) {
   memset(violating, 0, (size_t)n_nodes);
   for (int32_t r = 0; r < n_rules; ++r) {            /* for _, rule := range d.Rules */
     const or_rule* rule = &rules[r];
@@ -56,22 +87,28 @@ int or_violated(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
       continue;                                      /* ReadMetric err -> continue :28-32 */
     if (rule->op < 0 || rule->op > 2)
       return -1; /* EvaluateRule runs for >= 1 node of the map: panic (operator.go:25) */
-    const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
+    const int64_t base = (int64_t)rule->metric * n_nodes;
     const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
     for (int32_t n = 0; n < n_nodes; ++n) {          /* for nodeName, nodeMetric := range */
       if (!has_bit(pres, n)) continue;
-      if (or_evaluate_rule(col[n], rule->op, rule->target))
+      if (evaluate_rule_nano(nano_of(v_milli, v_scale, base + n), rule->op, rule->target))
         violating[n] = 1;                            /* violatingNodes[nodeName] = nil */
     }
   }
   return 0;
 }
 
+int or_violated(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                const uint64_t* present, const or_rule* rules, int32_t n_rules,
+                uint8_t* violating) {
+  return violated_dec(n_nodes, n_metrics, v_milli, NULL, present, rules, n_rules, violating);
+}
+
 /* ---- OrderedList ---------------------------------------------------------- */
 
 typedef struct sortable {
   int32_t node;
-  int64_t value;
+  __int128 value; /* units of 1e-9: Quantity.Cmp is integer order here */
 } sortable;
 
 /* Stable merge sort; `desc` selects the GreaterThan comparator (operator.go:37),
@@ -104,14 +141,14 @@ static void merge_sort(sortable* a, sortable* tmp, int32_t n, int desc) {
   memcpy(a, tmp, (size_t)n * sizeof(sortable));
 }
 
-int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
-                        const uint64_t* present, const or_rule* rule, const uint8_t* cand,
-                        int32_t* out) {
+static int32_t ordered_list_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                                const int8_t* v_scale, const uint64_t* present,
+                                const or_rule* rule, const uint8_t* cand, int32_t* out) {
   /* getSchedulingRule (telemetryscheduler.go:115-124) already rejected rules without a
    * metric name; a metric missing from the cache makes prioritizeNodesForRule fail
    * (:130-133) and prioritizeNodes answer with an empty list (:92-96). */
   if (!metric_in_cache(n_nodes, n_metrics, present, rule->metric)) return 0;
-  const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
+  const int64_t base = (int64_t)rule->metric * n_nodes;
   const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
   sortable* items = (sortable*)malloc(sizeof(sortable) * (size_t)(n_nodes > 0 ? n_nodes : 1));
   sortable* tmp = (sortable*)malloc(sizeof(sortable) * (size_t)(n_nodes > 0 ? n_nodes : 1));
@@ -120,7 +157,7 @@ int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_mil
   for (int32_t n = 0; n < n_nodes; ++n) {
     if (!cand[n] || !has_bit(pres, n)) continue;
     items[cnt].node = n;
-    items[cnt].value = col[n];
+    items[cnt].value = nano_of(v_milli, v_scale, base + n);
     ++cnt;
   }
   if (rule->op == 1) merge_sort(items, tmp, cnt, 1);       /* "GreaterThan" :36-37 */
@@ -132,11 +169,18 @@ int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_mil
   return cnt;
 }
 
-int32_t or_ordered_list_request(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
-                                const uint64_t* present, const or_rule* rule, int32_t n_req,
-                                const int32_t* req_node, int32_t* out_pos) {
+int32_t or_ordered_list(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                        const uint64_t* present, const or_rule* rule, const uint8_t* cand,
+                        int32_t* out) {
+  return ordered_list_dec(n_nodes, n_metrics, v_milli, NULL, present, rule, cand, out);
+}
+
+int32_t or_ordered_list_request_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                                    const int8_t* v_scale, const uint64_t* present,
+                                    const or_rule* rule, int32_t n_req, const int32_t* req_node,
+                                    int32_t* out_pos) {
   if (rule->metric < 0 || !metric_in_cache(n_nodes, n_metrics, present, rule->metric)) return 0;
-  const int64_t* col = v_milli + (int64_t)rule->metric * n_nodes;
+  const int64_t base = (int64_t)rule->metric * n_nodes;
   const uint64_t* pres = present + (int64_t)rule->metric * w64(n_nodes);
   const size_t cap = (size_t)(n_req > 0 ? n_req : 1);
   sortable* items = (sortable*)malloc(sizeof(sortable) * cap);
@@ -149,7 +193,7 @@ int32_t or_ordered_list_request(int32_t n_nodes, int32_t n_metrics, const int64_
     seen[n] = 1;
     if (!has_bit(pres, n)) continue;          /* if v, ok := nodeData[node.Name]; ok */
     items[cnt].node = j;
-    items[cnt].value = col[n];
+    items[cnt].value = nano_of(v_milli, v_scale, base + n);
     ++cnt;
   }
   if (rule->op == 1) merge_sort(items, tmp, cnt, 1);
@@ -161,10 +205,18 @@ int32_t or_ordered_list_request(int32_t n_nodes, int32_t n_metrics, const int64_
   return cnt;
 }
 
-int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
-                const uint64_t* present, int32_t n_pods, const or_rule* rules,
-                const int32_t* rule_off, const or_rule* prio, const uint64_t* cand,
-                uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len) {
+int32_t or_ordered_list_request(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                                const uint64_t* present, const or_rule* rule, int32_t n_req,
+                                const int32_t* req_node, int32_t* out_pos) {
+  return or_ordered_list_request_dec(n_nodes, n_metrics, v_milli, NULL, present, rule, n_req,
+                                     req_node, out_pos);
+}
+
+int or_tas_eval_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                    const int8_t* v_scale, const uint64_t* present, int32_t n_pods,
+                    const or_rule* rules, const int32_t* rule_off, const or_rule* prio,
+                    const uint64_t* cand, uint32_t flags, uint64_t* pass_out,
+                    int32_t* order_out, int32_t* order_len) {
   const int64_t W = w64(n_nodes);
   uint8_t* viol = (uint8_t*)malloc((size_t)(n_nodes > 0 ? n_nodes : 1));
   uint8_t* cset = (uint8_t*)malloc((size_t)(n_nodes > 0 ? n_nodes : 1));
@@ -175,8 +227,8 @@ int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
       cset[n] = cand ? (uint8_t)has_bit(cand + (int64_t)p * W, n) : 1;
     if (flags & 1u) {
       /* filterNodes: violatingNodes := dontscheduleStrategy.Violated(m.cache) (:199) */
-      if (or_violated(n_nodes, n_metrics, v_milli, present, rules + rule_off[p],
-                      rule_off[p + 1] - rule_off[p], viol) != 0) {
+      if (violated_dec(n_nodes, n_metrics, v_milli, v_scale, present, rules + rule_off[p],
+                       rule_off[p + 1] - rule_off[p], viol) != 0) {
         rc = -1;
         break;
       }
@@ -198,8 +250,8 @@ int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
       if (r->metric >= 0) {
         /* an unknown operator is not an error here: OrderedList's switch has no default
          * (operator.go:35-40), the list is just left unsorted */
-        len = or_ordered_list(n_nodes, n_metrics, v_milli, present, r, cset,
-                              order_out + (int64_t)p * n_nodes);
+        len = ordered_list_dec(n_nodes, n_metrics, v_milli, v_scale, present, r, cset,
+                               order_out + (int64_t)p * n_nodes);
       }
       order_len[p] = len;
     }
@@ -209,16 +261,24 @@ int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
   return rc;
 }
 
-int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
-                      const uint64_t* present, int32_t n_strategies, const or_rule* rules,
-                      const int32_t* rule_off, uint64_t* viol_out) {
+int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                const uint64_t* present, int32_t n_pods, const or_rule* rules,
+                const int32_t* rule_off, const or_rule* prio, const uint64_t* cand,
+                uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len) {
+  return or_tas_eval_dec(n_nodes, n_metrics, v_milli, NULL, present, n_pods, rules, rule_off,
+                         prio, cand, flags, pass_out, order_out, order_len);
+}
+
+int or_tas_violations_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                          const int8_t* v_scale, const uint64_t* present, int32_t n_strategies,
+                          const or_rule* rules, const int32_t* rule_off, uint64_t* viol_out) {
   const int64_t W = w64(n_nodes);
   uint8_t* viol = (uint8_t*)malloc((size_t)(n_nodes > 0 ? n_nodes : 1));
   int rc = 0;
   /* for strat := range enforcer.RegisteredStrategies[StrategyType] (enforce.go:156) */
   for (int32_t s = 0; s < n_strategies; ++s) {
-    if (or_violated(n_nodes, n_metrics, v_milli, present, rules + rule_off[s],
-                    rule_off[s + 1] - rule_off[s], viol) != 0) {
+    if (violated_dec(n_nodes, n_metrics, v_milli, v_scale, present, rules + rule_off[s],
+                     rule_off[s + 1] - rule_off[s], viol) != 0) {
       rc = -1;
       break;
     }
@@ -229,6 +289,13 @@ int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli
   }
   free(viol);
   return rc;
+}
+
+int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                      const uint64_t* present, int32_t n_strategies, const or_rule* rules,
+                      const int32_t* rule_off, uint64_t* viol_out) {
+  return or_tas_violations_dec(n_nodes, n_metrics, v_milli, NULL, present, n_strategies, rules,
+                               rule_off, viol_out);
 }
 
 /* ---- deschedule label payloads ------------------------------------------- */

@@ -33,6 +33,16 @@ typedef struct or_rule {
  * Returns 1/0, or -1 for an operator the reference would panic on (operator.go:25). */
 int or_evaluate_rule(int64_t v_milli, int32_t op, int64_t target);
 
+/* The same on an exact decimal value u * 10^-s, 0 <= s <= 9 (every value resource.ParseQuantity
+ * yields: 9 fractional digits at most, |value| <= 2^63 - 1); -2 for s out of range.  Values
+ * are aligned to 10^-9 in 128-bit integers, as inf.Dec.Cmp aligns scales. */
+int or_evaluate_rule_dec(int64_t u, int32_t s, int32_t op, int64_t target);
+/* Quantity.Cmp of two such values: -1 / 0 / 1. */
+int or_cmp_dec(int64_t u1, int32_t s1, int64_t u2, int32_t s2);
+
+/* The _dec variants below take every value as v[m][n] * 10^-v_scale[m][n] (v_scale NULL =
+ * milli, 3, as the variants without the suffix). */
+
 /* Strategy.Violated for dontschedule (dontschedule/strategy.go:25-44) and deschedule
  * (deschedule/strategy.go:31-50) — identical loops.  violating[n] set to 1 for every
  * node of the union.  Returns 0, or -1 on an invalid operator. */
@@ -67,12 +77,24 @@ int or_tas_eval(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
                 const uint64_t* present, int32_t n_pods, const or_rule* rules,
                 const int32_t* rule_off, const or_rule* prio, const uint64_t* cand,
                 uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len);
+int or_tas_eval_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                    const int8_t* v_scale, const uint64_t* present, int32_t n_pods,
+                    const or_rule* rules, const int32_t* rule_off, const or_rule* prio,
+                    const uint64_t* cand, uint32_t flags, uint64_t* pass_out,
+                    int32_t* order_out, int32_t* order_len);
+int32_t or_ordered_list_request_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                                    const int8_t* v_scale, const uint64_t* present,
+                                    const or_rule* rule, int32_t n_req, const int32_t* req_node,
+                                    int32_t* out_pos);
 
 /* nodeStatusForStrategy (deschedule/enforce.go:154-164): per strategy, Violated as a
  * bitmap viol_out[s][W64]. */
 int or_tas_violations(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
                       const uint64_t* present, int32_t n_strategies, const or_rule* rules,
                       const int32_t* rule_off, uint64_t* viol_out);
+int or_tas_violations_dec(int32_t n_nodes, int32_t n_metrics, const int64_t* v_milli,
+                          const int8_t* v_scale, const uint64_t* present, int32_t n_strategies,
+                          const or_rule* rules, const int32_t* rule_off, uint64_t* viol_out);
 
 /* Deschedule.updateNodeLabels (deschedule/enforce.go:99-151) per node, for S <= 64
  * registered strategies with policy names names[s] (NULL = all distinct).  The reference

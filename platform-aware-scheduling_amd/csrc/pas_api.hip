@@ -191,6 +191,7 @@ void free_tas(pas_ctx* ctx) {
   free_ptr(reinterpret_cast<void*&>(t.perm));
   free_ptr(reinterpret_cast<void*&>(t.f1k));
   free_ptr(reinterpret_cast<void*&>(t.f32));
+  free_ptr(reinterpret_cast<void*&>(t.scale_tab));
   free_ptr(t.keys_a);
   free_ptr(t.keys_b);
   free_ptr(reinterpret_cast<void*&>(t.ids_a));
@@ -439,6 +440,32 @@ static int check_tas_gen(pas_ctx* ctx, uint64_t gen) {
     return set_error(ctx, PAS_ESTALE, "TAS snapshot generation mismatch: resident " +
                                           std::to_string(ctx->tas.gen) + ", requested " +
                                           std::to_string(gen));
+  return PAS_OK;
+}
+
+int pas_tas_snapshot_set_scale(pas_ctx* ctx, uint64_t gen, int32_t n_metrics,
+                               const int32_t* col_scale, void* hip_stream) {
+  if (!ctx) return PAS_EINVAL;
+  int rc = check_tas_gen(ctx, gen);
+  if (rc) return rc;
+  const int32_t M = ctx->tas.n_metrics;
+  if (n_metrics != M || (M > 0 && !col_scale))
+    return set_error(ctx, PAS_EINVAL, "pas_tas_snapshot_set_scale: n_metrics != the snapshot's");
+  std::vector<int64_t> tab(2 * (size_t)M);
+  for (int32_t m = 0; m < M; ++m) {
+    if (col_scale[m] < 0 || col_scale[m] > 9)
+      return set_error(ctx, PAS_EINVAL, "pas_tas_snapshot_set_scale: scale outside 0..9");
+    int64_t mult = 1;
+    for (int32_t i = 0; i < col_scale[m]; ++i) mult *= 10;
+    tab[2 * (size_t)m] = mult;
+    tab[2 * (size_t)m + 1] = INT64_MAX / mult;
+  }
+  if (M == 0) return PAS_OK;
+  if ((rc = activate(ctx))) return rc;
+  hipStream_t s = pick_stream(ctx, hip_stream);
+  PAS_HIP(ctx, hipMemcpyAsync(ctx->tas.scale_tab, tab.data(), sizeof(int64_t) * tab.size(),
+                              hipMemcpyHostToDevice, s));
+  PAS_HIP(ctx, hipStreamSynchronize(s));  // tab is this call's
   return PAS_OK;
 }
 

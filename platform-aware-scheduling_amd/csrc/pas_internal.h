@@ -56,6 +56,9 @@ struct TasSnapshot {
   int32_t* perm = nullptr;
   int64_t* f1k = nullptr;  // [M][R / 1024] sorted[m][1024 a]: fences of the range search
   int64_t* f32 = nullptr;  // [M][R / 32]   sorted[m][32 b]
+  // column m holds value * 10^scale[m]: scale_tab[m] = {10^scale, INT64_MAX / 10^scale}
+  // (pas_tas_snapshot_set_scale; milli after every snapshot_set)
+  int64_t* scale_tab = nullptr;
   // build scratch (kept for column updates): sort keys {value, row} and node ids, two
   // buffers each, [M][R]; per-word popcounts and their scan; the updated rows
   void* keys_a = nullptr;
@@ -82,6 +85,19 @@ struct TasSnapshot {
 
 // Device-resident GAS snapshot (node-major):
 //   n_cards int32 [N], cap int64 [N][Q], used int64 [N][K][Q]
+// core.EvaluateRule's CmpInt64 (operator.go:16-22) against column m's fixed point: the
+// integer target * 10^scale[m] in *tm (0), or the saturation when that is past int64: +1 above
+// every value, -1 below every value.  A column at scale 0 never saturates
+// below: its values are ParseQuantity's, >= -(2^63 - 1).
+__device__ __forceinline__ int target_scaled(int64_t t, const int64_t* __restrict__ scale_tab,
+                                             int32_t m, int64_t* tm) {
+  const int64_t mult = scale_tab[2 * m], maxq = scale_tab[2 * m + 1];
+  if (t > maxq) return 1;
+  if (t < -maxq) return -1;
+  *tm = t * mult;
+  return 0;
+}
+
 struct GasSnapshot {
   bool valid = false;
   uint64_t gen = 0;

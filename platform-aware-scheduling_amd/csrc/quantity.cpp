@@ -297,29 +297,60 @@ int pas_quantity_as_int64(const char* quantity, int64_t* out) {
   return PAS_OK;
 }
 
-int pas_quantity_to_milli(const char* quantity, int64_t* milli_out) {
-  if (!milli_out) return PAS_EINVAL;
+int pas_quantity_to_scaled(const char* quantity, int32_t places, int64_t* out) {
+  if (!out || places < 0 || places > 9) return PAS_EINVAL;
   Parsed q;
   const int rc = pas::parse_quantity(quantity, &q);
   if (rc != PAS_OK) return rc;
-  __int128 milli;
-  if (q.dec) {
-    if (q.nano % 1000000 != 0) return PAS_ENOTEXACT;
-    milli = q.nano / 1000000;
-  } else {
-    milli = q.value;
-    int32_t e = q.scale + 3;
+  __int128 v;
+  if (q.dec) {  // units of 1e-9 -> units of 10^-places
+    __int128 div = 1;
+    for (int32_t i = places; i < 9; ++i) div *= 10;
+    if (q.nano % div != 0) return PAS_ENOTEXACT;
+    v = q.nano / div;
+  } else {  // value * 10^(scale + places)
+    v = q.value;
+    int32_t e = q.scale + places;
     for (; e > 0; --e) {
-      milli *= 10;
-      if (milli > INT64_MAX || milli < INT64_MIN) return PAS_ENOTEXACT;
+      v *= 10;
+      if (v > INT64_MAX || v < INT64_MIN) return PAS_ENOTEXACT;
     }
     for (; e < 0; ++e) {
-      if (milli % 10 != 0) return PAS_ENOTEXACT;
-      milli /= 10;
+      if (v % 10 != 0) return PAS_ENOTEXACT;
+      v /= 10;
     }
   }
-  if (milli > INT64_MAX || milli < INT64_MIN) return PAS_ENOTEXACT;
-  *milli_out = (int64_t)milli;
+  if (v > INT64_MAX || v < INT64_MIN) return PAS_ENOTEXACT;
+  *out = (int64_t)v;
+  return PAS_OK;
+}
+
+int pas_quantity_to_milli(const char* quantity, int64_t* milli_out) {
+  return pas_quantity_to_scaled(quantity, 3, milli_out);
+}
+
+int pas_quantity_decimals(const char* quantity, int32_t* places) {
+  if (!places) return PAS_EINVAL;
+  Parsed q;
+  const int rc = pas::parse_quantity(quantity, &q);
+  if (rc != PAS_OK) return rc;
+  int32_t k = 0;
+  if (q.dec) {  // 9 minus the trailing zero digits of the nano value
+    __int128 n = q.nano;
+    k = 9;
+    while (k > 0 && n % 10 == 0) {
+      n /= 10;
+      --k;
+    }
+  } else if (q.scale < 0) {  // -scale minus the trailing zero digits of the value
+    int64_t v = q.value;
+    k = -q.scale;
+    while (k > 0 && v % 10 == 0) {
+      v /= 10;
+      --k;
+    }
+  }
+  *places = k;
   return PAS_OK;
 }
 

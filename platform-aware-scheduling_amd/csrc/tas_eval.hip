@@ -56,17 +56,6 @@ __device__ __forceinline__ uint64_t tail_mask64(int32_t c, int32_t n) {
   return (1ull << (n - lo)) - 1ull;
 }
 
-// target * 1000 with saturation: +1 (above every int64 milli value), -1 (below every
-// value) or 0 with *tm exact.
-__device__ __forceinline__ int target_milli(int64_t t, int64_t* tm) {
-  constexpr int64_t kMax = INT64_MAX / 1000;
-  constexpr int64_t kMin = INT64_MIN / 1000;
-  if (t > kMax) return 1;
-  if (t < kMin) return -1;
-  *tm = t * 1000;
-  return 0;
-}
-
 __device__ __forceinline__ int order_of(int32_t op) {
   return op == PAS_OP_GREATER_THAN ? kOrderDesc : op == PAS_OP_LESS_THAN ? kOrderAsc : kOrderIndex;
 }
@@ -117,6 +106,7 @@ struct RangesParams {
   const int64_t* f1k;     // [M][R / 1024] sorted[m][1024 a]
   const int64_t* f32;     // [M][R / 32]   sorted[m][32 b]
   int2* ranges;
+  const int64_t* scale_tab;  // [M][2] the columns' fixed point (target_scaled)
 };
 
 constexpr int kRuleLanes = 8;  // lanes per rule in the range search
@@ -157,7 +147,7 @@ __device__ void ranges_group(const RangesParams& R, int32_t r) {
     const int32_t m = rule.metric;
     const int32_t c = R.cnt[m];
     int64_t t = 0;
-    const int sat = target_milli(rule.target, &t);
+    const int sat = target_scaled(rule.target, R.scale_tab, m, &t);
     int32_t lb, ub;
     if (sat != 0) {
       lb = ub = sat > 0 ? c : 0;
@@ -694,7 +684,8 @@ template <int kRun, bool kPlan = false>
 __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
     const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
-    const uint64_t* __restrict__ present, uint64_t* __restrict__ viol_out, PlanOut plan) {
+    const uint64_t* __restrict__ present, const int64_t* __restrict__ scale_tab,
+    uint64_t* __restrict__ viol_out, PlanOut plan) {
   static_assert(kRun <= 64, "one word per lane");
   __shared__ int64_t red[kPlan ? kWaves : 1];
   __shared__ uint64_t vws[kPlan ? kWaves : 1][kPlan ? 64 : 1][kPlan ? kRun : 1];
@@ -762,7 +753,7 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     load(ru1, nv, &npr);  // the next run in flight during this rule's compares
     if (ru.metric >= 0 && ru.metric < M && ru.op >= 0 && ru.op <= 2) {
       int64_t tm = 0;
-      const int sat = target_milli(ru.target, &tm);
+      const int sat = target_scaled(ru.target, scale_tab, ru.metric, &tm);
 #pragma unroll
       for (int k = 0; k < kRun; ++k) {
         const bool valid = (gw0 + k) * 64 + lane < N;
@@ -912,7 +903,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   timing_begin(ctx, s, PAS_K_TAS_SPAN, &span);
   // ranges (blocks 1..) beside the grouping (block 0), one launch
   const int32_t range_rules = (flags & PAS_TAS_FILTER) ? n_rules : 0;
-  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges};
+  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges,
+                  t.scale_tab};
   GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, tune.no_group};
   const size_t group_lds = sizeof(int32_t) * ((size_t)G + 1 + (size_t)M);  // hist | cnt
   if (group_lds > 64 * 1024)
@@ -977,7 +969,8 @@ int tas_group_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_prio,
     return set_error(ctx, PAS_ECAPACITY, "more than 4096 metric columns");
   const uint32_t flags = PAS_TAS_FILTER | PAS_TAS_PRIORITIZE;
   const int32_t range_rules = d_ranges ? n_rules : 0;
-  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges};
+  RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges,
+                  t.scale_tab};
   GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, 0};
   const size_t group_lds = sizeof(int32_t) * ((size_t)3 * M + 1 + (size_t)M);
   if (group_lds > 64 * 1024)
@@ -1006,8 +999,8 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   const int32_t per = (run == 2 || run == 4 || run == 16) ? run : 8;
   const int32_t rwaves = (W64 + per - 1) / per;
   rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
-      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol,
-      PlanOut{NamePlan{}, nullptr, nullptr, nullptr, nullptr});
+      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, t.scale_tab,
+      d_viol, PlanOut{NamePlan{}, nullptr, nullptr, nullptr, nullptr});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
@@ -1039,7 +1032,7 @@ int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_VIOLATIONS, &tl);
   tas_violations_run_kernel<kRun, true><<<blocks, kTpb, 0, s>>>(
-      N, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, d_viol,
+      N, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, t.scale_tab, d_viol,
       PlanOut{names, d_labels, d_add, d_rem, part});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());

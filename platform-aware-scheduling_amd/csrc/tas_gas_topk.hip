@@ -56,6 +56,7 @@ struct LazyTopkParams {
   const int64_t* sorted;  // [M][R] ascending present values; fences f1k [M][R/1024], f32
   const int64_t* f1k;
   const int64_t* f32;
+  const int64_t* scale_tab;  // [M][2] the columns' fixed point (target_scaled)
   // GAS snapshot (same nodes) and the pods' requests
   int32_t K, Q, C, i915;
   const int32_t* n_cards;
@@ -69,14 +70,6 @@ struct LazyTopkParams {
   int32_t* len_out;       // [P]
 };
 
-__device__ __forceinline__ int target_milli(int64_t t, int64_t* tm) {
-  constexpr int64_t kMax = INT64_MAX / 1000;
-  constexpr int64_t kMin = INT64_MIN / 1000;
-  if (t > kMax) return 1;
-  if (t < kMin) return -1;
-  *tm = t * 1000;
-  return 0;
-}
 
 __device__ __forceinline__ int64_t order_key(int32_t op, int64_t v) {
   return op == PAS_OP_GREATER_THAN ? ~v : op == PAS_OP_LESS_THAN ? v : 0;
@@ -237,10 +230,12 @@ struct alignas(16) LazyRule {
   uint64_t span;
 };
 
-__device__ __forceinline__ void compile_rule(const pas_rule& ru, int32_t M, int32_t* metric,
-                                             LazyRule* out) {
+__device__ __forceinline__ void compile_rule(const pas_rule& ru, int32_t M,
+                                             const int64_t* __restrict__ scale_tab,
+                                             int32_t* metric, LazyRule* out) {
   int64_t tm = 0;
-  const int sat = target_milli(ru.target, &tm);
+  const int sat = target_scaled(ru.target, scale_tab, (ru.metric >= 0 && ru.metric < M)
+                                                          ? ru.metric : 0, &tm);
   int64_t lo = 0, hi = -1;  // empty
   if (ru.metric >= 0 && ru.metric < M) {
     if (ru.op == PAS_OP_LESS_THAN) {
@@ -332,7 +327,7 @@ void tas_gas_topk_kernel(LazyTopkParams a) {
     ru.target = __shfl(ru_l.target, src, 64);
     const bool same = (sm >> src) & 1ull;
     int64_t tm = 0;
-    const int sat = target_milli(ru.target, &tm);
+    const int sat = target_scaled(ru.target, a.scale_tab, same ? pr.metric : 0, &tm);
     int32_t lb = 0, ub = 0;
     half_bounds(a, same ? pr.metric : 0, same ? c0 : 0, tm, sub, half_mask, &lb, &ub);
     if (sat != 0) lb = ub = sat > 0 ? c0 : 0;
@@ -362,7 +357,7 @@ void tas_gas_topk_kernel(LazyTopkParams a) {
   if (staged) {
     LazyRule cr{0, 0};
     int32_t cm = -1;
-    if (have && r0 + sub < r1) compile_rule(a.rules[r0 + sub], a.M, &cm, &cr);
+    if (have && r0 + sub < r1) compile_rule(a.rules[r0 + sub], a.M, a.scale_tab, &cm, &cr);
     srule[pslot][sub] = cr;
     smetric[pslot][sub] = cm;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
@@ -437,7 +432,7 @@ void tas_gas_topk_kernel(LazyTopkParams a) {
         if (rb + u >= r1 || rule.metric < 0 || rule.metric >= a.M || rule.op < 0 || rule.op > 2)
           continue;
         int64_t tm = 0;
-        const int sat = target_milli(rule.target, &tm);
+        const int sat = target_scaled(rule.target, a.scale_tab, rule.metric, &tm);
         bool hit;
         if (rule.op == PAS_OP_LESS_THAN) hit = sat > 0 || (sat == 0 && v[u] < tm);
         else if (rule.op == PAS_OP_GREATER_THAN) hit = sat < 0 || (sat == 0 && v[u] > tm);
@@ -562,6 +557,7 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
   a.sorted = t.sorted;
   a.f1k = t.f1k;
   a.f32 = t.f32;
+  a.scale_tab = t.scale_tab;
   a.K = g.max_cards;
   a.Q = g.n_res;
   a.C = max_containers;

@@ -181,6 +181,14 @@ int build_columns(pas_ctx* ctx, int32_t C, const int32_t* d_rows, const int64_t*
 
 }  // namespace
 
+__global__ void scale_fill_kernel(int64_t* tab, int32_t M) {
+  const int32_t m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m < M) {
+    tab[2 * m] = 1000;
+    tab[2 * m + 1] = INT64_MAX / 1000;
+  }
+}
+
 int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
                        const int64_t* d_vals, const uint64_t* d_present, hipStream_t s) {
   TasSnapshot& t = ctx->tas;
@@ -213,6 +221,7 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     PAS_HIP(ctx, hipMalloc(&t.popc, sizeof(uint32_t) * (mw + 1)));
     PAS_HIP(ctx, hipMalloc(&t.word_scan, sizeof(uint32_t) * (mw + 1)));
     PAS_HIP(ctx, hipMalloc(&t.rows, sizeof(int32_t) * mm));
+    PAS_HIP(ctx, hipMalloc(&t.scale_tab, sizeof(int64_t) * 2 * mm));
     // temp storage for the largest (whole-snapshot) sort and scan
     size_t sort_bytes = 0, scan_bytes = 0;
     SortKey* ka = static_cast<SortKey*>(t.keys_a);
@@ -231,6 +240,9 @@ int tas_snapshot_build(pas_ctx* ctx, uint64_t gen, int32_t N, int32_t M,
     t.row = R;
   }
   if (M > 0) {
+    // every column milli until pas_tas_snapshot_set_scale says otherwise
+    scale_fill_kernel<<<(M + 255) / 256, 256, 0, s>>>(t.scale_tab, M);
+    PAS_HIP(ctx, hipGetLastError());
     if (MN > 0 && d_vals != t.vals)
       PAS_HIP(ctx, hipMemcpyAsync(t.vals, d_vals, sizeof(int64_t) * MN,
                                   hipMemcpyDeviceToDevice, s));

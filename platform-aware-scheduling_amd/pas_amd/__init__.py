@@ -8,12 +8,14 @@ from . import _lib
 from ._lib import (PAS_OP_EQUALS, PAS_OP_GREATER_THAN, PAS_OP_LESS_THAN, PAS_TAS_FILTER,
                    PAS_TAS_PRIORITIZE, PasError)
 from .context import (RULE_DTYPE, Context, label_patch_json, make_rules, parse_operator,
-                      quantity_as_int64, quantity_to_milli, w64)
+                      quantity_as_int64, quantity_decimals, quantity_to_milli,
+                      quantity_to_scaled, w64)
 
 LIB = _lib.load()
 
 __all__ = [
     "Context", "PasError", "RULE_DTYPE", "make_rules", "parse_operator", "quantity_to_milli",
+    "quantity_to_scaled", "quantity_decimals",
     "quantity_as_int64", "w64", "label_patch_json", "PAS_OP_LESS_THAN", "PAS_OP_GREATER_THAN", "PAS_OP_EQUALS",
     "PAS_TAS_FILTER", "PAS_TAS_PRIORITIZE", "LIB",
 ]

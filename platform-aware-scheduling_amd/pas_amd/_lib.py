@@ -119,12 +119,15 @@ SIGNATURES = {
     "pas_parse_operator": (c_int, [c_char_p]),
     "pas_quantity_to_milli": (c_int, [c_char_p, POINTER(c_int64)]),
     "pas_quantity_as_int64": (c_int, [c_char_p, POINTER(c_int64)]),
+    "pas_quantity_to_scaled": (c_int, [c_char_p, c_int32, POINTER(c_int64)]),
+    "pas_quantity_decimals": (c_int, [c_char_p, POINTER(c_int32)]),
     "pas_tas_snapshot_set": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P]),
     "pas_tas_snapshot_set_device": (c_int, [_P, c_uint64, c_int32, c_int32, _P, _P, _P]),
     "pas_tas_snapshot_update": (c_int, [_P, c_uint64, c_uint64, c_int32, _P, _P, _P]),
     "pas_tas_snapshot_update_device": (
         c_int, [_P, c_uint64, c_uint64, c_int32, _P, _P, _P, _P]),
     "pas_tas_snapshot_info":(c_int, [_P, POINTER(c_uint64), POINTER(c_int32), POINTER(c_int32)]),
+    "pas_tas_snapshot_set_scale": (c_int, [_P, c_uint64, c_int32, _P, _P]),
     "pas_tas_eval": (c_int, [_P, c_uint64, c_int32, _P, _P, _P, _P, c_uint32, _P, _P, _P]),
     "pas_tas_prioritize_request": (c_int, [_P, c_uint64, _P, c_int32, _P, _P, _P]),
     "pas_tas_prioritize_request_device": (c_int, [_P, c_uint64, _P, c_int32, _P, _P, _P, _P]),

@@ -72,6 +72,25 @@ def quantity_to_milli(q: str) -> int:
     return out.value
 
 
+def quantity_to_scaled(q: str, places: int) -> int:
+    """Exact value * 10^places (0..9) of a resource.Quantity string; PasError(PAS_ENOTEXACT)
+    when that is not an integer or is outside int64."""
+    out = c_int64()
+    rc = _lib.load().pas_quantity_to_scaled(q.encode(), places, byref(out))
+    if rc != _lib.PAS_OK:
+        raise PasError(rc, f"quantity {q!r} at 10^-{places}")
+    return out.value
+
+
+def quantity_decimals(q: str) -> int:
+    """The fewest decimal places (0..9) that hold the parsed quantity exactly."""
+    out = ctypes.c_int32()
+    rc = _lib.load().pas_quantity_decimals(q.encode(), byref(out))
+    if rc != _lib.PAS_OK:
+        raise PasError(rc, f"quantity {q!r}")
+    return out.value
+
+
 def quantity_as_int64(q: str) -> int:
     """resource.Quantity.AsInt64 with `ok` ignored (gpuscheduler/utils.go:23)."""
     out = c_int64()
@@ -161,7 +180,9 @@ class Context:
         self._check(self._l.pas_reset_timing(self._h), "pas_reset_timing")
 
     # ------------------------------------------------------------------ TAS
-    def tas_snapshot_set(self, gen: int, v_milli: np.ndarray, present: np.ndarray):
+    def tas_snapshot_set(self, gen: int, v_milli: np.ndarray, present: np.ndarray,
+                         scale=None):
+        """Columns of value * 1000, or of value * 10^scale[m] (pas_tas_snapshot_set_scale)."""
         v = np.ascontiguousarray(v_milli, dtype=np.int64)
         m, n = v.shape
         p = np.ascontiguousarray(present, dtype=np.uint64)
@@ -169,6 +190,16 @@ class Context:
         self._check(self._l.pas_tas_snapshot_set(self._h, gen, n, m, _ptr(v), _ptr(p)),
                     "pas_tas_snapshot_set")
         self.n_nodes, self.n_metrics = n, m
+        if scale is not None:
+            self.tas_snapshot_set_scale(gen, scale)
+
+    def tas_snapshot_set_scale(self, gen: int, scale, stream=None):
+        """Decimal scale per column (0..9): column m holds value * 10^scale[m]."""
+        sc = np.ascontiguousarray(scale, dtype=np.int32)
+        self._check(self._l.pas_tas_snapshot_set_scale(self._h, gen, len(sc),
+                                                       _ptr(sc) if sc.size else None,
+                                                       _stream(stream)),
+                    "pas_tas_snapshot_set_scale")
 
     def tas_snapshot_set_device(self, gen: int, n_nodes: int, n_metrics: int, v_t, p_t,
                                 stream=None):

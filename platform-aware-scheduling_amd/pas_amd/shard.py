@@ -6,7 +6,7 @@ Every reference computation on the path is per node given the snapshot: the filt
 the prioritize order (core.OrderedList, operator.go:30-42) is global.  So each rank holds a
 contiguous node range of the cluster as its resident snapshot and:
 
-  * top-k prioritize: evaluates every pod against its shard, keeps the first k entries of
+  * top-k prioritize: evaluates every pod (of its pod group, GridTopK) against its shard, keeps the first k entries of
     the shard's HostPriorityList as (key, global node) records (pas_tas_topk_device, or
     pas_tas_gas_topk_device for TAS + GAS), the records of all ranks are all-gathered over
     RCCL, and every rank merges them into the exact global first k (pas_topk_merge_device);
@@ -42,21 +42,22 @@ def node_range(n_total: int, world: int, rank: int, align: int = 64) -> Tuple[in
     return n0, n1
 
 
-def _all_gather(t: torch.Tensor, world: int) -> torch.Tensor:
-    """[world * t.numel()] concatenation of every rank's `t` (same shape on all ranks)."""
+def _all_gather(t: torch.Tensor, world: int, group=None) -> torch.Tensor:
+    """[world * t.numel()] concatenation of every rank's `t` (same shape on all ranks) over
+    `group` (a torch.distributed process group of `world` ranks; None = the default group)."""
     if not collective(world):
         return t.reshape(-1)
     import torch.distributed as dist
     flat = t.contiguous().reshape(-1)
-    if dist.get_backend() == "nccl":
+    if dist.get_backend(group) == "nccl":
         out = torch.empty(world * flat.numel(), dtype=flat.dtype, device=flat.device)
         CALLS["all_gather_into_tensor"] += 1
-        dist.all_gather_into_tensor(out, flat)
+        dist.all_gather_into_tensor(out, flat, group=group)
         return out
     host = flat.cpu()
     parts = [torch.empty_like(host) for _ in range(world)]
     CALLS["all_gather"] += 1
-    dist.all_gather(parts, host)
+    dist.all_gather(parts, host, group=group)
     return torch.cat(parts).to(flat.device)
 
 
@@ -152,12 +153,15 @@ class ShardedTopK:
 
     The rank's Context holds the snapshot of nodes [node_base, node_base + n_local);
     `run` returns (nodes [P][k] int32 global node ids, -1 past len; lens [P] int32), the
-    same on every rank."""
+    same on every rank of `group` (a process group of `world` ranks, the node shards of the
+    cluster; None = the default group)."""
 
-    def __init__(self, ctx, k: int, world: int, rank: int, node_base: int, device="cuda"):
+    def __init__(self, ctx, k: int, world: int, rank: int, node_base: int, device="cuda",
+                 group=None):
         self.ctx, self.k, self.world, self.rank = ctx, k, world, rank
         self.node_base = node_base
         self.device = device
+        self.group = group
         self._bufs = {}
 
     def _buf(self, name, shape, dtype):
@@ -200,8 +204,8 @@ class ShardedTopK:
         records(key, node, ln, stream)
         if on_gpu and stream != cur:
             cur.wait_stream(stream)  # records written before the all-gather reads them
-        keys_all = _all_gather(key, self.world)
-        nodes_all = _all_gather(node, self.world)
+        keys_all = _all_gather(key, self.world, self.group)
+        nodes_all = _all_gather(node, self.world, self.group)
         if on_gpu and stream != cur:
             stream.wait_stream(cur)  # gathered records complete before the merge reads them
         out_node = self._buf("out_node", (n_pods, k), torch.int32)
@@ -213,65 +217,115 @@ class ShardedTopK:
         return out_node, out_len
 
 
-class PodShardedTopK:
-    """The combined TAS + GAS top-k (BASELINE configs[4]) split by pod instead of by node: every
-    rank holds the WHOLE cluster as its resident TAS and GAS snapshots (1M nodes x 64 metrics
-    is ~3 GB with the orders: it fits one GPU many times over) and evaluates the pods of its
-    pod_slice only, so a step has no data-path collective and each rank's kernel walks P / N
-    pods.  Each pod's list is final on the rank that owns it (a pod is one scheduling request,
-    telemetryscheduler.go:184-225, gpuscheduler/scheduler.go:449-482); `gather` assembles
-    every rank's slice once, at the end.  Node sharding (ShardedTopK) stays the path for a
-    cluster that exceeds one GPU's memory.
+def grid_position(world: int, node_shards: int, rank: int) -> Tuple[int, int]:
+    """(pod group, node shard) of `rank` in a node_shards x (world / node_shards) grid: the
+    node shards of one pod group are consecutive ranks."""
+    if node_shards < 1 or world % node_shards:
+        raise ValueError(f"node_shards={node_shards} must divide world={world}")
+    return rank // node_shards, rank % node_shards
+
+
+def snapshot_bytes_per_node(n_metrics: int, cards: int = 8, kinds: int = 3) -> int:
+    """Device bytes per node of the resident state a C5 rank holds (tas_snapshot.hip /
+    gas_fit.hip): TAS columns 8 M + presence M / 8, the sorted values 8 M, three orders 12 M,
+    the build's sort keys and ids 40 M, the lazy top-k's node-major copies 8 M + M / 8; GAS
+    capacity 8 Q, usage and the card-major free table 16 K Q, card count 4."""
+    return 76 * n_metrics + (n_metrics + 31) // 32 * 8 + 8 * kinds + 16 * cards * kinds + 4
+
+
+def min_node_shards(world: int, n_nodes: int, n_metrics: int, cards: int = 8, kinds: int = 3,
+                    budget_bytes: float = None) -> int:
+    """The fewest node shards s (a divisor of world) whose per-rank snapshot fits
+    `budget_bytes` (default: half of the device's memory, else 144 GB = half of an MI355X's
+    288 GB): 1 for every BASELINE config (1M nodes x 64 metrics is ~5 GB)."""
+    if budget_bytes is None:
+        total = 288e9
+        if torch.cuda.is_available():
+            total = torch.cuda.get_device_properties(0).total_memory
+        budget_bytes = total / 2
+    per_node = snapshot_bytes_per_node(n_metrics, cards, kinds)
+    for s in range(1, world + 1):
+        if world % s == 0:
+            n0, n1 = node_range(n_nodes, s, 0)
+            if (n1 - n0) * per_node <= budget_bytes:
+                return s
+    return world
+
+
+def pod_batch_slice(p0: int, p1: int, rules, rule_off, prio, req, mask, ncont):
+    """Host arrays of pods [p0, p1) of a TAS + GAS batch, rule offsets rebased to 0."""
+    r0, r1 = int(rule_off[p0]), int(rule_off[p1])
+    return (rules[r0:r1], (rule_off[p0:p1 + 1] - r0).astype(rule_off.dtype), prio[p0:p1],
+            req[p0:p1], mask[p0:p1], ncont[p0:p1])
+
+
+class GridTopK:
+    """The combined TAS + GAS top-k (BASELINE configs[4]) over a 2-D split: node_shards = s
+    node shards x g = world / s pod groups.  Rank r is node shard r % s
+    of pod group r // s: its Context holds nodes node_range(N, s, r % s) of the cluster as the
+    resident TAS and GAS snapshots, and it evaluates the pods of pod_slice(P, g, r // s) only.
+    Each step the group's s ranks all-gather their records over the group's process group and
+    merge them into the group's pods' final lists (identical on those s ranks); groups never
+    talk during a step (a pod is one scheduling request, telemetryscheduler.go:184-225,
+    gpuscheduler/scheduler.go:449-482).  Per-rank kernel work is (P / g) pods x (N / s) nodes.
+    s = 1 is pure pod sharding (no step collective; the snapshot replicated), s = world pure
+    node sharding (ShardedTopK); min_node_shards picks the fewest shards the memory needs.
+    `gather` assembles every group's lists once, at the end.
 
     rules / rule_off / prio / req / mask / ncont: host arrays of the WHOLE batch; the rank's
-    slice is cut out here (rule_off rebased), once."""
+    pod slice is cut out here, once.  Every rank constructs every group's process group (a
+    collective call), in the same order."""
 
-    def __init__(self, ctx, k: int, world: int, rank: int, n_pods: int, rules, rule_off, prio,
-                 req, mask, ncont, device="cuda"):
+    def __init__(self, ctx, k: int, world: int, rank: int, node_shards: int, n_pods: int,
+                 n_nodes: int, rules, rule_off, prio, req, mask, ncont, device="cuda"):
         import numpy as np
         self.ctx, self.k, self.world, self.rank = ctx, k, world, rank
+        self.s = node_shards
+        self.g = world // node_shards
+        self.group_id, self.shard_id = grid_position(world, node_shards, rank)
+        self.n0, self.n1 = node_range(n_nodes, self.s, self.shard_id)
         self.n_pods = n_pods
-        self.p0, self.p1 = pod_slice(n_pods, world, rank)
-        self.per = (n_pods + world - 1) // world
-        p0, p1 = self.p0, self.p1
-        r0, r1 = int(rule_off[p0]), int(rule_off[p1])
+        self.p0, self.p1 = pod_slice(n_pods, self.g, self.group_id)
+        self.per = (n_pods + self.g - 1) // self.g
+        pg = None
+        if collective(world) and 1 < self.s < world:
+            import torch.distributed as dist
+            for gi in range(self.g):  # every rank creates every group, in order
+                grp = dist.new_group(list(range(gi * self.s, (gi + 1) * self.s)))
+                if gi == self.group_id:
+                    pg = grp
+        self.topk = ShardedTopK(ctx, k, self.s, self.shard_id, self.n0, device, group=pg)
 
         def dev(a):
             return torch.from_numpy(np.ascontiguousarray(a)).to(device)
-        self.n_rules = r1 - r0
-        self.rules = dev(rules[r0:r1].view(np.uint8))
-        self.off = dev((rule_off[p0:p1 + 1] - r0).astype(np.int32))
-        self.prio = dev(prio[p0:p1].view(np.uint8))
-        self.req, self.ncont = dev(req[p0:p1]), dev(ncont[p0:p1])
-        self.mask = dev(mask[p0:p1].view(np.int32))
+        r, off, pr, rq, mk, nc = pod_batch_slice(self.p0, self.p1, rules, rule_off, prio, req,
+                                                 mask, ncont)
+        self.n_rules = len(r)
+        self.rules, self.off, self.prio = dev(r.view(np.uint8)), dev(off), dev(pr.view(np.uint8))
+        self.req, self.mask, self.ncont = dev(rq), dev(mk.view(np.int32)), dev(nc)
         self.C = req.shape[1]
-        n = p1 - p0
-        self.key = torch.empty((n, k), dtype=torch.int64, device=device)
-        self.node = torch.empty((n, k), dtype=torch.int32, device=device)
-        self.len = torch.empty((n,), dtype=torch.int32, device=device)
-        # the slice padded to `per` rows for the final gather
+        # the group's lists padded to `per` rows for the final gather
         self.out_node = torch.full((self.per, k), -1, dtype=torch.int32, device=device)
         self.out_len = torch.zeros((self.per,), dtype=torch.int32, device=device)
 
     def run(self, tas_gen: int, gas_gen: int, i915_index: int, stream=None):
-        """One step: the rank's pods' first k (their final lists, node ids, -1 past len)."""
+        """One step: the group's pods' first k (final lists: node ids, -1 past len)."""
         n = self.p1 - self.p0
         if n:
-            self.ctx.tas_gas_topk_device(tas_gen, gas_gen, n, self.n_rules, self.rules, self.off,
-                                         self.prio, None, self.C, i915_index, self.req, self.mask,
-                                         self.ncont, self.k, 0, self.key, self.node, self.len,
-                                         stream)
-            # records -> node lists (one shard: the merge only maps the sentinels to -1)
-            self.ctx.topk_merge_device(n, self.k, 1, self.key, self.node, self.out_node[:n],
-                                       self.out_len[:n], stream)
+            nodes, lens = self.topk.run_tas_gas(tas_gen, gas_gen, n, self.n_rules, self.rules,
+                                                self.off, self.prio, self.C, i915_index,
+                                                self.req, self.mask, self.ncont, None, stream)
+            self.out_node[:n], self.out_len[:n] = nodes, lens
         return self.out_node[:n], self.out_len[:n]
 
     def gather(self):
-        """Every pod's list on every rank ([P][k], [P]): one all-gather of the slices (end of
-        the job, not per step)."""
-        nodes = _all_gather(self.out_node, self.world).view(-1, self.k)[:self.n_pods]
-        lens = _all_gather(self.out_len, self.world)[:self.n_pods]
-        return nodes, lens
+        """Every pod's list on every rank ([P][k], [P]): one all-gather of the groups' lists
+        (shard 0 of each group), at the end of the job, not per step."""
+        nodes = _all_gather(self.out_node, self.world).view(self.world, self.per, self.k)
+        lens = _all_gather(self.out_len, self.world).view(self.world, self.per)
+        first = torch.arange(0, self.world, self.s, device=nodes.device)
+        return (nodes[first].reshape(-1, self.k)[:self.n_pods],
+                lens[first].reshape(-1)[:self.n_pods])
 
 
 _PAD = {}  # gather_violations' padded rows of a narrower last shard, by shape and device

@@ -4,8 +4,10 @@ per cache refresh; it is restated here so the whole path can be exercised from t
 reference's own data shapes (metric maps of Quantity strings, node labels, usage maps).
 
 TAS (cache/autoupdating.go:76-85, metrics/client.go:25-32): one column per metric name, one
-row bit per node that has the metric, value * 1000 exact (pas_quantity_to_milli); values
-that are not milli-exact are reported and keep that metric on the CPU path.
+row bit per node that has the metric, value * 10^scale exact (pas_quantity_to_scaled) with the
+column's scale the most decimal places among its values (at least 3, milli): ParseQuantity
+keeps at most 9, so every column is exact unless its range at that scale passes int64
+(pas_tas_snapshot_set_scale).
 
 GAS (gpuscheduler/scheduler.go:132-178, 269-275; node_resource_cache.go:474-491):
   cards      strings.Split(label "gpu.intel.com/cards", ".") -- duplicates and empty names
@@ -25,7 +27,7 @@ from typing import Dict, List, Mapping, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from .context import quantity_as_int64, quantity_to_milli, w64
+from .context import quantity_as_int64, quantity_decimals, quantity_to_scaled, w64
 
 GPU_LIST_LABEL = "gpu.intel.com/cards"
 RESOURCE_PREFIX = "gpu.intel.com/"
@@ -34,28 +36,32 @@ RESOURCE_PREFIX = "gpu.intel.com/"
 def tas_snapshot_from_metrics(metrics: Mapping[str, Mapping[str, str]],
                               node_names: Sequence[str],
                               metric_names: Optional[Sequence[str]] = None):
-    """(v_milli [M][N] int64, present [M][W64] uint64, inexact [(metric, node)]) from
-    {metric: {node: quantity string}}.  Nodes not in node_names are ignored."""
+    """(v [M][N] int64, present [M][W64] uint64, scale [M] int32) from {metric: {node:
+    quantity string}}: column m holds value * 10^scale[m] exactly, scale[m] the most decimal
+    places among the column's values (pas_quantity_decimals; 3 for a column of milli-exact
+    values or none), for Context.tas_snapshot_set(gen, v, present, scale).  Nodes not in
+    node_names are ignored.  A column whose values need more range than int64 at that scale
+    raises PasError(PAS_ENOTEXACT) naming the metric: no value is dropped."""
     metric_names = list(metrics) if metric_names is None else list(metric_names)
     index = {n: i for i, n in enumerate(node_names)}
     n, m = len(node_names), len(metric_names)
     v = np.zeros((m, n), np.int64)
     present = np.zeros((m, w64(n)), np.uint64)
-    inexact: List[Tuple[str, str]] = []
+    scale = np.full(m, 3, np.int32)
     for j, name in enumerate(metric_names):
-        for node, q in metrics.get(name, {}).items():
-            i = index.get(node)
-            if i is None:
-                continue
+        items = [(index[node], q) for node, q in metrics.get(name, {}).items() if node in index]
+        k = max([quantity_decimals(q) for _, q in items], default=0)
+        scale[j] = max(k, 3)  # milli unless a value needs more places
+        for i, q in items:
             try:
-                v[j, i] = quantity_to_milli(q)
+                v[j, i] = quantity_to_scaled(q, int(scale[j]))
             except _lib.PasError as e:
                 if e.code != _lib.PAS_ENOTEXACT:
                     raise
-                inexact.append((name, node))
-                continue
+                raise _lib.PasError(e.code, f"metric {name!r}: {q!r} at 10^-{scale[j]} is "
+                                            "outside int64") from None
             present[j, i >> 6] |= np.uint64(1 << (i & 63))
-    return v, present, inexact
+    return v, present, scale
 
 
 def go_sort_strings(names):

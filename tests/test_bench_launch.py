@@ -81,12 +81,15 @@ def test_multi_rank_bench_carries_node_sharded_record():
     assert out["n_gpus"] == 2 and out["config"]["world_size"] == 2
     ns = out["node_sharded"]
     assert ns["world_size"] == 2 and ns["backend"] == "gloo" and ns["nodes"] == 60000
+    # the 2-D split (shard.GridTopK) at the memory-minimal shard count: 1 node shard x 2 pod
+    # groups (pure pod sharding), and at 2 x 1 (pure node sharding); the same lists
     c5 = ns["c5_topk"]
-    assert c5["pods"] == 1024 and c5["nodes_per_gpu"] == 30016 and c5["ranks_agree"]
+    assert c5["node_shards"] == 1 and c5["pod_groups"] == 2
+    assert c5["pods_per_gpu"] == 512 and c5["nodes_per_gpu"] == 60000
     assert c5["ms_per_step"] > 0 and 0 < c5["entries"] <= 1024 * 16
+    nsh = ns["c5_topk_node_sharded"]
+    assert nsh["node_shards"] == 2 and nsh["pods_per_gpu"] == 1024
+    assert nsh["nodes_per_gpu"] == 30016 and nsh["ms_per_step"] > 0
+    assert ns["splits_agree"] is True
     c4 = ns["c4_deschedule"]
     assert c4["nodes_per_gpu"] == 30016 and c4["ms_per_step"] > 0
-    # the same C5 step split by pod over the replicated cluster: same lists on every rank
-    ps = ns["c5_topk_pod_sharded"]
-    assert ps["pods"] == 1024 and ps["pods_per_gpu"] == 512 and ps["nodes_per_gpu"] == 60000
-    assert ps["ms_per_step"] > 0 and ps["equals_node_sharded"] is True

@@ -159,6 +159,54 @@ class _C5:
         return out_node, out_len, (fits[0] if fits else None)
 
 
+    def run_grid(self, node_shards, pod_groups):
+        """The GridTopK split simulated on one GPU: pod group gi's pods (pod_slice) over each of
+        the node_shards ranges (pod_batch_slice of the batch, rules rebased), the lazy combined
+        top-k per (group, shard) in a context of its own, merged within the group; the groups'
+        lists concatenated ([P][k], [P])."""
+        from pas_amd.shard import pod_batch_slice, pod_slice
+        P, N, k = self.P, self.N, self.k
+        t, g = self.tsnap, self.gsnap
+        out_nodes, out_lens = [], []
+        for gi in range(pod_groups):
+            p0, p1 = pod_slice(P, pod_groups, gi)
+            rules, off, prio, req, mask, nc = pod_batch_slice(
+                p0, p1, self.tbatch.rules, self.tbatch.rule_off, self.tbatch.prio,
+                self.gbatch.req, self.gbatch.req_mask, self.gbatch.n_containers)
+            n = p1 - p0
+            rules_t, off_t, prio_t = _dev(rules.view(np.uint8)), _dev(off), _dev(prio.view(np.uint8))
+            req_t, mask_t, nc_t = _dev(req), _dev(mask.view(np.int32)), _dev(nc)
+            keys, nodes = [], []
+            for si in range(node_shards):
+                n0, n1 = node_range(N, node_shards, si)
+                with pas_amd.Context(0) as c:
+                    st = torch.cuda.current_stream()
+                    c.tas_snapshot_set_device(1, n1 - n0, self.M, _dev(t.v_milli[:, n0:n1]),
+                                              _dev(t.present[:, n0 // 64:(n1 + 63) // 64]
+                                                   .view(np.int64)), st)
+                    c.gas_snapshot_set_device(2, n1 - n0, g.used.shape[1], g.used.shape[2],
+                                              _dev(g.n_cards[n0:n1]), _dev(g.cap[n0:n1]),
+                                              _dev(g.used[n0:n1]), st)
+                    key = torch.empty((n, k), dtype=torch.int64, device="cuda")
+                    node = torch.empty((n, k), dtype=torch.int32, device="cuda")
+                    ln = torch.empty(n, dtype=torch.int32, device="cuda")
+                    c.tas_gas_topk_device(1, 2, n, len(rules), rules_t, off_t, prio_t, None,
+                                          req.shape[1], wl.I915, req_t, mask_t, nc_t, k, n0, key,
+                                          node, ln, st)
+                    torch.cuda.synchronize()
+                    keys.append(key)
+                    nodes.append(node)
+            out_node = torch.empty((n, k), dtype=torch.int32, device="cuda")
+            out_len = torch.empty(n, dtype=torch.int32, device="cuda")
+            with pas_amd.Context(0) as c:
+                c.topk_merge_device(n, k, node_shards, torch.stack(keys), torch.stack(nodes),
+                                    out_node, out_len, torch.cuda.current_stream())
+                torch.cuda.synchronize()
+            out_nodes.append(out_node)
+            out_lens.append(out_len)
+        return torch.cat(out_nodes), torch.cat(out_lens)
+
+
 @pytest.fixture(scope="module")
 def c5():
     return _C5()
@@ -244,6 +292,11 @@ def test_c5_full_batch_properties(c5):
         lz_nodes, lz_lens, _ = c5.run_ranges(world, lazy=True)
         assert torch.equal(lz_lens, lens1), world
         assert torch.equal(lz_nodes, nodes1), world
+    # the 2-D split (GridTopK): 2 node shards x 4 pod groups, and 1 x 8 (pure pod sharding)
+    for shards, groups in ((2, 4), (1, 8)):
+        g_nodes, g_lens = c5.run_grid(shards, groups)
+        assert torch.equal(g_lens, lens1), (shards, groups)
+        assert torch.equal(g_nodes, nodes1), (shards, groups)
     # every pass bit is also a fit bit (pass = cand AND NOT violated)
     assert not bool(((pass_t & ~fit_t) != 0).any())
     vals = _dev(c5.tsnap.v_milli)

@@ -37,10 +37,9 @@ TWO_NODES = dict(pod_labels={"telemetry-policy": "test-policy"}, names=["node A"
 
 def tas(ctx, metric_values, policies, gen):
     names = ["node A", "node B"]
-    v, pres, inexact = sn.tas_snapshot_from_metrics(
+    v, pres, scale = sn.tas_snapshot_from_metrics(
         {"dummyMetric1": {k: str(x) for k, x in metric_values.items()}}, names)
-    assert not inexact
-    ctx.tas_snapshot_set(gen, v, pres)
+    ctx.tas_snapshot_set(gen, v, pres, scale)
     return ext.MetricsExtender(ctx, gen, names, ["dummyMetric1"], policies)
 
 
@@ -160,10 +159,10 @@ def test_deschedule_enforce_g4(ctx):
     from test_oracle_golden import apply_label_patch
     g = G["G4_deschedule_enforce"]
     for gen, c in enumerate(g["cases"], start=8300):
-        v, pres, _ = sn.tas_snapshot_from_metrics(
+        v, pres, scale = sn.tas_snapshot_from_metrics(
             {m: {k: str(x) for k, x in vals.items()} for m, vals in g["metrics"].items()},
             g["nodes"], ["memory", "cpu"])
-        ctx.tas_snapshot_set(gen, v, pres)
+        ctx.tas_snapshot_set(gen, v, pres, scale)
         e = ext.DescheduleEnforcer(ctx, gen, g["nodes"], ["memory", "cpu"],
                                    [(g["policy"], [tuple(r) for r in c["rules"]])])
         total, bodies = e.enforce([c["labels"]])
@@ -178,10 +177,10 @@ def test_deschedule_enforce_shared_names(ctx):
     mirror: one remove / count per name (enforce.go:89-134)."""
     from test_oracle_golden import apply_label_patch
     g = G["G4n_shared_policy_name"]
-    v, pres, _ = sn.tas_snapshot_from_metrics(
+    v, pres, scale = sn.tas_snapshot_from_metrics(
         {m: {k: str(x) for k, x in vals.items()} for m, vals in g["metrics"].items()},
         g["nodes"], ["memory"])
-    ctx.tas_snapshot_set(8310, v, pres)
+    ctx.tas_snapshot_set(8310, v, pres, scale)
     for c in g["cases"]:
         e = ext.DescheduleEnforcer(ctx, 8310, g["nodes"], ["memory"],
                                    [(nm, [tuple(r) for r in rules])
@@ -198,9 +197,9 @@ def test_deschedule_enforce_registry_dedupe(ctx):
     (deschedule/strategy.go:60-78: same name, same non-empty rules); same name with other
     rules, or empty rules, stays."""
     names = ["node A", "node B"]
-    v, pres, _ = sn.tas_snapshot_from_metrics({"m": {"node A": "50", "node B": "30"}}, names,
+    v, pres, scale = sn.tas_snapshot_from_metrics({"m": {"node A": "50", "node B": "30"}}, names,
                                               ["m"])
-    ctx.tas_snapshot_set(8320, v, pres)
+    ctx.tas_snapshot_set(8320, v, pres, scale)
     r1 = [("m", "GreaterThan", 40)]
     e = ext.DescheduleEnforcer(ctx, 8320, names, ["m"],
                                [("p", r1), ("p", list(r1)), ("p", [("m", "GreaterThan", 41)]),
@@ -245,8 +244,8 @@ def test_deschedule_enforce_more_than_64_strategies(ctx, oracle):
     nodes = [f"node-{i}" for i in range(n_nodes)]
     vals = {m: {nd: str(int(rng.integers(0, 100))) for nd in nodes if rng.random() > 0.05}
             for m in metrics}
-    v, pres, _ = sn.tas_snapshot_from_metrics(vals, nodes, metrics)
-    ctx.tas_snapshot_set(8330, v, pres)
+    v, pres, scale = sn.tas_snapshot_from_metrics(vals, nodes, metrics)
+    ctx.tas_snapshot_set(8330, v, pres, scale)
     strategies = []
     for j in range(150):
         rules = [(metrics[int(rng.integers(0, 3))], ["LessThan", "GreaterThan", "Equals"][
@@ -294,10 +293,10 @@ def test_gas_filter_unknown_kind(ctx):
 def _tas2(ctx, metrics, policies, gen):
     """Two cached metrics: dummyMetric1 on both nodes, emptyMetric cached with no node."""
     names = ["node A", "node B"]
-    v, pres, _ = sn.tas_snapshot_from_metrics(
+    v, pres, scale = sn.tas_snapshot_from_metrics(
         {"dummyMetric1": {k: str(x) for k, x in metrics.items()}, "emptyMetric": {}}, names,
         ["dummyMetric1", "emptyMetric"])
-    ctx.tas_snapshot_set(gen, v, pres)
+    ctx.tas_snapshot_set(gen, v, pres, scale)
     return ext.MetricsExtender(ctx, gen, names, ["dummyMetric1", "emptyMetric"], policies)
 
 
@@ -344,10 +343,10 @@ def test_deschedule_unknown_operator(ctx):
     """deschedule.Violated (deschedule/strategy.go:31-50) skips the same rules, and panics in
     the controller goroutine on a cached, non-empty metric."""
     names = ["node A", "node B"]
-    v, pres, _ = sn.tas_snapshot_from_metrics(
+    v, pres, scale = sn.tas_snapshot_from_metrics(
         {"dummyMetric1": {"node A": "50", "node B": "30"}, "emptyMetric": {}}, names,
         ["dummyMetric1", "emptyMetric"])
-    ctx.tas_snapshot_set(8520, v, pres)
+    ctx.tas_snapshot_set(8520, v, pres, scale)
     strategies = [("pol-a", [("absentMetric", "Foo", 1), ("dummyMetric1", "GreaterThan", 40)]),
                   ("pol-b", [("emptyMetric", "Bar", 1)])]
     e = ext.DescheduleEnforcer(ctx, 8520, names, ["dummyMetric1", "emptyMetric"], strategies)

@@ -171,11 +171,19 @@ def test_builder_matches_map_restatement(oracle):
 
 
 def test_tas_builder_exactness():
-    metrics = {"m1": {"a": "1.5", "b": "2", "zz": "7"}, "m2": {"b": "1m", "a": "0.0001"}}
-    v, pres, inexact = sn.tas_snapshot_from_metrics(metrics, ["a", "b"], ["m1", "m2", "m3"])
-    assert v[0].tolist() == [1500, 2000] and v[1, 1] == 1
-    assert int(pres[0, 0]) == 0b11 and int(pres[1, 0]) == 0b10 and int(pres[2, 0]) == 0
-    assert inexact == [("m2", "a")]  # sub-milli: not milli-exact
+    metrics = {"m1": {"a": "1.5", "b": "2", "zz": "7"}, "m2": {"b": "1m", "a": "0.0001"},
+               "m4": {"a": "1e-7", "b": "1500u"}, "m5": {"a": "9e15"}}
+    v, pres, scale = sn.tas_snapshot_from_metrics(metrics, ["a", "b"],
+                                                  ["m1", "m2", "m3", "m4", "m5"])
+    # milli unless a value needs more places: every value kept, exactly
+    assert scale.tolist() == [3, 4, 3, 7, 3]
+    assert v[0].tolist() == [1500, 2000] and v[1].tolist() == [1, 10]
+    assert v[3].tolist() == [1, 15000] and v[4, 0] == 9 * 10**18
+    assert int(pres[0, 0]) == 0b11 and int(pres[1, 0]) == 0b11 and int(pres[2, 0]) == 0
+    # a column that needs both 7 places and 1e12: outside int64 at 10^-7 -> named error
+    with pytest.raises(pas_amd.PasError) as e:
+        sn.tas_snapshot_from_metrics({"big": {"a": "1e-7", "b": "1e12"}}, ["a", "b"])
+    assert e.value.code == pas_amd._lib.PAS_ENOTEXACT and "big" in str(e.value)
 
 
 @pytest.mark.gpu
