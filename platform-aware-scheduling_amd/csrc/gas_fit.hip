@@ -236,18 +236,18 @@ __device__ __forceinline__ int32_t multi_skip_list(int32_t n_res, uint32_t ok_ma
   return m ? 1 + __builtin_ctz(m) : 0;
 }
 
-// One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
-// list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
-// [n_res + 1][kClasses][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list
-// and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
-// go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
-// PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
 // A fit kernel whose fork wait gave up returns at entry: its prep lists may be unwritten (the
 // call reports PAS_EDEVICE, gas_fault_check).
 __device__ __forceinline__ bool fit_aborted(const uint32_t* abort, uint32_t epoch) {
   return abort && __hip_atomic_load(abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == epoch;
 }
 
+// One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
+// list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
+// [n_res + 1][kClasses][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list
+// and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
+// go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
+// PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
 struct PrepArgs {
   int32_t n_pods, max_containers, n_res, i915;
   const int64_t* req;
