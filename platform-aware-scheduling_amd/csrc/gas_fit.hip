@@ -90,9 +90,11 @@ constexpr int kSingleTpb = PAS_GAS_SINGLE_TPB;
 constexpr int kPrepTpb = 64;  // pods per prep block: small blocks spread the pods over the CUs
 constexpr int kMaxCards = PAS_GAS_PACKED;  // cards of a fast-path node, in registers
 constexpr int kPacked = PAS_GAS_PACKED;    // selections of a fast-path pod
-// Multi-selection pods are listed by class: S = 2, S = 3, S >= 4 (each class has its own
-// loop in the multi kernel, so no per-pod dispatch on S).
-constexpr int kClasses = 3;
+// Multi-selection pods are listed by class (each class has its own loop in a fit kernel, so
+// no per-pod dispatch on S): S = 2, S = 3 (closed form, gas_rfit_closed_kernel), S >= 4 in
+// order, and S = 4 in closed form (lists with a skipped kind; gas_rfit_seq_kernel, rfour).
+constexpr int kClasses = 4;
+constexpr int kClsSeq = 2, kClsFour = 3;
 
 // A (pod, container) step, in compare form: cmp[q] = per-GPU need of a requested kind
 // (getPerGPUResourceRequest :180-190), INT64_MIN for the others, so every card passes them
@@ -126,6 +128,20 @@ struct alignas(16) GasThresholds {
 // selections also has its thresholds from row kThRow on.
 constexpr int kThRow = 4;
 static_assert(sizeof(GasThresholds) <= sizeof(GasSel) * (kPacked - kThRow), "row");
+// A pod with 4 selections in a list with a skipped kind (class kClsFour) has a row of its 15
+// thresholds instead (no GasSel rows): row (t, m) = 2^t - 1 + m for selection t and the set m
+// of earlier selections (bit s: selection s) whose takes sit on the card,
+//   0: n0  1: n1  2: n1+t0  3: n2  4: n2+t0  5: n2+t1  6: n2+t0+t1  7: n3  8: n3+t0  9: n3+t1
+//   10: n3+t0+t1  11: n3+t2  12: n3+t0+t2  13: n3+t1+t2  14: n3+t0+t1+t2.
+// flags: bit r row r overflows int64 (bit 0 also: a bad pod); bit 16 + t (t = 1..3) selection
+// t's need equals selection t - 1's (the kernel reuses the mask).
+struct alignas(16) GasFour {
+  int64_t th[15][PAS_GAS_MAX_RES];
+  int32_t flags;
+  int32_t pad[3];
+};
+static_assert(sizeof(GasFour) <= sizeof(GasSel) * kPacked, "row");
+constexpr int kFourSame = 16;  // GasFour::flags: first "same" bit (selection t at bit 16 + t)
 constexpr int32_t kBadPod = 1 << 30;  // multi-list word flag: a selection has a negative need
 
 // Pod with at most one card selection: its selecting step (compare form), and
@@ -362,7 +378,10 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
   const int32_t l = one_sel ? (steps == 1 ? skip_list(n_res, one.cmp, kinds, gmin) : 0)
                             : multi_skip_list(n_res, skip_ok, skip_req);
   const int32_t nl = n_res + 1;
-  const int32_t ml = l * kClasses + (steps == 2 ? 0 : steps == 3 ? 1 : 2);  // multi list
+  // four selections in closed form on the ranked lists (a skipped kind), else in order
+  const bool four = steps == 4 && l > 0;
+  const int32_t ml =
+      l * kClasses + (steps == 2 ? 0 : steps == 3 ? 1 : four ? kClsFour : kClsSeq);  // multi list
   const int32_t slot = wave_slot(counts, one_sel ? l : nl + ml);
   if (one_sel) {
     one.word = p | (steps << 24) | (one_bad ? kBadPod : 0);
@@ -383,17 +402,19 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
   // the pod's row sits at its list position, so a batch of a list is one contiguous copy
   GasSel* out = sels + ((int64_t)ml * n_pods + slot) * kPacked;
   int32_t k = 0, bad = 0;
-  // the first three selections in named registers (a runtime-indexed array would live in
+  // the first four selections in named registers (a runtime-indexed array would live in
   // scratch memory)
   int64_t cmp0[PAS_GAS_MAX_RES], cmp1[PAS_GAS_MAX_RES], cmp2[PAS_GAS_MAX_RES];
-  int64_t take0[PAS_GAS_MAX_RES], take1[PAS_GAS_MAX_RES];
+  int64_t cmp3[PAS_GAS_MAX_RES];
+  int64_t take0[PAS_GAS_MAX_RES], take1[PAS_GAS_MAX_RES], take2[PAS_GAS_MAX_RES];
 #pragma unroll
-  for (int q = 0; q < PAS_GAS_MAX_RES; ++q) cmp0[q] = cmp1[q] = cmp2[q] = take0[q] = take1[q] = 0;
+  for (int q = 0; q < PAS_GAS_MAX_RES; ++q)
+    cmp0[q] = cmp1[q] = cmp2[q] = cmp3[q] = take0[q] = take1[q] = take2[q] = 0;
   each_container([&](const GasStep& g) {
     bad |= g.num_i915 > 0 ? g.bad : 0;
     // selections k .. k + num_i915 - 1 all carry this container's step
     const bool s0 = k <= 0 && 0 < k + g.num_i915, s1 = k <= 1 && 1 < k + g.num_i915;
-    const bool s2 = k <= 2 && 2 < k + g.num_i915;
+    const bool s2 = k <= 2 && 2 < k + g.num_i915, s3 = k <= 3 && 3 < k + g.num_i915;
 #pragma unroll
     for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
       cmp0[q] = s0 ? g.cmp[q] : cmp0[q];
@@ -401,8 +422,11 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
       cmp1[q] = s1 ? g.cmp[q] : cmp1[q];
       take1[q] = s1 ? g.take[q] : take1[q];
       cmp2[q] = s2 ? g.cmp[q] : cmp2[q];
+      take2[q] = s2 ? g.take[q] : take2[q];
+      cmp3[q] = s3 ? g.cmp[q] : cmp3[q];
     }
     for (int32_t r = 0; r < g.num_i915; ++r, ++k) {
+      if (four) continue;  // a threshold row instead (below)
       GasSel e = {};
 #pragma unroll
       for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
@@ -412,6 +436,44 @@ __device__ __forceinline__ void prep_pod(const PrepArgs& a, const int32_t p) {
       out[k] = e;
     }
   });
+  if (four) {
+    // row (t, m): need t plus the takes of the set m of earlier selections, overflow flagged
+    // (as the two / three-selection rows below); unrequested kinds stay INT64_MIN
+    GasFour* f = reinterpret_cast<GasFour*>(out);
+    const int64_t* cmps[4] = {cmp0, cmp1, cmp2, cmp3};
+    const int64_t* takes[3] = {take0, take1, take2};
+    int32_t flags = bad ? 1 : 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+#pragma unroll
+      for (int m = 0; m < (1 << t); ++m) {
+        bool o = false;
+#pragma unroll
+        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) {
+          int64_t v = cmps[t][q];
+          if (v != INT64_MIN) {
+#pragma unroll
+            for (int s = 0; s < t; ++s) {
+              int64_t r;
+              if (((m >> s) & 1) && !o) {
+                o = __builtin_add_overflow(v, takes[s][q], &r);
+                v = r;
+              }
+            }
+          }
+          f->th[(1 << t) - 1 + m][q] = v;
+        }
+        flags |= o ? 1 << ((1 << t) - 1 + m) : 0;
+      }
+      if (t > 0) {
+        bool eq = true;
+#pragma unroll
+        for (int q = 0; q < PAS_GAS_MAX_RES; ++q) eq = eq && cmps[t][q] == cmps[t - 1][q];
+        flags |= eq ? 1 << (kFourSame + t) : 0;
+      }
+    }
+    f->flags = flags;
+  }
   if (steps <= 3) {
     // thresholds: need plus the takes of a subset of the earlier selections (cards taken
     // from by exactly those selections); unrequested kinds stay INT64_MIN
@@ -819,13 +881,19 @@ struct alignas(16) GasRMulti {
 struct alignas(16) GasRSeq {
   uint32_t rep[kPacked][PAS_GAS_MAX_RES];
 };
+// A closed-form four-selection pod's ranks: its full-mask rows (GasFour rows 0, 1, 3, 7: the
+// selections' own needs) per compared kind, replicated.  Its other rows are checked at one
+// card on 64-bit values (rfour).
+struct alignas(16) GasRFour {
+  uint32_t rep[4][PAS_GAS_MAX_RES];
+};
 // rword flags (free bits of a multi-list word): the full-mask rows that repeat an earlier one
 constexpr uint32_t kSame01 = 1u << 28, kSame03 = 1u << 29, kSame13 = 1u << 31;
 
 // rows per pod of a slot class: 0 one selection, 1 two, 2 three, 3 four to eight (a row per
-// selection, rows past S hold INT64_MIN)
+// selection, rows past S hold INT64_MIN), 4 four in closed form (its full-mask rows)
 __device__ __forceinline__ int32_t rank_rows(int32_t cls) {
-  return cls == 0 ? 1 : cls == 1 ? 3 : cls == 2 ? 7 : kPacked;
+  return cls == 0 ? 1 : cls == 1 ? 3 : cls == 2 ? 7 : cls == 3 ? kPacked : 4;
 }
 __device__ __forceinline__ int32_t rank_gs(int32_t cls) { return kRankMax / rank_rows(cls); }
 
@@ -834,13 +902,15 @@ __device__ __forceinline__ void rank_group(
     const GasSingle* __restrict__ single, const int32_t* __restrict__ multi,
     const GasSel* __restrict__ sels, int64_t* __restrict__ srt_s, int64_t* __restrict__ srt_m,
     GasRSingle* __restrict__ rsingle, GasRMulti* __restrict__ rmulti, int32_t* __restrict__ rword,
-    GasRSeq* __restrict__ rseq, int64_t (*v)[kRankItems], uint32_t* pks) {
+    GasRSeq* __restrict__ rseq, GasRFour* __restrict__ rfour, int64_t (*v)[kRankItems],
+    uint32_t* pks) {
   const int32_t NL = Q + 1;
-  const bool one = slot < NL, seq = slot >= 3 * NL;
-  const int32_t l = one ? slot : seq ? slot - 3 * NL : (slot - NL) >> 1;
-  const int32_t cls = one ? 0 : seq ? 3 : 1 + ((slot - NL) & 1);
+  const bool one = slot < NL, seq = slot >= 3 * NL && slot < 4 * NL, four = slot >= 4 * NL;
+  const int32_t l = one ? slot : seq ? slot - 3 * NL : four ? slot - 4 * NL : (slot - NL) >> 1;
+  const int32_t cls = one ? 0 : seq ? 3 : four ? 4 : 1 + ((slot - NL) & 1);
   const int32_t R = rank_rows(cls);
-  const int32_t ml = l * kClasses + (cls - 1 < 2 ? cls - 1 : 2);  // multi list (cls > 0)
+  const int32_t ml =
+      l * kClasses + (seq ? kClsSeq : four ? kClsFour : cls - 1);  // multi list (cls > 0)
   const int32_t cnt = counts[one ? l : NL + ml];
   const int32_t gb = gi * rank_gs(cls), ge = min(cnt, gb + rank_gs(cls));
   const int32_t n = (ge - gb) * R;
@@ -848,12 +918,16 @@ __device__ __forceinline__ void rank_group(
   if (one) {
     for (int32_t s = 0; s < l; ++s) base += counts[s];
   } else {
-    // two- and three-selection slots in slot order, then the sequential ones
-    const int32_t pairs = seq ? 2 * NL : slot - NL;
+    // two- and three-selection slots in slot order, then the sequential ones, then the
+    // closed-form four-selection ones
+    const int32_t pairs = seq || four ? 2 * NL : slot - NL;
     for (int32_t s = 0; s < pairs; ++s)
       base += (int64_t)counts[NL + (s >> 1) * kClasses + (s & 1)] * rank_rows(1 + (s & 1));
-    if (seq)  // list 0's sequential pods are not ranked (no groups, no rows)
-      for (int32_t s = 1; s < l; ++s) base += (int64_t)counts[NL + s * kClasses + 2] * kPacked;
+    // list 0's sequential pods are not ranked (no groups, no rows), nor filed as four
+    for (int32_t s = 1; s < (seq ? l : four ? NL : 0); ++s)
+      base += (int64_t)counts[NL + s * kClasses + kClsSeq] * kPacked;
+    if (four)
+      for (int32_t s = 1; s < l; ++s) base += (int64_t)counts[NL + s * kClasses + kClsFour] * 4;
   }
   base += (int64_t)gb * R;
   int64_t* srt = one ? srt_s : srt_m;
@@ -863,15 +937,22 @@ __device__ __forceinline__ void rank_group(
   const int32_t j = q - (skip >= 0 && q > skip ? 1 : 0);  // compared-kind index
   const bool live = kind && i < n;
   const int32_t pos = gb + (i < n ? i / R : 0), row = i < n ? i % R : 0;
-  const GasThresholds* th = one || seq ? nullptr
-                                      : reinterpret_cast<const GasThresholds*>(
-                                            sels + ((int64_t)ml * P + pos) * kPacked + kThRow);
+  const GasThresholds* th = one || seq || four
+                                ? nullptr
+                                : reinterpret_cast<const GasThresholds*>(
+                                      sels + ((int64_t)ml * P + pos) * kPacked + kThRow);
+  const GasFour* th4 =
+      four ? reinterpret_cast<const GasFour*>(sels + ((int64_t)ml * P + pos) * kPacked) : nullptr;
+  // a four-selection pod's full-mask rows: GasFour rows 0, 1, 3, 7
+  const int32_t frow = (1 << row) - 1;
   // every global load of the group up front (one round trip): the value (padded with
   // INT64_MAX: never below an item, equal only to items past the padding), the pod word, the
   // threshold flags, the one-selection word
   const bool item = i < n;
   const int32_t mword = !one && item ? multi[(int64_t)ml * P + pos] : 0;
-  const uint32_t over = !one && !seq && item ? (uint32_t)th->over : 0u;
+  const uint32_t over = !item || one || seq ? 0u
+                        : four         ? (uint32_t)th4->flags >> frow
+                                       : (uint32_t)th->over >> row;
   const int32_t sword = one && item ? single[(int64_t)l * P + pos].word : 0;
   int64_t y = INT64_MAX;
   if (live) {
@@ -880,6 +961,8 @@ __device__ __forceinline__ void rank_group(
     } else if (seq) {  // selection `row` of the pod, loaded unconditionally (INT64_MIN past S)
       const int64_t x = sels[((int64_t)ml * P + pos) * kPacked + row].ct[q][0];
       y = row < ((mword >> 24) & 0xF) ? x : INT64_MIN;
+    } else if (four) {
+      y = th4->th[frow][q];
     } else {
       y = th->th[row][q];
     }
@@ -902,11 +985,13 @@ __device__ __forceinline__ void rank_group(
     srt[(base + less + eqb) * PAS_GAS_MAX_RES + j] = y;
     // 0x80 never passes: an overflowing threshold, or (one selection) a bad pod, whose word
     // is then 0 on every node without a branch in the fit kernel
-    g = (((over >> row) & 1u) || (sword & kBadPod)) ? 0x80u : (uint32_t)(less + 1);
+    g = ((over & 1u) || (sword & kBadPod)) ? 0x80u : (uint32_t)(less + 1);
     if (one) {
       rsingle[(int64_t)l * P + pos].g[j] = g * 0x01010101u;
     } else if (seq) {
       rseq[(int64_t)l * P + pos].rep[row][j] = g * 0x01010101u;
+    } else if (four) {
+      rfour[(int64_t)l * P + pos].rep[row][j] = g * 0x01010101u;
     } else if (row == 0 || row == 1 || row == 3) {
       rmulti[(int64_t)(l * 2 + cls - 1) * P + pos].rep[row == 3 ? 2 : row][j] = g * 0x01010101u;
     } else {
@@ -915,7 +1000,7 @@ __device__ __forceinline__ void rank_group(
   }
   __syncthreads();
   // one thread per item: the packed rows and the pod word
-  if (threadIdx.x >= kRankItems || i >= n || seq) return;
+  if (threadIdx.x >= kRankItems || i >= n || seq || four) return;
   if (one) {
     rsingle[(int64_t)l * P + pos].word = sword;
     return;
@@ -962,6 +1047,7 @@ struct RankArgs {
   GasRMulti* rmulti;
   int32_t* rword;
   GasRSeq* rseq;
+  GasRFour* rfour;
 };
 struct RankLds {
   int64_t v[PAS_GAS_MAX_RES][kRankItems];
@@ -974,7 +1060,7 @@ __device__ __forceinline__ void rank_prep_body(const RankArgs& a, int32_t first,
   const int32_t P = a.P, Q = a.Q;
   const int32_t* counts = a.counts;
   int32_t (&cnt_s)[(1 + kClasses) * (PAS_GAS_MAX_RES + 1)] = L.cnt_s;
-  const int32_t NL = Q + 1, slots = NL * 4;
+  const int32_t NL = Q + 1, slots = NL * 5;
   // the list counts, loaded once (a slot scan of dependent global loads costs a round trip each)
   if (threadIdx.x < (1 + kClasses) * NL) cnt_s[threadIdx.x] = counts[threadIdx.x];
   __syncthreads();
@@ -988,8 +1074,10 @@ __device__ __forceinline__ void rank_prep_body(const RankArgs& a, int32_t first,
     } else if (slot < 3 * NL) {
       cnt = counts[NL + ((slot - NL) >> 1) * kClasses + ((slot - NL) & 1)];
       cls = 1 + ((slot - NL) & 1);
+    } else if (slot < 4 * NL) {
+      cnt = slot == 3 * NL ? 0 : counts[NL + (slot - 3 * NL) * kClasses + kClsSeq], cls = 3;
     } else {
-      cnt = slot == 3 * NL ? 0 : counts[NL + (slot - 3 * NL) * kClasses + 2], cls = 3;
+      cnt = counts[NL + (slot - 4 * NL) * kClasses + kClsFour], cls = 4;  // (list 0: none)
     }
     return (cnt + rank_gs(cls) - 1) / rank_gs(cls);
   };
@@ -1004,7 +1092,7 @@ __device__ __forceinline__ void rank_prep_body(const RankArgs& a, int32_t first,
     if (slot >= slots) return;
     __syncthreads();  // the previous group's reads of v / pks are done
     rank_group(P, Q, counts, slot, gi, a.single, a.multi, a.sels, a.srt_s, a.srt_m, a.rsingle,
-               a.rmulti, a.rword, a.rseq, L.v, L.pks);
+               a.rmulti, a.rword, a.rseq, a.rfour, L.v, L.pks);
   }
 }
 
@@ -1475,6 +1563,175 @@ __device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, ch
   }
 }
 
+// Four-selection pods in closed form (class kClsFour: lists with a skipped kind).  Selection t
+// takes the first card whose free covers its need plus the takes already on that card
+// (getCardsForContainerGPURequest, scheduler.go:200-257; addRM, resource_map.go:38-53).  A
+// card no earlier selection took from passes iff it is in the mask of the selection's own need
+// (ranks, as rclosed); a card that earlier selections took from passes iff its snapshot free
+// covers the threshold row of exactly those selections (GasFour), checked at that one card on
+// its 64-bit free values from the lane's LDS copy (FreeTab).  With e_ab = (c_a == c_b):
+//   c0 = lowest(m0)
+//   c1 = min(lowest(m1 \ {c0}), c0 if row 2 fits at c0)
+//   c2 = min(lowest(m2 \ {c0, c1}), c0 if row (e01 ? 6 : 4) fits at c0,
+//            c1 if !e01 and row 5 fits at c1)
+//   c3 = min(lowest(m3 \ {c0, c1, c2}), c0 if row 8 + 2 e01 + 4 e02 fits at c0,
+//            c1 if !e01 and row 9 + 4 e12 fits at c1, c2 if !e02, !e12 and row 11 fits at c2)
+// Card positions are mask bit positions 4c + 3 (0xFFFFFFFF: none, as rclosed).
+// The pod's GasFour from row 2 on, as staged in LDS (rows 0, 1, 3, 7 are ranked instead).
+struct alignas(16) FourStage {
+  int64_t th[13][PAS_GAS_MAX_RES];  // GasFour rows 2 .. 14
+  int32_t flags;
+  int32_t pad[3];
+};
+static_assert(sizeof(FourStage) + 2 * sizeof(int64_t) * PAS_GAS_MAX_RES == sizeof(GasFour) &&
+                  offsetof(GasFour, flags) == 15 * sizeof(int64_t) * PAS_GAS_MAX_RES,
+              "FourStage is GasFour from row 2 on");
+constexpr int kFourMB = 4;  // four-selection pods staged per batch and wave
+
+template <int Q, int SKIP, int kC>
+__device__ __forceinline__ uint32_t rfour(const uint32_t (&fa)[kC], const uint32_t (&fb)[kC],
+                                          const GasRFour& rk, const FourStage& st, uint32_t flags,
+                                          const FreeTab<kC>& tab, int lane) {
+  constexpr uint32_t kNone = ~0u;
+  auto mask = [&](int t) {
+    uint32_t g[kC];
+#pragma unroll
+    for (int j = 0; j < kC; ++j) g[j] = rk.rep[t][j];
+    return rmask<kC>(fa, fb, g);
+  };
+  auto load = [&](uint32_t p, int64_t (&f)[kC]) {
+    const int64_t* x = tab.at(min(p >> 2, 7u), lane);
+#pragma unroll
+    for (int j = 0; j < kC; ++j) f[j] = x[j];
+  };
+  // row r >= 2 fits at a card of snapshot free f (and does not overflow)
+  auto fits = [&](int r, const int64_t (&f)[kC]) {
+    bool ok = ((flags >> r) & 1u) == 0u;
+#pragma unroll
+    for (int q = 0, j = 0; q < Q; ++q)
+      if (q != SKIP) ok = ok && st.th[r - 2][q] <= f[j++];
+    return ok;
+  };
+  const uint32_t m0 = mask(0);
+  const uint32_t m1 = ((flags >> (kFourSame + 1)) & 1u) ? m0 : mask(1);
+  const uint32_t m2 = ((flags >> (kFourSame + 2)) & 1u) ? m1 : mask(2);
+  const uint32_t m3 = ((flags >> (kFourSame + 3)) & 1u) ? m2 : mask(3);
+  int64_t f0[kC], f1[kC], f2[kC];
+  const uint32_t p0 = lowbit(m0);
+  load(p0, f0);
+  const uint32_t b0 = 1u << (p0 & 31u);
+  const uint32_t p1 = min(lowbit(m1 & ~b0), fits(2, f0) ? p0 : kNone);
+  load(p1, f1);
+  const uint32_t b1 = 1u << (p1 & 31u);
+  const bool e01 = p0 == p1;
+  const bool a0 = e01 ? fits(6, f0) : fits(4, f0);
+  const bool a1 = !e01 && fits(5, f1);
+  const uint32_t p2 = min(lowbit(m2 & ~(b0 | b1)), min(a0 ? p0 : kNone, a1 ? p1 : kNone));
+  load(p2, f2);
+  const uint32_t b2 = 1u << (p2 & 31u);
+  const bool e02 = p0 == p2, e12 = p1 == p2;
+  const bool c0 = e01 ? (e02 ? fits(14, f0) : fits(10, f0)) : (e02 ? fits(12, f0) : fits(8, f0));
+  const bool c1 = !e01 && (e12 ? fits(13, f1) : fits(9, f1));
+  const bool c2 = !e02 && !e12 && fits(11, f2);
+  const uint32_t p3 = min(min(lowbit(m3 & ~(b0 | b1 | b2)), c0 ? p0 : kNone),
+                          min(c1 ? p1 : kNone, c2 ? p2 : kNone));
+  // card fields as arithmetic shifts: a selection without a card makes the word negative
+  const int32_t word = ((int32_t)p0 >> 2) | (((int32_t)p1 >> 2) << 3) |
+                       (((int32_t)p2 >> 2) << 6) | (((int32_t)p3 >> 2) << 9);
+  return (uint32_t)min(word ^ (int32_t)(0x80000000u | (4u << 24)), 0);
+}
+
+// The closed-form four-selection pods of a list with a skipped kind: groups of 31 pods (their
+// 4 full-mask rows ranked), a chunk takes whole groups; per group the node's cards are ranked
+// once, then batches of kFourMB pods (FourStage + GasRFour) are staged as in rseq_list.
+template <int Q, int SKIP, bool kBits>
+__device__ __forceinline__ void rfour_list(const int64_t* __restrict__ free_t, char* wlds,
+                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                           const int32_t* __restrict__ list,
+                                           const GasSel* __restrict__ sels,
+                                           const GasRFour* __restrict__ rf,
+                                           const int64_t* __restrict__ srt, int64_t item0,
+                                           int32_t cnt, const BlockTile& bt, ResOut res,
+                                           uint64_t* __restrict__ fit) {
+  constexpr int kC = Q - 1;
+  const int32_t lane = threadIdx.x & 63;
+  const FreeTab<kC> tab{reinterpret_cast<int64_t*>(wlds)};
+  char* over = wlds + sizeof(int64_t) * kMaxCards * 64 * kC;
+  int64_t* lds = reinterpret_cast<int64_t*>(over);
+  FourStage* stage = reinterpret_cast<FourStage*>(over);
+  GasRFour* rstage = reinterpret_cast<GasRFour*>(stage + kFourMB);
+  constexpr int32_t gs = kRankMax / 4;
+  int32_t g0, g1;
+  chunk_groups(cnt, bt.chunks, bt.chunk, gs, &g0, &g1);
+  if (g0 < g1) fill_tab_t<Q, SKIP, kC>(free_t, n, valid, N, tab, lane);
+  constexpr int kPieces = (int)(sizeof(FourStage) / 16), kRPieces = (int)(sizeof(GasRFour) / 16);
+  constexpr int kIters = (kFourMB * kPieces + 63) / 64;
+  static_assert(kFourMB * kRPieces <= 64, "rank rows");
+  constexpr size_t kSkipRows = 2 * sizeof(int64_t) * PAS_GAS_MAX_RES;  // GasFour rows 0, 1
+  for (int32_t gi = g0; gi < g1; ++gi) {
+    const int32_t gb = gi * gs, ge = min(cnt, gb + gs);
+    load_sorted<kC>(srt, item0 + (int64_t)gb * 4, (ge - gb) * 4, lds, lane);
+    uint32_t fa[kC], fb[kC];
+    rank_cards_t<Q, SKIP, kC>(free_t, n, valid, N, lds, (ge - gb) * 4, fa, fb);
+    for (int32_t b0 = gb; b0 < ge; b0 += kFourMB) {
+      const int32_t nb = __builtin_amdgcn_readfirstlane(min(kFourMB, ge - b0));
+      int4 v[kIters];
+#pragma unroll
+      for (int it = 0; it < kIters; ++it) {
+        const int32_t c = lane + 64 * it, pod = c / kPieces, pc = c % kPieces;
+        const int4* src = reinterpret_cast<const int4*>(
+            reinterpret_cast<const char*>(sels + (int64_t)(b0 + min(pod, nb - 1)) * kPacked) +
+            kSkipRows);
+        v[it] = pod < nb ? src[pc] : int4{0, 0, 0, 0};
+      }
+      const int4 rv = lane < nb * kRPieces ? reinterpret_cast<const int4*>(rf + b0)[lane]
+                                           : int4{0, 0, 0, 0};
+      const int32_t wd = lane < nb ? list[b0 + lane] : 0;
+      __builtin_amdgcn_wave_barrier();  // the previous batch's (or the ranking's) reads are done
+#pragma unroll
+      for (int it = 0; it < kIters; ++it)
+        if (lane + 64 * it < kFourMB * kPieces) reinterpret_cast<int4*>(stage)[lane + 64 * it] = v[it];
+      if (lane < kFourMB * kRPieces) reinterpret_cast<int4*>(rstage)[lane] = rv;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+      const FourStage* st = lane_ptr(stage);  // (lane_ptr: record reads at immediate offsets)
+      const GasRFour* rst = lane_ptr(rstage);
+#pragma unroll
+      for (int j = 0; j < kFourMB; ++j) {
+        if (j >= nb) break;
+        const int32_t pod = __builtin_amdgcn_readlane(wd, j) & 0xFFFFFF;
+        const uint32_t flags = (uint32_t)__builtin_amdgcn_readfirstlane(st[j].flags);
+        uint32_t out = rfour<Q, SKIP, kC>(fa, fb, rst[j], st[j], flags, tab, lane);
+        if constexpr (kBits) out = out ? node_ok : 0u;
+        put_result<kBits>(res, fit, pod, N, n, valid, out);
+      }
+    }
+  }
+}
+
+// The closed-form four-selection lists l = 1 .. Q (list 0 files its four-selection pods as
+// sequential ones).  item0: the first sorted row of list 1's groups (after the sequential ones).
+template <int Q, bool kBits, int l = 1>
+__device__ __forceinline__ void four_lists(const int64_t* __restrict__ free_t, char* wlds,
+                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
+                                           int32_t P, const int32_t* __restrict__ multi,
+                                           const GasSel* __restrict__ sels,
+                                           const GasRFour* __restrict__ rf,
+                                           const int64_t* __restrict__ srt, int64_t item0,
+                                           const int32_t* __restrict__ counts, const BlockTile& bt,
+                                           ResOut res, uint64_t* __restrict__ fit) {
+  constexpr int L = l * kClasses + kClsFour;
+  const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[L]);
+  rfour_list<Q, l - 1, kBits>(free_t, wlds, node_ok, N, n, valid, multi + (int64_t)L * P,
+                              sels + (int64_t)L * P * kPacked, rf + (int64_t)l * P, srt, item0,
+                              cnt, bt, res, fit);
+  __builtin_amdgcn_wave_barrier();
+  if constexpr (l < Q)
+    four_lists<Q, kBits, l + 1>(free_t, wlds, node_ok, N, n, valid, P, multi, sels, rf, srt,
+                                item0 + (int64_t)cnt * 4, counts, bt, res, fit);
+}
+
 // The lists of pods with 4 to 8 selections (class 2 of each kind-skip list): ranked where a
 // kind is skipped (rseq_list), else on 64-bit values (multi_list).  item0: the first sorted
 // row of list 1's groups (after the two- and three-selection lists' rows).
@@ -1805,10 +2062,13 @@ struct MultiLds {
   static constexpr size_t kRowsOrStage =
       kRows > sizeof(GasRMulti) * kRankMB ? kRows : sizeof(GasRMulti) * kRankMB;
   static constexpr size_t kRanked = kRowsOrStage + sizeof(uint32_t) * kMaxCards * 64;
-  static constexpr size_t kSeqOver = sizeof(int64_t) * kC * kRankItems >
-                                             sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB
-                                         ? sizeof(int64_t) * kC * kRankItems
-                                         : sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB;
+  // the sequential kernel: the FreeTab copy, then the sorted rows overlaid by a batch stage
+  // (sequential pods or closed-form four-selection pods)
+  static constexpr size_t cmax(size_t a, size_t b) { return a > b ? a : b; }
+  static constexpr size_t kSeqOver =
+      cmax(sizeof(int64_t) * kC * kRankItems,
+           cmax(sizeof(GasSel) * kPacked * kMB + sizeof(GasRSeq) * kMB,
+                (sizeof(FourStage) + sizeof(GasRFour)) * kFourMB));
   static constexpr size_t kSeq = sizeof(int64_t) * kMaxCards * 64 * kC + kSeqOver;
 };
 
@@ -1859,9 +2119,9 @@ template <int Q, bool kBits>
 __device__ __forceinline__ void rfit_seq_body(
     const BlockTile& bt, char* w, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
-    const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
-    const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, ResOut res,
-    uint64_t* __restrict__ fit) {
+    const GasRFour* __restrict__ rf, const int64_t* __restrict__ srt,
+    const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
+    const int32_t* __restrict__ counts, ResOut res, uint64_t* __restrict__ fit) {
   const int32_t n = bt.node_block * kSeqTpb + threadIdx.x;
   const bool in = n < N;
   const int32_t nc = in ? n_cards[n] : 0;
@@ -1876,20 +2136,28 @@ __device__ __forceinline__ void rfit_seq_body(
     item_seq += (int64_t)counts[l * kClasses] * 3 + (int64_t)counts[l * kClasses + 1] * 7;
   seq_lists<Q, kBits>(free_t, w, node_ok, N, n, valid, P, multi, sels, rq, srt,
                       __builtin_amdgcn_readfirstlane(item_seq), counts, bt, res, fit);
+  if constexpr (Q > 1) {
+    // the closed-form four-selection lists' rows follow the ranked sequential lists' rows
+    int64_t item_four = item_seq;
+#pragma unroll
+    for (int l = 1; l <= Q; ++l) item_four += (int64_t)counts[l * kClasses + kClsSeq] * kPacked;
+    four_lists<Q, kBits>(free_t, w, node_ok, N, n, valid, P, multi, sels, rf, srt,
+                         __builtin_amdgcn_readfirstlane(item_four), counts, bt, res, fit);
+  }
 }
 
 template <int Q, bool kBits>
 __global__ __launch_bounds__(kSeqTpb) void gas_rfit_seq_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
-    const int64_t* __restrict__ srt, const int32_t* __restrict__ multi,
-    const GasSel* __restrict__ sels, const int32_t* __restrict__ counts, int32_t chunks,
-    ResOut res, uint64_t* __restrict__ fit) {
+    const GasRFour* __restrict__ rf, const int64_t* __restrict__ srt,
+    const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
+    const int32_t* __restrict__ counts, int32_t chunks, ResOut res, uint64_t* __restrict__ fit) {
   __shared__ int4 smem[kSeqTpb / 64][MultiLds<Q>::kSeq / 16];
   if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P, n_cards,
-                          free_t, rq, srt, multi, sels, counts, res, fit);
+                          free_t, rq, rf, srt, multi, sels, counts, res, fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -2163,10 +2431,11 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   const size_t b_srs = al(sizeof(int64_t) * PAS_GAS_MAX_RES * (size_t)n_pods);
   const size_t b_srm = al(sizeof(int64_t) * PAS_GAS_MAX_RES * kPacked * (size_t)n_pods);
   const size_t b_rq = al(sizeof(GasRSeq) * (size_t)NL * n_pods);
+  const size_t b_rf = al(sizeof(GasRFour) * (size_t)NL * n_pods);
   const bool empty = N == 0 || n_pods == 0;
   const size_t need = empty ? 0
                             : b_single + b_multi + b_sels + 2 * b_pods + b_rs + b_rm + b_rw +
-                                  b_srs + b_srm + b_rq;
+                                  b_srs + b_srm + b_rq + b_rf;
   // the stream's scratch slot (ordered after its previous user on another stream)
   int rc = PAS_OK;
   AuxSlot* slot = aux_acquire(ctx, s, need, &rc);
@@ -2219,6 +2488,8 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   base += b_srm;
   GasRSeq* rseq = reinterpret_cast<GasRSeq*>(base);
   base += b_rq;
+  GasRFour* rfour = reinterpret_cast<GasRFour*>(base);
+  base += b_rf;
   // this fit's list counts (zeroed by the previous fit's prep kernel, or at allocation) and
   // the other set, which this fit's prep kernel zeroes for the next one
   int32_t* counts = slot->gas_counts + kCounts * slot->gas_counts_set;
@@ -2300,7 +2571,7 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
                     counts_next, kCounts, slot->gas_limit, d_side_count,
                     kFlags ? sync + 4 : nullptr, epoch};
   const RankArgs ra{n_pods, Q, counts, single, multi, sels, srt_s, srt_m, rsingle, rmulti, rword,
-                    rseq};
+                    rseq, rfour};
   gas_prep_kernel<<<(n_pods + kPrepTpb - 1) / kPrepTpb, kPrepTpb, 0, s>>>(pa);
   PAS_HIP(ctx, hipGetLastError());
   // the prep kernel ran: the other set is zeroed (on s) for the slot's next fit
@@ -2403,15 +2674,15 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   case QQ * 2 + B:                                                                             \
     if (PAS_GAS_SEQ_FIRST)                                                                     \
       gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_q, ro, d_fit);                                                        \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, rfour, srt_m, multi, \
+          sels, counts + NL, ch_q, ro, d_fit);                                                  \
     gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, s>>>(                          \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
         counts + NL, ch_c, ro, d_fit);                                                          \
     if (!PAS_GAS_SEQ_FIRST)                                                                    \
       gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
-          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, srt_m, multi, sels,   \
-          counts + NL, ch_q, ro, d_fit);                                                        \
+          N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, rfour, srt_m, multi, \
+          sels, counts + NL, ch_q, ro, d_fit);                                                  \
     gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                         \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,       \
         ch_s, ro, d_fit);                                                                       \

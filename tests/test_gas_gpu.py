@@ -193,6 +193,62 @@ def test_kind_skip_lists(ctx, oracle, q):
     assert 0.1 < (want >> 31).mean() < 0.95
 
 
+FOUR_SPLITS = [(4,), (2, 2), (1, 1, 1, 1), (2, 1, 1), (1, 2, 1), (1, 1, 2), (3, 1), (1, 3)]
+
+
+@pytest.mark.parametrize("q", [2, 3, 4])
+@pytest.mark.parametrize("k", [4, 8])
+def test_four_selection_closed_form(ctx, oracle, q, k):
+    """Pods of exactly 4 selections in a kind-skip list (every real card keeps >= 5 of kind 0
+    free): gas_rfit_seq_kernel's closed form (GasFour rows, rfour).  Every container split of
+    4 selections (identical selections: the reused masks), small frees so that selections
+    share cards in every occupancy pattern, needs of 2^62 on nodes with int64-max capacity
+    (rows whose sums overflow int64), nodes with fewer cards than K or no label, a kind-1
+    request that one pod in 7 drops; words and node bitmaps against the oracle."""
+    import torch
+    rng = np.random.default_rng(700 + 10 * q + k)
+    n, p, c = 700, 192, 4
+    big = 2**63 - 1
+    n_cards = rng.integers(-1, k + 1, size=n).astype(np.int32)
+    cap = np.zeros((n, q), np.int64)
+    cap[:, 0] = 10
+    cap[:, 1:] = rng.choice(np.array([12, 20, 40, big], np.int64), size=(n, q - 1))
+    used = rng.integers(0, 8, size=(n, k, q)).astype(np.int64)
+    used[:, :, 0] = rng.integers(0, 6, size=(n, k))
+    req = np.zeros((p, c, q), np.int64)
+    mask = np.zeros((p, c), np.uint32)
+    ncont = np.zeros(p, np.int32)
+    for pi in range(p):
+        split = FOUR_SPLITS[pi % len(FOUR_SPLITS)]
+        ncont[pi] = len(split)
+        huge = pi % 11 == 3 and all(s == 1 for s in split)
+        for ci, ni in enumerate(split):
+            req[pi, ci, 0] = ni
+            per = rng.integers(1, 9, size=q - 1)
+            req[pi, ci, 1:] = per * ni
+            if huge:
+                req[pi, ci, 1] = 2**62
+            mask[pi, ci] = (1 << q) - 1
+            if q > 2 and pi % 7 == 5:
+                mask[pi, ci] &= ~np.uint32(2)  # kind 1 not requested (kinds 2.. are)
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    got = gpu_fit(ctx, n_cards, cap, used, req, mask, ncont, 0)
+    np.testing.assert_array_equal(got, want)
+    fits = (want >> 31).astype(bool)
+    assert 0.05 < fits.mean() < 0.95
+    # every occupancy pattern of the 4 selections occurs among the fitting words
+    cards = [decode_gas_word(w)[1] for w in want[fits][:20000]]
+    patterns = {tuple(sorted(np.unique(cs, return_counts=True)[1])) for cs in cards}
+    assert {(4,), (1, 3), (2, 2), (1, 1, 2), (1, 1, 1, 1)} <= patterns
+    # the node bitmaps of the same fit
+    dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    bm = torch.zeros((p, (n + 63) // 64), dtype=torch.int64, device="cuda")
+    ctx.gas_fit_bitmap_device(_gen[0], p, c, 0, dev(req), dev(mask.view(np.int32)), dev(ncont),
+                              bm)
+    ctx.synchronize()
+    np.testing.assert_array_equal(wl.unpack_bits(bm.cpu().numpy().view(np.uint64), n), fits)
+
+
 @pytest.mark.parametrize("cap_max", [2**31 - 2, 2**31 - 1])
 def test_narrow_kind_boundary(ctx, oracle, cap_max):
     # kinds whose cap stays <= INT32_MAX - 1 on every node compare in 32 bits (needs clamped):
