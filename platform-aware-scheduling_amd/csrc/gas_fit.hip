@@ -261,7 +261,7 @@ __device__ __forceinline__ bool fit_aborted(const uint32_t* abort, uint32_t epoc
 // One thread per pod files it under `single` (<= 1 selection: its selecting step, in the
 // list of its skippable kind; lists [n_res + 1][n_pods]) or `multi` (several: lists
 // [n_res + 1][kClasses][n_pods] of words pod | S << 24, by skippable kind as multi_skip_list
-// and by class S = 2 / 3 / more); a multi pod's selections (containers in order, then gpuNum)
+// and by class: S = 2, S = 3, S >= 4 in order, S = 4 in closed form); a multi pod's selections (containers in order, then gpuNum)
 // go to the row sels[list][slot][8] of its list position.  pod_steps saturates at
 // PAS_GAS_MAX_SELECTIONS + 1 (such pods only go to the generic path).  counts: [n_res + 1] single lists, then [n_res + 1][kClasses] multi lists.
 struct PrepArgs {
@@ -1028,7 +1028,8 @@ __device__ __forceinline__ void chunk_groups(int32_t cnt, int32_t chunks, int32_
 
 // One block per non-empty group (a persistent loop over the groups of every list slot), a
 // thread per (item, kind).  Slots: [0, NL) the one-selection lists; NL + 2 l + c list l's
-// two- (c = 0) and three-selection (c = 1) pods.  A group's items are its pods' rows
+// two- (c = 0) and three-selection (c = 1) pods; then per list the sequential pods, then the
+// closed-form four-selection pods (their full-mask rows).  A group's items are its pods' rows
 // (pod-major).  Per compared kind: an item's rank = #{items below it} (+ #{equal items before
 // it} for its sorted position), written as the sorted row (srt_*[item][kind j]) and as the
 // item's rank in its pod's record.  Items of a slot sit after those of the slots before it,
@@ -1066,7 +1067,8 @@ __device__ __forceinline__ void rank_prep_body(const RankArgs& a, int32_t first,
   __syncthreads();
   counts = cnt_s;
   // slots: one-selection lists, two/three-selection pairs, sequential lists (list 0's
-  // sequential pods, with no kind skipped, are evaluated on 64-bit values: no groups)
+  // sequential pods, with no kind skipped, are evaluated on 64-bit values: no groups),
+  // closed-form four-selection lists (none in list 0)
   auto slot_groups = [&](int32_t slot) {
     int32_t cnt, cls;
     if (slot < NL) {
@@ -2051,8 +2053,11 @@ __device__ __forceinline__ void rmulti_lists(const int64_t* __restrict__ free_t,
 
 // Pods with several selections, two kernels so that each gets the registers of its own phase:
 // the two- and three-selection lists on ranks (ranked straight from free_t, no register copy of
-// the node's free values: 8 waves per SIMD instead of the sequential phase's 4), then the lists
-// of four to eight selections (sequential, with the node's free values in registers).
+// the node's free values: 7 waves per SIMD instead of the other kernel's 4), then the lists
+// that read the node's 64-bit free values (FreeTab): four to eight selections in order, and
+// the closed-form four-selection lists.  (Three-selection pods in that closed form, 3 ranked
+// rows instead of 7: the closed kernel's VALU 134 -> 65 M, the other's 74 -> 138 M, C3 0.57-0.59
+// -> 0.62 ms: the 4-wave kernel became the fit's critical path.)
 template <int Q>
 struct MultiLds {
   static constexpr int kC = Q > 1 ? Q - 1 : 1;

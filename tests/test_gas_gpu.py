@@ -193,20 +193,24 @@ def test_kind_skip_lists(ctx, oracle, q):
     assert 0.1 < (want >> 31).mean() < 0.95
 
 
-FOUR_SPLITS = [(4,), (2, 2), (1, 1, 1, 1), (2, 1, 1), (1, 2, 1), (1, 1, 2), (3, 1), (1, 3)]
+SPLITS = {4: [(4,), (2, 2), (1, 1, 1, 1), (2, 1, 1), (1, 2, 1), (1, 1, 2), (3, 1), (1, 3)],
+          3: [(3,), (2, 1), (1, 2), (1, 1, 1)]}
+PATTERNS = {4: {(4,), (1, 3), (2, 2), (1, 1, 2), (1, 1, 1, 1)}, 3: {(3,), (1, 2), (1, 1, 1)}}
 
 
+@pytest.mark.parametrize("sel", [3, 4])
 @pytest.mark.parametrize("q", [2, 3, 4])
 @pytest.mark.parametrize("k", [4, 8])
-def test_four_selection_closed_form(ctx, oracle, q, k):
-    """Pods of exactly 4 selections in a kind-skip list (every real card keeps >= 5 of kind 0
-    free): gas_rfit_seq_kernel's closed form (GasFour rows, rfour).  Every container split of
-    4 selections (identical selections: the reused masks), small frees so that selections
-    share cards in every occupancy pattern, needs of 2^62 on nodes with int64-max capacity
-    (rows whose sums overflow int64), nodes with fewer cards than K or no label, a kind-1
-    request that one pod in 7 drops; words and node bitmaps against the oracle."""
+def test_closed_form_64bit_rows(ctx, oracle, sel, q, k):
+    """Pods of exactly 3 or 4 selections in a kind-skip list (every real card keeps >= 5 of
+    kind 0 free): the closed forms (4: gas_rfit_seq_kernel on 64-bit one-card rows, GasFour /
+    rfour; 3: gas_rfit_closed_kernel on ranks).  Every container split (identical selections: the reused masks), small frees
+    so that selections share cards in every occupancy pattern, needs of 2^62 on nodes with
+    int64-max capacity (rows whose sums overflow int64), nodes with fewer cards than K or no
+    label, a kind-1 request that one pod in 7 drops; words and node bitmaps against the
+    oracle."""
     import torch
-    rng = np.random.default_rng(700 + 10 * q + k)
+    rng = np.random.default_rng(700 + 100 * sel + 10 * q + k)
     n, p, c = 700, 192, 4
     big = 2**63 - 1
     n_cards = rng.integers(-1, k + 1, size=n).astype(np.int32)
@@ -219,7 +223,7 @@ def test_four_selection_closed_form(ctx, oracle, q, k):
     mask = np.zeros((p, c), np.uint32)
     ncont = np.zeros(p, np.int32)
     for pi in range(p):
-        split = FOUR_SPLITS[pi % len(FOUR_SPLITS)]
+        split = SPLITS[sel][pi % len(SPLITS[sel])]
         ncont[pi] = len(split)
         huge = pi % 11 == 3 and all(s == 1 for s in split)
         for ci, ni in enumerate(split):
@@ -239,7 +243,7 @@ def test_four_selection_closed_form(ctx, oracle, q, k):
     # every occupancy pattern of the 4 selections occurs among the fitting words
     cards = [decode_gas_word(w)[1] for w in want[fits][:20000]]
     patterns = {tuple(sorted(np.unique(cs, return_counts=True)[1])) for cs in cards}
-    assert {(4,), (1, 3), (2, 2), (1, 1, 2), (1, 1, 1, 1)} <= patterns
+    assert PATTERNS[sel] <= patterns
     # the node bitmaps of the same fit
     dev = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
     bm = torch.zeros((p, (n + 63) // 64), dtype=torch.int64, device="cuda")
