@@ -1606,12 +1606,14 @@ __device__ __forceinline__ uint32_t rfour(const uint32_t (&fa)[kC], const uint32
 #pragma unroll
     for (int j = 0; j < kC; ++j) f[j] = x[j];
   };
-  // row r >= 2 fits at a card of snapshot free f (and does not overflow)
+  // row r >= 2 fits at a card of snapshot free f (and does not overflow).  Every check is
+  // evaluated and combined with bitwise operations: straight-line compares and lane-mask
+  // logic, no divergent branches around the threshold loads
   auto fits = [&](int r, const int64_t (&f)[kC]) {
     bool ok = ((flags >> r) & 1u) == 0u;
 #pragma unroll
     for (int q = 0, j = 0; q < Q; ++q)
-      if (q != SKIP) ok = ok && st.th[r - 2][q] <= f[j++];
+      if (q != SKIP) ok = ok & (st.th[r - 2][q] <= f[j++]);
     return ok;
   };
   const uint32_t m0 = mask(0);
@@ -1626,15 +1628,18 @@ __device__ __forceinline__ uint32_t rfour(const uint32_t (&fa)[kC], const uint32
   load(p1, f1);
   const uint32_t b1 = 1u << (p1 & 31u);
   const bool e01 = p0 == p1;
-  const bool a0 = e01 ? fits(6, f0) : fits(4, f0);
-  const bool a1 = !e01 && fits(5, f1);
+  const bool r4 = fits(4, f0), r6 = fits(6, f0), r5 = fits(5, f1);
+  const bool a0 = (e01 & r6) | (!e01 & r4);
+  const bool a1 = !e01 & r5;
   const uint32_t p2 = min(lowbit(m2 & ~(b0 | b1)), min(a0 ? p0 : kNone, a1 ? p1 : kNone));
   load(p2, f2);
   const uint32_t b2 = 1u << (p2 & 31u);
   const bool e02 = p0 == p2, e12 = p1 == p2;
-  const bool c0 = e01 ? (e02 ? fits(14, f0) : fits(10, f0)) : (e02 ? fits(12, f0) : fits(8, f0));
-  const bool c1 = !e01 && (e12 ? fits(13, f1) : fits(9, f1));
-  const bool c2 = !e02 && !e12 && fits(11, f2);
+  const bool r8 = fits(8, f0), r10 = fits(10, f0), r12 = fits(12, f0), r14 = fits(14, f0);
+  const bool r9 = fits(9, f1), r13 = fits(13, f1), r11 = fits(11, f2);
+  const bool c0 = (e01 & ((e02 & r14) | (!e02 & r10))) | (!e01 & ((e02 & r12) | (!e02 & r8)));
+  const bool c1 = !e01 & ((e12 & r13) | (!e12 & r9));
+  const bool c2 = !e02 & !e12 & r11;
   const uint32_t p3 = min(min(lowbit(m3 & ~(b0 | b1 | b2)), c0 ? p0 : kNone),
                           min(c1 ? p1 : kNone, c2 ? p2 : kNone));
   // card fields as arithmetic shifts: a selection without a card makes the word negative

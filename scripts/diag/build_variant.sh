@@ -9,6 +9,7 @@ make -s -C "$P"
 mkdir -p "$R/lib_ab" "/tmp/ab_build_$NAME"
 objs=()
 for o in "$P"/build/*.o; do
+  case "$o" in *_fault.o) continue ;; esac  # (lib/libpas_fault.so's objects)
   if [ "$(basename "$o" .o)" = "$SRC" ]; then
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result \
       -I"$R/include" -I"$P/csrc" $DEFS -c "${SRCFILE:-$P/csrc/$SRC.hip}" -o "/tmp/ab_build_$NAME/$SRC.o"
