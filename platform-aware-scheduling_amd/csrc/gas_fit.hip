@@ -656,6 +656,29 @@ __device__ __forceinline__ void put_result(ResOut res, uint64_t* __restrict__ fi
   }
 }
 
+// Word results of a batch of fewer than 2^31 result bytes (every C3-sized batch): one buffer
+// over all rows, a row's byte offset p * ld * 4 as the store's scalar offset.  The per-row
+// form (put_result above) builds a 64-bit row base and a buffer descriptor per pod, ~8 scalar
+// instructions against 2 here.
+struct ResSoff {
+  uint32_t* w;
+  uint32_t ld4;    // ld * 4
+  uint32_t bytes;  // the whole result buffer, P * ld * 4 < 2^31
+  __device__ ResSoff(const ResOut& r, int32_t P)
+      : w(r.w), ld4((uint32_t)r.ld * 4u), bytes((uint32_t)P * ((uint32_t)r.ld * 4u)) {}
+};
+
+template <bool kBits>
+__device__ __forceinline__ void put_result(ResSoff res, uint64_t* __restrict__ fit, int64_t p,
+                                           int32_t N, int32_t n, bool valid, uint32_t out) {
+  static_assert(!kBits, "bitmap results take put_result(ResOut)");
+  // one descriptor over the whole buffer; a lane past N stores at the buffer's end (vector
+  // offset = its size: out of range, dropped whether or not the check adds the scalar offset)
+  const __amdgpu_buffer_rsrc_t all = __builtin_amdgcn_make_buffer_rsrc(res.w, 0, res.bytes, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b32(out, all, valid ? n * 4 : res.bytes,
+                                        (int32_t)((uint32_t)p * res.ld4), PAS_GAS_STORE_AUX);
+}
+
 // Blocks of the fit kernels cover (node block, pod chunk) pairs.  A 1-D grid is mapped so
 // that every chunk of a node block runs on the same XCD (block b runs on XCD b % 8,
 // MI355X_MICROARCH.md): pairs are ordered node-major and each XCD takes a contiguous run of
@@ -1416,14 +1439,14 @@ __device__ __forceinline__ uint32_t multi_seq(const int64_t (*free)[Q],  // [kMa
 // the rows of kMB pods in its own LDS slice (one contiguous copy: rows sit in list order) and
 // reads them back with broadcast LDS reads (values in VGPRs).  No block barrier: a wave
 // waiting for its copy does not hold up the other waves of the block.
-template <int Q, int SKIP, bool kBits>
+template <int Q, int SKIP, bool kBits, class RO>
 __device__ __forceinline__ void multi_list(const int64_t* __restrict__ free_t, GasSel* stage,
                                            int64_t* tab_base, uint32_t node_ok,
                                            int32_t N, int32_t n, bool valid,
                                            const int32_t* __restrict__ list,
                                            const GasSel* __restrict__ sels,
                                            const int32_t* __restrict__ count, const BlockTile& bt,
-                                           ResOut res,
+                                           RO res,
                                            uint64_t* __restrict__ fit) {
   const int32_t lane = threadIdx.x & 63;
   const uint64_t live = __ballot(valid && node_ok != 0u);
@@ -1500,14 +1523,14 @@ __device__ __forceinline__ void multi_list(const int64_t* __restrict__ free_t, G
 // whole groups; per group the node's cards are ranked once, then batches of kMB pods (their
 // 64-bit rows for the current-free checks and their rank rows) are staged as in multi_list.
 // LDS: the FreeTab copy, then the sorted rows of the ranking, overlaid by the batch stage.
-template <int Q, int SKIP, bool kBits>
+template <int Q, int SKIP, bool kBits, class RO>
 __device__ __forceinline__ void rseq_list(const int64_t* __restrict__ free_t, char* wlds,
                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                           const int32_t* __restrict__ list,
                                           const GasSel* __restrict__ sels,
                                           const GasRSeq* __restrict__ rq,
                                           const int64_t* __restrict__ srt, int64_t item0,
-                                          int32_t cnt, const BlockTile& bt, ResOut res,
+                                          int32_t cnt, const BlockTile& bt, RO res,
                                           uint64_t* __restrict__ fit) {
   constexpr int kC = Q - 1;
   const int32_t lane = threadIdx.x & 63;
@@ -1651,14 +1674,14 @@ __device__ __forceinline__ uint32_t rfour(const uint32_t (&fa)[kC], const uint32
 // The closed-form four-selection pods of a list with a skipped kind: groups of 31 pods (their
 // 4 full-mask rows ranked), a chunk takes whole groups; per group the node's cards are ranked
 // once, then batches of kFourMB pods (FourStage + GasRFour) are staged as in rseq_list.
-template <int Q, int SKIP, bool kBits>
+template <int Q, int SKIP, bool kBits, class RO>
 __device__ __forceinline__ void rfour_list(const int64_t* __restrict__ free_t, char* wlds,
                                            uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                            const int32_t* __restrict__ list,
                                            const GasSel* __restrict__ sels,
                                            const GasRFour* __restrict__ rf,
                                            const int64_t* __restrict__ srt, int64_t item0,
-                                           int32_t cnt, const BlockTile& bt, ResOut res,
+                                           int32_t cnt, const BlockTile& bt, RO res,
                                            uint64_t* __restrict__ fit) {
   constexpr int kC = Q - 1;
   const int32_t lane = threadIdx.x & 63;
@@ -1719,7 +1742,7 @@ __device__ __forceinline__ void rfour_list(const int64_t* __restrict__ free_t, c
 
 // The closed-form four-selection lists l = 1 .. Q (list 0 files its four-selection pods as
 // sequential ones).  item0: the first sorted row of list 1's groups (after the sequential ones).
-template <int Q, bool kBits, int l = 1>
+template <int Q, bool kBits, int l = 1, class RO>
 __device__ __forceinline__ void four_lists(const int64_t* __restrict__ free_t, char* wlds,
                                            uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                            int32_t P, const int32_t* __restrict__ multi,
@@ -1727,7 +1750,7 @@ __device__ __forceinline__ void four_lists(const int64_t* __restrict__ free_t, c
                                            const GasRFour* __restrict__ rf,
                                            const int64_t* __restrict__ srt, int64_t item0,
                                            const int32_t* __restrict__ counts, const BlockTile& bt,
-                                           ResOut res, uint64_t* __restrict__ fit) {
+                                           RO res, uint64_t* __restrict__ fit) {
   constexpr int L = l * kClasses + kClsFour;
   const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[L]);
   rfour_list<Q, l - 1, kBits>(free_t, wlds, node_ok, N, n, valid, multi + (int64_t)L * P,
@@ -1742,7 +1765,7 @@ __device__ __forceinline__ void four_lists(const int64_t* __restrict__ free_t, c
 // The lists of pods with 4 to 8 selections (class 2 of each kind-skip list): ranked where a
 // kind is skipped (rseq_list), else on 64-bit values (multi_list).  item0: the first sorted
 // row of list 1's groups (after the two- and three-selection lists' rows).
-template <int Q, bool kBits, int l = 0>
+template <int Q, bool kBits, int l = 0, class RO>
 __device__ __forceinline__ void seq_lists(const int64_t* __restrict__ free_t, char* wlds,
                                           uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                           int32_t P, const int32_t* __restrict__ multi,
@@ -1750,7 +1773,7 @@ __device__ __forceinline__ void seq_lists(const int64_t* __restrict__ free_t, ch
                                           const GasRSeq* __restrict__ rq,
                                           const int64_t* __restrict__ srt, int64_t item0,
                                           const int32_t* __restrict__ counts, const BlockTile& bt,
-                                          ResOut res, uint64_t* __restrict__ fit) {
+                                          RO res, uint64_t* __restrict__ fit) {
   constexpr int L = l * kClasses + 2;
   int32_t cnt = 0;
   if constexpr (l == 0 || Q == 1) {
@@ -1771,13 +1794,13 @@ __device__ __forceinline__ void seq_lists(const int64_t* __restrict__ free_t, ch
 }
 
 
-template <int Q, int SKIP, bool kBits>
+template <int Q, int SKIP, bool kBits, class RO>
 __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
                                              uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                              const GasRSingle* __restrict__ rs,
                                              const int64_t* __restrict__ srt, int64_t item0,
                                              int32_t cnt, const BlockTile& bt, int64_t* lds,
-                                             GasRSingle* stage, ResOut res,
+                                             GasRSingle* stage, RO res,
                                              uint64_t* __restrict__ fit) {
   constexpr int kSkip = Q == 1 ? -1 : SKIP;
   constexpr int C = Q - (kSkip >= 0 ? 1 : 0);
@@ -1812,8 +1835,9 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
     if constexpr (kBits) {
       out = m ? 0x80000000u : 0u;
     } else {
-      const int32_t base = ((w >> 24) & 0xF) == 1 ? (int32_t)0x81000000u : (int32_t)0x80000000u;
-      out = (uint32_t)min(((int32_t)ffbl(m) >> 2) ^ base, 0);
+      // base = 0x80000000 | steps << 24 (steps <= 1): one scalar AND, a three-input XOR
+      const int32_t sbits = (int32_t)((uint32_t)w & 0x0F000000u);
+      out = (uint32_t)min((((int32_t)ffbl(m) >> 2) ^ sbits) ^ (int32_t)0x80000000u, 0);
     }
     put_result<kBits>(res, fit, pod, N, n, valid, out);
   };
@@ -1851,14 +1875,14 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
   }
 }
 
-template <int Q, bool kBits, int L = 0>
+template <int Q, bool kBits, int L = 0, class RO>
 __device__ __forceinline__ void rsingle_lists(const int64_t* __restrict__ free_t,
                                               uint32_t node_ok, int32_t N, int32_t n, bool valid,
                                               int32_t P, const GasRSingle* __restrict__ rs,
                                               const int64_t* __restrict__ srt, int64_t item0,
                                               const int32_t* __restrict__ counts,
                                               const BlockTile& bt, int64_t* lds,
-                                              GasRSingle* stage, ResOut res,
+                                              GasRSingle* stage, RO res,
                                               uint64_t* __restrict__ fit) {
   const int32_t cnt = __builtin_amdgcn_readfirstlane(counts[L]);
   rsingle_list<Q, L - 1, kBits>(free_t, node_ok, N, n, valid, rs + (int64_t)L * P, srt, item0,
@@ -1874,11 +1898,11 @@ struct SingleLds {
   static constexpr size_t kBytes = sizeof(int64_t) * Q * kRankItems + sizeof(GasRSingle) * kPodBatch;
 };
 
-template <int Q, bool kBits>
+template <int Q, bool kBits, class RO>
 __device__ __forceinline__ void rfit_single_body(
     const BlockTile& bt, char* wlds, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs,
-    const int64_t* __restrict__ srt, const int32_t* __restrict__ counts, ResOut res,
+    const int64_t* __restrict__ srt, const int32_t* __restrict__ counts, RO res,
     uint64_t* __restrict__ fit) {
   // chunks past every list's end: nothing to load
   int32_t most = 0;
@@ -1898,7 +1922,8 @@ __device__ __forceinline__ void rfit_single_body(
                           res, fit);
 }
 
-template <int Q, bool kBits>
+// kSoff: word results through put_result(ResSoff) (a batch of < 2^31 result bytes)
+template <int Q, bool kBits, bool kSoff>
 __global__ __launch_bounds__(kSingleTpb) void gas_rfit_single_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSingle* __restrict__ rs, const int64_t* __restrict__ srt,
@@ -1907,8 +1932,12 @@ __global__ __launch_bounds__(kSingleTpb) void gas_rfit_single_kernel(
   __shared__ int4 smem[kSingleTpb / 64][SingleLds<Q>::kBytes / 16];  // a slice per wave
   if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  rfit_single_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
-                             n_cards, free_t, rs, srt, counts, res, fit);
+  if constexpr (kSoff)
+    rfit_single_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                               n_cards, free_t, rs, srt, counts, ResSoff(res, P), fit);
+  else
+    rfit_single_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                               n_cards, free_t, rs, srt, counts, res, fit);
 }
 
 // A row of packed ranks (byte j = kind j) checked at one card: x = the card's packed ranks
@@ -1956,12 +1985,12 @@ __device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint3
     for (int j = 0; j < C; ++j) g3[j] = r.rep[2][j];
     const uint32_t m3 = (w & kSame03) ? m0 : (w & kSame13) ? m1 : rmask<C>(fa, fb, g3);
     const uint32_t x1 = tab[min(p1 >> 2, 7u) * 64 + lane];
-    uint32_t touched;
-    if (p0 == p1) {
-      touched = rpoint<C>(x0, r.pk[3]) ? p0 : ~0u;
-    } else {
-      touched = min(rpoint<C>(x0, r.pk[1]) ? p0 : ~0u, rpoint<C>(x1, r.pk[2]) ? p1 : ~0u);
-    }
+    // c0 == c1: row 6 at c0; else row 4 at c0, row 5 at c1 (every check evaluated, combined
+    // bitwise: no divergent branch)
+    const bool e01 = p0 == p1;
+    const bool r6 = rpoint<C>(x0, r.pk[3]), r4 = rpoint<C>(x0, r.pk[1]);
+    const bool r5 = rpoint<C>(x1, r.pk[2]);
+    const uint32_t touched = min(((e01 & r6) | (!e01 & r4)) ? p0 : ~0u, (!e01 & r5) ? p1 : ~0u);
     const uint32_t un = lowbit(m3 & ~(1u << (p0 & 31u)) & ~(1u << (p1 & 31u)));
     const uint32_t p2 = min(un, touched);
     word |= ((int32_t)p2 >> 2) << 6;
@@ -1973,7 +2002,7 @@ __device__ __forceinline__ uint32_t rclosed(const uint32_t (&fa)[C], const uint3
   return (uint32_t)min(word ^ (int32_t)(0x80000000u | ((uint32_t)S << 24)), 0);
 }
 
-template <int Q, int SKIP, int S, bool kBits>
+template <int Q, int SKIP, int S, bool kBits, class RO>
 __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, uint32_t node_ok,
                                             int32_t N, int32_t n, bool valid,
                                             const GasRMulti* __restrict__ rm,
@@ -1981,7 +2010,7 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
                                             const int64_t* __restrict__ srt, int64_t item0,
                                             int32_t cnt, const BlockTile& bt, int64_t* lds,
                                             GasRMulti* stage, uint32_t* tab,
-                                            ResOut res,
+                                            RO res,
                                             uint64_t* __restrict__ fit) {
   constexpr int kSkip = Q == 1 ? -1 : SKIP;
   constexpr int C = Q - (kSkip >= 0 ? 1 : 0);
@@ -2034,7 +2063,7 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
   }
 }
 
-template <int Q, bool kBits, int L = 0>
+template <int Q, bool kBits, int L = 0, class RO>
 __device__ __forceinline__ void rmulti_lists(const int64_t* __restrict__ free_t, uint32_t node_ok,
                                              int32_t N, int32_t n, bool valid, int32_t P,
                                              const GasRMulti* __restrict__ rm,
@@ -2042,7 +2071,7 @@ __device__ __forceinline__ void rmulti_lists(const int64_t* __restrict__ free_t,
                                              const int64_t* __restrict__ srt, int64_t item0,
                                              const int32_t* __restrict__ counts,
                                              const BlockTile& bt, int64_t* lds, GasRMulti* stage,
-                                             uint32_t* tab, ResOut res,
+                                             uint32_t* tab, RO res,
                                              uint64_t* __restrict__ fit) {
   // slot L: list L / 2, class L % 2 (S = 2 + L % 2); counts of the multi lists [l][kClasses]
   constexpr int l = L / 2, S = 2 + L % 2;
@@ -2082,12 +2111,12 @@ struct MultiLds {
   static constexpr size_t kSeq = sizeof(int64_t) * kMaxCards * 64 * kC + kSeqOver;
 };
 
-template <int Q, bool kBits>
+template <int Q, bool kBits, class RO>
 __device__ __forceinline__ void rfit_closed_body(
     const BlockTile& bt, char* w, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
     const int32_t* __restrict__ rw, const int64_t* __restrict__ srt,
-    const int32_t* __restrict__ counts, ResOut res, uint64_t* __restrict__ fit) {
+    const int32_t* __restrict__ counts, RO res, uint64_t* __restrict__ fit) {
   const int32_t n = bt.node_block * kClosedTpb + threadIdx.x;
   const bool in = n < N;
   const int32_t nc = in ? n_cards[n] : 0;
@@ -2112,7 +2141,7 @@ __device__ __forceinline__ void rfit_closed_body(
 #endif
 template <int Q>
 constexpr int closed_waves() { return Q < 4 ? PAS_GAS_CLOSED_WAVES : 5; }
-template <int Q, bool kBits>
+template <int Q, bool kBits, bool kSoff>
 __global__ __launch_bounds__(kClosedTpb) __attribute__((amdgpu_waves_per_eu(closed_waves<Q>()))) void gas_rfit_closed_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRMulti* __restrict__ rm,
@@ -2121,17 +2150,21 @@ __global__ __launch_bounds__(kClosedTpb) __attribute__((amdgpu_waves_per_eu(clos
   __shared__ int4 smem[kClosedTpb / 64][MultiLds<Q>::kRanked / 16];
   if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  rfit_closed_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
-                             n_cards, free_t, rm, rw, srt, counts, res, fit);
+  if constexpr (kSoff)
+    rfit_closed_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                               n_cards, free_t, rm, rw, srt, counts, ResSoff(res, P), fit);
+  else
+    rfit_closed_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                               n_cards, free_t, rm, rw, srt, counts, res, fit);
 }
 
-template <int Q, bool kBits>
+template <int Q, bool kBits, class RO>
 __device__ __forceinline__ void rfit_seq_body(
     const BlockTile& bt, char* w, int32_t N, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
     const GasRFour* __restrict__ rf, const int64_t* __restrict__ srt,
     const int32_t* __restrict__ multi, const GasSel* __restrict__ sels,
-    const int32_t* __restrict__ counts, ResOut res, uint64_t* __restrict__ fit) {
+    const int32_t* __restrict__ counts, RO res, uint64_t* __restrict__ fit) {
   const int32_t n = bt.node_block * kSeqTpb + threadIdx.x;
   const bool in = n < N;
   const int32_t nc = in ? n_cards[n] : 0;
@@ -2156,7 +2189,7 @@ __device__ __forceinline__ void rfit_seq_body(
   }
 }
 
-template <int Q, bool kBits>
+template <int Q, bool kBits, bool kSoff>
 __global__ __launch_bounds__(kSeqTpb) void gas_rfit_seq_kernel(
     int32_t N, int32_t K, int32_t P, const int32_t* __restrict__ n_cards,
     const int64_t* __restrict__ free_t, const GasRSeq* __restrict__ rq,
@@ -2166,8 +2199,12 @@ __global__ __launch_bounds__(kSeqTpb) void gas_rfit_seq_kernel(
   __shared__ int4 smem[kSeqTpb / 64][MultiLds<Q>::kSeq / 16];
   if (fit_aborted(res.abort, res.epoch)) return;
   const int32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P, n_cards,
-                          free_t, rq, rf, srt, multi, sels, counts, res, fit);
+  if constexpr (kSoff)
+    rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                            n_cards, free_t, rq, rf, srt, multi, sels, counts, ResSoff(res, P), fit);
+  else
+    rfit_seq_body<Q, kBits>(block_tile(chunks), reinterpret_cast<char*>(smem[wave]), N, P,
+                            n_cards, free_t, rq, rf, srt, multi, sels, counts, res, fit);
 }
 
 // ---------------------------------------------------------------------------- generic path
@@ -2679,26 +2716,29 @@ int gas_fit_launch(pas_ctx* ctx, int32_t n_pods, int32_t max_containers, int32_t
   // node) words alone (the fast kernels skip pods past 8 selections and nodes past 8 cards),
   // so it runs beside them, after the single-selection kernel on ss; bitmap rows are or-ed
   // into the fast kernels' words, so it runs after the join
-  switch (Q * 2 + (bits ? 1 : 0)) {
-#define PAS_GAS_CASE(QQ, B)                                                                    \
-  case QQ * 2 + B:                                                                             \
+  // word results of < 2^31 bytes: row offsets as the stores' 32-bit scalar offsets (ResSoff)
+  const bool soff = !bits && (int64_t)n_pods * ld_res * 4 < ((int64_t)1 << 31);
+  switch (Q * 4 + (bits ? 1 : 0) * 2 + (soff ? 1 : 0)) {
+#define PAS_GAS_CASE(QQ, B, SO)                                                                \
+  case QQ * 4 + B * 2 + SO:                                                                    \
     if (PAS_GAS_SEQ_FIRST)                                                                     \
-      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
+      gas_rfit_seq_kernel<QQ, B, SO><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                         \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, rfour, srt_m, multi, \
           sels, counts + NL, ch_q, ro, d_fit);                                                  \
-    gas_rfit_closed_kernel<QQ, B><<<nb_c * ch_c, kClosedTpb, 0, s>>>(                          \
+    gas_rfit_closed_kernel<QQ, B, SO><<<nb_c * ch_c, kClosedTpb, 0, s>>>(                      \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rmulti, rword, srt_m,         \
         counts + NL, ch_c, ro, d_fit);                                                          \
     if (!PAS_GAS_SEQ_FIRST)                                                                    \
-      gas_rfit_seq_kernel<QQ, B><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                             \
+      gas_rfit_seq_kernel<QQ, B, SO><<<nb_q * ch_q, kSeqTpb, 0, qs>>>(                         \
           N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rseq, rfour, srt_m, multi, \
           sels, counts + NL, ch_q, ro, d_fit);                                                  \
-    gas_rfit_single_kernel<QQ, B><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                         \
+    gas_rfit_single_kernel<QQ, B, SO><<<nb_s * ch_s, kSingleTpb, 0, ss>>>(                     \
         N, K, n_pods, g.n_cards, static_cast<int64_t*>(g.free_t), rsingle, srt_s, counts,       \
         ch_s, ro, d_fit);                                                                       \
     break;
-    PAS_GAS_CASE(1, 0) PAS_GAS_CASE(2, 0) PAS_GAS_CASE(3, 0) PAS_GAS_CASE(4, 0)
-    PAS_GAS_CASE(1, 1) PAS_GAS_CASE(2, 1) PAS_GAS_CASE(3, 1) PAS_GAS_CASE(4, 1)
+    PAS_GAS_CASE(1, 0, 0) PAS_GAS_CASE(2, 0, 0) PAS_GAS_CASE(3, 0, 0) PAS_GAS_CASE(4, 0, 0)
+    PAS_GAS_CASE(1, 0, 1) PAS_GAS_CASE(2, 0, 1) PAS_GAS_CASE(3, 0, 1) PAS_GAS_CASE(4, 0, 1)
+    PAS_GAS_CASE(1, 1, 0) PAS_GAS_CASE(2, 1, 0) PAS_GAS_CASE(3, 1, 0) PAS_GAS_CASE(4, 1, 0)
 #undef PAS_GAS_CASE
     default: return set_error(ctx, PAS_EINVAL, "pas_gas_fit: n_res out of range");
   }
