@@ -625,6 +625,9 @@ typedef unsigned long long lane_mask;  // one bit per lane of the wave (ballot)
 #ifndef PAS_GAS_ABLATE
 #define PAS_GAS_ABLATE 0  // diagnostic timing builds only: 1 = no result stores (outputs wrong)
 #endif
+#ifndef PAS_GAS_RUN_FAST
+#define PAS_GAS_RUN_FAST 1  // full runs of pods as straight-line code (0: every pod tested)
+#endif
 #ifndef PAS_GAS_STORE_AUX
 #define PAS_GAS_STORE_AUX 2  // result word store cache policy: nt (0: plain global store)
 #endif
@@ -1862,6 +1865,19 @@ __device__ __forceinline__ void rsingle_list(const int64_t* __restrict__ free_t,
     // eight pods per iteration, so the records' LDS offsets are constants off one address
     for (int32_t j0 = 0; j0 < nb; j0 += 8) {
       const GasRSingle* st = lane_ptr(stage) + j0;
+      if (PAS_GAS_RUN_FAST && j0 + 8 <= nb) {
+        // a full run of 8: straight-line code (no exit test between pods), so the pods'
+        // record reads and tests interleave
+        GasRSingle r[8];
+        int32_t w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) r[u] = st[u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = __builtin_amdgcn_readfirstlane(r[u].word);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) one_pod(r[u], w[u]);
+        continue;
+      }
 #pragma unroll
       for (int u = 0; u < 8; u += 2) {
         if (j0 + u >= nb) break;
@@ -2048,6 +2064,16 @@ __device__ __forceinline__ void rmulti_list(const int64_t* __restrict__ free_t, 
       // four pods per iteration: their records' LDS offsets are constants off one address
       for (int32_t j0 = 0; j0 < nb; j0 += 4) {
         const GasRMulti* st = lane_ptr(stage) + j0;
+        if (PAS_GAS_RUN_FAST && j0 + 4 <= nb) {  // a full run: straight-line, as rsingle_list
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const uint32_t w = (uint32_t)__builtin_amdgcn_readlane(wd, j0 + u);
+            uint32_t out = rclosed<C, S>(fa, fb, st[u], w, tab, lane, node_ok);
+            if constexpr (kBits) out = out ? node_ok : 0u;
+            put_result<kBits>(res, fit, w & 0xFFFFFF, N, n, valid, out);
+          }
+          continue;
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           if (j0 + u >= nb) break;
