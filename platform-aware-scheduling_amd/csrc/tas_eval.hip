@@ -752,16 +752,24 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     uint64_t npr;
     load(ru1, nv, &npr);  // the next run in flight during this rule's compares
     if (ru.metric >= 0 && ru.metric < M && ru.op >= 0 && ru.op <= 2) {
+      // the rule as the value range it hits, [lo, hi] (empty: lo > hi), once per rule: the
+      // word loop is two compares per word, no branch on the operator
       int64_t tm = 0;
       const int sat = target_scaled(ru.target, scale_tab, ru.metric, &tm);
+      int64_t lo = 1, hi = 0;
+      if (ru.op == PAS_OP_LESS_THAN) {  // v < t
+        if (sat > 0) lo = INT64_MIN, hi = INT64_MAX;
+        else if (sat == 0 && tm != INT64_MIN) lo = INT64_MIN, hi = tm - 1;
+      } else if (ru.op == PAS_OP_GREATER_THAN) {  // v > t
+        if (sat < 0) lo = INT64_MIN, hi = INT64_MAX;
+        else if (sat == 0 && tm != INT64_MAX) lo = tm + 1, hi = INT64_MAX;
+      } else if (sat == 0) {  // v == t
+        lo = hi = tm;
+      }
 #pragma unroll
       for (int k = 0; k < kRun; ++k) {
         const bool valid = (gw0 + k) * 64 + lane < N;
-        bool hit;
-        if (ru.op == PAS_OP_LESS_THAN) hit = sat > 0 || (sat == 0 && v[k] < tm);
-        else if (ru.op == PAS_OP_GREATER_THAN) hit = sat < 0 || (sat == 0 && v[k] > tm);
-        else hit = sat == 0 && v[k] == tm;
-        const uint64_t mask = __ballot(hit && valid);
+        const uint64_t mask = __ballot((v[k] >= lo) & (v[k] <= hi) & valid);
         acc = lane == k ? (acc | (mask & pr)) : acc;
       }
     }
