@@ -250,3 +250,32 @@ def test_result_row_pitch(ctx, oracle, extra):
     assert (got[:, n:] == 0xDEADBEEF).all()
     with pytest.raises(pas_amd.PasError):
         ctx.gas_fit_ld_device(gen, p, c, 0, req_t, mask_t, ncont_t, res_t, n - 1, stream=stream)
+
+
+@pytest.mark.parametrize("past", [False, True])
+def test_result_batches_either_side_of_2gib(ctx, oracle, past):
+    """Word results of < 2^31 bytes are stored through one buffer descriptor with the row
+    offset as the store's scalar offset (gas_fit.hip, ResSoff); a batch of >= 2^31 bytes (here
+    through a pitch of ~2.7M words) takes the per-row descriptors.  Same words either way, the
+    padding untouched (its last column included)."""
+    rng = np.random.default_rng(77)
+    n_cards, cap, used, req, mask, ncont = random_wide(rng, 1000, 8, 3, 200, 3, 8)
+    want = oracle.gas_fit(n_cards, cap, used, req, mask, ncont, 0)
+    gen = _upload(ctx, n_cards, cap, used)
+    dev = torch.device("cuda", 0)
+    p, c, _ = req.shape
+    n = len(n_cards)
+    ld = (1 << 31) // (4 * p) + 64 if past else n + 96
+    assert (p * ld * 4 >= 1 << 31) == past
+    res_t = torch.full((p, ld), -0x21524111, dtype=torch.int32, device=dev)  # 0xDEADBEEF
+    stream = torch.cuda.current_stream()
+    ctx.gas_fit_ld_device(gen, p, c, 0, torch.from_numpy(req).to(dev),
+                          torch.from_numpy(mask.view(np.int32)).to(dev),
+                          torch.from_numpy(ncont).to(dev), res_t, ld, stream=stream)
+    torch.cuda.synchronize()
+    got = res_t[:, : n + 64].cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[:, :n], want)
+    assert (got[:, n:] == 0xDEADBEEF).all()
+    assert (res_t[:, -1].cpu().numpy().view(np.uint32) == 0xDEADBEEF).all()
+    del res_t
+    torch.cuda.empty_cache()
