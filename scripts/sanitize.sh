@@ -12,8 +12,8 @@
 # `-m "not gpu"` suite runs, minus the two files whose subjects live in HIP translation
 # units the host-only library does not contain (test_abi.py: the ABI version and
 # pas_parse_operator, pas_api.hip; test_labels.py: pas_label_patch_json, tas_labels.hip).
-# Under TSan the three gloo process-group files are left out as well (test_bench_launch.py,
-# test_dist_gloo.py, test_shard.py: their spawned ranks never finish the rendezvous with
+# Under TSan the four gloo process-group files are left out as well (test_bench_launch.py,
+# test_dist_gloo.py, test_grid_split.py, test_shard.py: their spawned ranks never finish the rendezvous with
 # libtsan preloaded; none of them calls the host C++).
 set -u
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
@@ -62,7 +62,7 @@ run asan_ubsan "$(gcc -print-file-name=libasan.so)" "$ROOT/$SAN/libpas_host_asan
     "$ROOT/oracle/build/liboracle_asan.so" "$TMP/planted_asan.so" "overflow(4)" || rc=1
 run tsan "$(gcc -print-file-name=libtsan.so)" "$ROOT/$SAN/libpas_host_tsan.so" \
     "$ROOT/oracle/build/liboracle_tsan.so" "$TMP/planted_tsan.so" "race()" \
-    "--ignore=tests/test_bench_launch.py --ignore=tests/test_dist_gloo.py --ignore=tests/test_shard.py" \
+    "--ignore=tests/test_bench_launch.py --ignore=tests/test_dist_gloo.py --ignore=tests/test_grid_split.py --ignore=tests/test_shard.py" \
     || rc=1
 [ $rc = 0 ] && echo "sanitize: clean" || echo "sanitize: FAILED"
 exit $rc
