@@ -19,6 +19,8 @@ __global__ __launch_bounds__(256) void body(uint32_t* out, uint32_t seed) {
   }
   const uint32_t c = seed | 1u;
   const uint64_t c64 = (uint64_t)c << 32 | c;
+  const uint64_t msk = __ballot(a[0] & 1u), ones = __ballot(1);
+  if constexpr (FORM == 11) asm volatile("v_cmp_gt_u32_e32 vcc, %0, %1" : : "v"(c), "v"(a[1]) : "vcc");
   for (int it = 0; it < kIters; ++it) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -28,8 +30,36 @@ __global__ __launch_bounds__(256) void body(uint32_t* out, uint32_t seed) {
         asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(b[k]) : "v"(c64));
       } else if constexpr (FORM == 2) {
         asm volatile("v_bitop3_b32 %0, %0, %1, %2 bitop3:0x80" : "+v"(a[k]) : "v"(c), "v"(c));
-      } else {
+      } else if constexpr (FORM == 3) {
         asm volatile("v_cmp_le_i64_e32 vcc, %0, %1" : : "v"(b[k]), "v"(c64) : "vcc");
+      } else if constexpr (FORM == 4) {  // carry-in from an SGPR pair (the search's form)
+        asm volatile("v_addc_co_u32_e64 %0, s[20:21], %0, %0, s[22:23]" : "+v"(a[k]) : : "s20", "s21");
+      } else if constexpr (FORM == 5) {  // carry in and out through vcc
+        asm volatile("v_addc_co_u32_e32 %0, vcc, %0, %0, vcc" : "+v"(a[k]) : : "vcc");
+      } else if constexpr (FORM == 6) {
+        asm volatile("v_lshl_add_u32 %0, %0, 3, %1" : "+v"(a[k]) : "v"(c));
+      } else if constexpr (FORM == 7) {
+        asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[k]) : "v"(c));
+      } else if constexpr (FORM == 8) {
+        asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "v"(a[(k + 1) & 7]));
+      } else if constexpr (FORM == 9) {
+        asm volatile("v_lshrrev_b32_e32 %0, 4, %0" : "+v"(a[k]));
+      } else if constexpr (FORM == 10) {  // select on a mask from a compare (SGPR pair)
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "s"(msk));
+      } else if constexpr (FORM == 11) {  // vcc written by a compare before the loop
+        asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[k]) : "v"(c));
+      } else if constexpr (FORM == 12) {  // all-ones mask
+        asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "s"(ones));
+      } else if constexpr (FORM == 13) {  // mixed: one vcc select per three subtractions
+        if (k & 3)
+          asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a[k]) : "v"(c));
+        else
+          asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(a[k]) : "v"(c));
+      } else {  // mixed, the select on an SGPR pair
+        if (k & 3)
+          asm volatile("v_sub_u32 %0, %0, %1" : "+v"(a[k]) : "v"(c));
+        else
+          asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(a[k]) : "v"(c), "s"(msk));
       }
     }
   }
@@ -63,11 +93,19 @@ int main() {
   hipMalloc(&out, sizeof(uint32_t) * blocks * 256);
   const double insts = (double)blocks * 4 * kIters * 8;  // wave instructions
   const double ghz = p.clockRate / 1e6;
-  const char* names[] = {"v_sub_u32", "v_lshl_add_u64", "v_bitop3_b32", "v_cmp_le_i64"};
-  float t[4] = {run<0>(out, blocks), run<1>(out, blocks), run<2>(out, blocks), run<3>(out, blocks)};
-  for (int f = 0; f < 4; ++f) {
+  const char* names[] = {"v_sub_u32",         "v_lshl_add_u64",    "v_bitop3_b32",
+                         "v_cmp_le_i64",      "v_addc_co_u32_e64", "v_addc_co_u32_e32",
+                         "v_lshl_add_u32",    "v_cndmask_b32_e32", "v_and_or_b32",
+                         "v_lshrrev_b32",     "v_cndmask_e64 cmp", "v_cndmask_e32 vcc=",
+                         "v_cndmask_e64 ~0",  "mix 1 vcc sel:3 sub", "mix 1 e64 sel:3 sub"};
+  float t[15] = {run<0>(out, blocks), run<1>(out, blocks), run<2>(out, blocks),
+                 run<3>(out, blocks), run<4>(out, blocks), run<5>(out, blocks),
+                 run<6>(out, blocks), run<7>(out, blocks), run<8>(out, blocks),
+                 run<9>(out, blocks), run<10>(out, blocks), run<11>(out, blocks),
+                 run<12>(out, blocks), run<13>(out, blocks), run<14>(out, blocks)};
+  for (int f = 0; f < 15; ++f) {
     const double per_simd = insts / (cus * 4);
-    printf("%-16s %.3f ms  %.2f cycles per wave instruction per SIMD (clock %.2f GHz)\n", names[f],
+    printf("%-20s %.3f ms  %.2f cycles per wave instruction per SIMD (clock %.2f GHz)\n", names[f],
            t[f], t[f] * 1e-3 * ghz * 1e9 / per_simd, ghz);
   }
   hipFree(out);
