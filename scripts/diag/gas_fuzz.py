@@ -6,7 +6,7 @@ value ranges, every container count and kind mask, i915 anywhere or absent, extr
 values.  Each case prints one line (the GPU box's hang detector needs output); the first
 mismatch stops the sweep with the case's parameters.
 
-  python scripts/diag/gas_fuzz.py --cases 200 [--seed0 1]
+  python scripts/diag/gas_fuzz.py --cases 200 [--seed0 1] [--bind]
 """
 import argparse
 import os
@@ -23,11 +23,11 @@ import oracle  # noqa: E402  (test infrastructure: the checker)
 import pas_amd  # noqa: E402
 
 
-def case(rng):
+def case(rng, n=None, p=None):
     q = int(rng.integers(1, 5))
     k = int(rng.choice([1, 2, 3, 4, 5, 7, 8]))
-    n = int(rng.integers(1, 1500))
-    p = int(rng.choice([1, 50, 127, 128, 200, 400, 1000, 2500]))
+    n = int(rng.integers(1, 1500)) if n is None else n
+    p = int(rng.choice([1, 50, 127, 128, 200, 400, 1000, 2500])) if p is None else p
     c = int(rng.integers(1, 5))
     i915 = int(rng.integers(-1, q))
     col = max(i915, 0)
@@ -66,6 +66,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=200)
     ap.add_argument("--seed0", type=int, default=1)
+    ap.add_argument("--bind", action="store_true", help="also bind, then fit the committed usage")
     a = ap.parse_args()
     oracle.load()
     ctx = pas_amd.Context(0)
@@ -81,6 +82,25 @@ def main():
         print(f"case {i} seed {seed} {meta} {'ok' if ok else 'MISMATCH'} "
               f"fit {float((want >> 31).mean()) if want.size else 0:.2f} {time.time() - t0:.0f}s",
               flush=True)
+        if ok and a.bind and meta["p"] > 0 and meta["n"] > 0:
+            # binds of random pods to random nodes, committed (bindNode), then a fit on the
+            # committed usage: statuses, words and usage against the oracle's in-order binds
+            rng = np.random.default_rng(seed + 10**6)
+            B = int(rng.integers(1, 300))
+            pods = rng.integers(0, meta["p"], size=B).astype(np.int32)
+            nodes = rng.integers(0, meta["n"], size=B).astype(np.int32)
+            res, st = ctx.gas_bind(seed, seed + 10**7, pods, nodes, *args[3:], i915)
+            w_used, w_res, w_st = oracle.gas_bind(*args, i915, pods, nodes)
+            _, after = ctx.gas_snapshot_get()
+            got2 = ctx.gas_fit(seed + 10**7, *args[3:], i915)
+            want2 = oracle.gas_fit(args[0], args[1], w_used, *args[3:], i915)
+            ok = (np.array_equal(res, w_res) and np.array_equal(st, w_st)
+                  and np.array_equal(after, w_used) and np.array_equal(got2, want2))
+            if not ok:
+                print(f"bind mismatch: res {np.array_equal(res, w_res)} st "
+                      f"{np.array_equal(st, w_st)} used {np.array_equal(after, w_used)} fit "
+                      f"{np.array_equal(got2, want2)}")
+                got, want = got2, want2
         if not ok:
             bad = np.argwhere(got != want)
             print("first mismatches (pod, node, got, want):",
