@@ -510,8 +510,10 @@ def bench_gas(args, world, rank):
                                             args.steps, alg_bytes)
     # The fit kernels are bound by VALU issue, not by HBM: their VALU
     # wave-instructions per step (SQ_INSTS_VALU, committed PMC pass) over the same GPU time,
-    # against the chip's issue peak: 1024 SIMDs x 2.4 GHz / 4 cycles per wave64 VALU
-    # instruction (scripts/diag/issue_rates.hip measures 4.3 for this mix).
+    # against the chip's issue rate at 4 cycles per wave64 VALU instruction: 1024 SIMDs x
+    # 2.4 GHz / 4 (scripts/diag/issue_rates.hip measures 4.3 for this mix; valu_rate.hip has
+    # the per-form costs: 2.4-2.7 for plain VOP2 ops, 4.0-4.8 for the VOP3 and 64-bit forms
+    # the fit loops are made of, so this is the mix's rate, not an absolute ceiling).
     valu = load_traffic("gas_fit_valu_per_step")
     if valu:
         peak = 1024 * 2.4e9 / 4
