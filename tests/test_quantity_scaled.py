@@ -4,6 +4,7 @@ module (k8s.io/apimachinery v0.22.2, not vendored in the reference; the referenc
 sub-milli literal, so these cases are parity unpinned against the reference itself and pinned
 against the published algorithm: the exact decimal, rounded away from zero to 9 fractional
 digits when it takes the inf.Dec path, capped at 2^63 - 1)."""
+import re
 from decimal import ROUND_UP, Decimal, getcontext
 
 import numpy as np
@@ -103,3 +104,50 @@ def test_scaled_argument_errors():
         pas_amd.quantity_to_scaled("1", -1)
     with pytest.raises(pas_amd.PasError):
         pas_amd.quantity_decimals("1.2.3")
+
+
+GRAMMAR = re.compile(r"^[+-]?\d+(\.\d+)?([numkMGTP]|[eE][+-]?\d{1,2})?$")
+ALPHABET = "0123456789.+-eEnumkMGTPKi \t"
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_mutated_literals(seed):
+    """Random edits of valid literals (character swaps, cuts, inserts from the Quantity
+    alphabet, binary suffixes): every call returns a value or PasError, and a literal in the
+    plain decimal grammar (sign, digits, fraction, SI or exponent suffix) matches the decimal
+    restatement (PAS_ENOTEXACT past int64)."""
+    rng = np.random.default_rng(0x0F00 + seed)
+    base = CASES + ["1Ki", "1.5Gi", "16Mi", "+7", "007", "-0", "1e18", "9.9e-10"]
+    compared = 0
+    for _ in range(3000):
+        s = list(base[int(rng.integers(0, len(base)))])
+        for _ in range(int(rng.integers(1, 4))):
+            op = int(rng.integers(0, 3))
+            i = int(rng.integers(0, len(s) + 1))
+            ch = ALPHABET[int(rng.integers(0, len(ALPHABET)))]
+            if op == 0 and s:
+                s[min(i, len(s) - 1)] = ch
+            elif op == 1 and s:
+                del s[min(i, len(s) - 1)]
+            else:
+                s.insert(i, ch)
+        lit = "".join(s)
+        results = []
+        for fn in (pas_amd.quantity_decimals, lambda x: pas_amd.quantity_to_scaled(x, 9),
+                   pas_amd.quantity_to_milli):
+            try:
+                results.append(fn(lit))
+            except pas_amd.PasError as e:
+                results.append(e)
+        if GRAMMAR.match(lit) and not ("e" in lit.lower() and lit[-1] in "EPTGMk"):
+            v = go_value(lit)
+            k = want_decimals(v)
+            assert results[0] == k, lit
+            want = int(v.scaleb(9))
+            if -2**63 <= want < 2**63:
+                assert results[1] == want, lit
+            else:
+                assert isinstance(results[1], pas_amd.PasError), lit
+                assert results[1].code == pas_amd._lib.PAS_ENOTEXACT, lit
+            compared += 1
+    assert compared > 300
