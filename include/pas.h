@@ -202,7 +202,10 @@ int pas_tas_snapshot_update_device(pas_ctx* ctx, uint64_t gen_from, uint64_t gen
  * Order (the reference's is Go-map order + unstable sort.Slice, i.e. unspecified for
  * ties and for operators other than LessThan/GreaterThan): GreaterThan = value
  * descending, LessThan = value ascending, ties by ascending node index; any other
- * operator = ascending node index.  The oracle uses the same rule. */
+ * operator = ascending node index.  The oracle uses the same rule.
+ * The _device form cannot check d_rule_off on the host: each pod's span is read clamped,
+ * [a, b) with a = clamp(rule_off[p], 0, n_rules), b = clamp(rule_off[p+1], a, n_rules), so an
+ * offset array that is not a CSR never takes a kernel outside the rules. */
 int pas_tas_eval(pas_ctx* ctx, uint64_t gen, int32_t n_pods, const pas_rule* rules,
                  const int32_t* rule_off, const pas_rule* prio, const uint64_t* cand,
                  uint32_t flags, uint64_t* pass_out, int32_t* order_out, int32_t* order_len);
@@ -240,7 +243,9 @@ int pas_tas_prioritize_request_device(pas_ctx* ctx, uint64_t gen, const pas_rule
  * rules[rule_off[s] .. rule_off[s+1])), the node set of deschedule.Strategy.Violated
  * (deschedule/strategy.go:31-50), as the bitmap viol_out[s][W64].  The per-node
  * policy lists of nodeStatusForStrategy (deschedule/enforce.go:154-164) are the
- * columns of this matrix. */
+ * columns of this matrix.  The _device forms (and pas_tas_deschedule_device) read d_rule_off
+ * clamped into [0, n_rules] and non-decreasing, in strategy order, so an offset array that is
+ * not a CSR never takes the sweep outside the rules or the strategies. */
 int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const pas_rule* rules,
                        const int32_t* rule_off, uint64_t* viol_out);
 int pas_tas_violations_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
@@ -378,7 +383,9 @@ int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
  * up to PAS_GAS_MAX_CARDS cards, and pods any number of selections (numI915 up to INT64_MAX
  * per container): a container's selections are runs on ascending cards (a card first fit
  * passes over never fits again within the container), evaluated in O(cards).  A fitting pod
- * of more than PAS_GAS_MAX_SELECTIONS selections gets bit 31 | PAS_GAS_SEL_LIMIT << 24. */
+ * of more than PAS_GAS_MAX_SELECTIONS selections gets bit 31 | PAS_GAS_SEL_LIMIT << 24.
+ * The _device forms read d_n_containers[p] clamped into [0, max_containers] (the host form
+ * rejects values outside it with PAS_EINVAL). */
 int pas_gas_fit(pas_ctx* ctx, uint64_t gen, int32_t n_pods, int32_t max_containers,
                 int32_t i915_index, const int64_t* req, const uint32_t* req_mask,
                 const int32_t* n_containers, uint32_t* res_out);

@@ -2292,7 +2292,10 @@ __device__ void fit_pair(const GenericArgs& a, int32_t p, int32_t n) {
     for (int q = 0; q < Q; ++q) cap[q] = a.cap[(int64_t)n * Q + q];
     for (int k = 0; k < ncard; ++k)
       for (int q = 0; q < Q; ++q) w[k][q] = a.used[((int64_t)n * a.K + k) * Q + q];
-    for (int32_t c = 0; fits && c < a.ncont[p]; ++c) {
+    // (clamped as gas_prep_kernel does: a device n_containers past max_containers never
+    // indexes past the pod's request rows)
+    const int32_t nct = min(max(a.ncont[p], 0), a.C);
+    for (int32_t c = 0; fits && c < nct; ++c) {
       const int64_t b = (int64_t)p * a.C + c;
       const uint32_t m = a.mask[b];
       if (m == 0u) continue;  // no GPU resources: no cards (:206-208)

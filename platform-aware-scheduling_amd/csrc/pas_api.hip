@@ -655,7 +655,7 @@ int pas_tas_violations(pas_ctx* ctx, uint64_t gen, int32_t n_strategies, const p
   hipStream_t s = ctx->stream;
   if (n_rules) PAS_HIP(ctx, hipMemcpyAsync(d_rules, rules, b_rules, hipMemcpyHostToDevice, s));
   PAS_HIP(ctx, hipMemcpyAsync(d_off, rule_off, b_off, hipMemcpyHostToDevice, s));
-  rc = tas_violations_launch(ctx, n_strategies, d_rules, d_off, d_viol, s);
+  rc = tas_violations_launch(ctx, n_strategies, n_rules, d_rules, d_off, d_viol, s);
   if (rc) return rc;
   PAS_HIP(ctx, hipMemcpyAsync(viol_out, d_viol, b_viol, hipMemcpyDeviceToHost, s));
   PAS_HIP(ctx, hipStreamSynchronize(s));
@@ -674,7 +674,7 @@ int pas_tas_violations_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
   if (!d_rule_off || !d_viol_out || (n_rules > 0 && !d_rules))
     return set_error(ctx, PAS_EINVAL, "pas_tas_violations_device: null input");
   if ((rc = activate(ctx))) return rc;
-  return tas_violations_launch(ctx, n_strategies, d_rules, d_rule_off, d_viol_out,
+  return tas_violations_launch(ctx, n_strategies, n_rules, d_rules, d_rule_off, d_viol_out,
                                pick_stream(ctx, hip_stream));
 }
 
@@ -1257,7 +1257,7 @@ int pas_tas_deschedule_device(pas_ctx* ctx, uint64_t gen, int32_t n_strategies,
   if (n_strategies > 0 && (!d_rule_off || (n_rules > 0 && !d_rules)))
     return set_error(ctx, PAS_EINVAL, "pas_tas_deschedule_device: null input");
   if ((rc = activate(ctx))) return rc;
-  return tas_deschedule_launch(ctx, n_strategies, d_rules, d_rule_off, d_viol_out,
+  return tas_deschedule_launch(ctx, n_strategies, n_rules, d_rules, d_rule_off, d_viol_out,
                                make_name_plan(n_strategies, name_id), d_labels, d_add_out,
                                d_remove_out, d_total_out, pick_stream(ctx, hip_stream));
 }

@@ -260,8 +260,10 @@ int prio_request_workspace(pas_ctx* ctx, int32_t n_req, size_t* bytes);  // stat
 int prio_request_launch(pas_ctx* ctx, const pas_rule& rule, int32_t n_req, const int32_t* d_req,
                         int32_t* d_pos, int32_t* d_len, void* ws, size_t ws_bytes,
                         hipStream_t s);
-int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
-                          const int32_t* d_rule_off, uint64_t* d_viol, hipStream_t s);
+// (n_rules bounds the device rule_off: offsets are clamped into [0, n_rules], rule_span)
+int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, int32_t n_rules,
+                          const pas_rule* d_rules, const int32_t* d_rule_off, uint64_t* d_viol,
+                          hipStream_t s);
 // A GAS fit whose side-stream wait timed out (device flags) reports here: after the fit's
 // stream was synchronized, PAS_EDEVICE (and the side streams drained) if a wait gave up since
 // the last report, else PAS_OK.
@@ -332,8 +334,9 @@ int label_total_launch(pas_ctx* ctx, int32_t n_parts, int64_t pairs, const int64
                        int64_t* d_total, hipStream_t s);
 // The deschedule sweep with the label plan fused in (pas_tas_deschedule_device): viol as
 // tas_violations_launch, add / rem / total as label_plan_launch on those bitmaps.
-int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
-                          const int32_t* d_rule_off, uint64_t* d_viol, const NamePlan& names,
+int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, int32_t n_rules,
+                          const pas_rule* d_rules, const int32_t* d_rule_off, uint64_t* d_viol,
+                          const NamePlan& names,
                           const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                           int64_t* d_total, hipStream_t s);
 

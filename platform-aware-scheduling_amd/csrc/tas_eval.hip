@@ -195,7 +195,16 @@ struct GroupParams {
   int2* keys;   // [P] scratch: {bucket, cnt0} of each pod
   int4* desc;   // [2P] per bucketed position: {pod, ocol, cnt0, 0}, {r0, r1, 0, 0}
   int32_t no_group;
+  int32_t n_rules;
 };
+
+// Pod / strategy i's rule span from a device rule_off (the _device entry points cannot check
+// it on the host): clamped into [0, n_rules] and non-decreasing, so that an offset array that
+// is not a CSR never indexes past the rules (what is computed for it is unspecified).
+__device__ __forceinline__ int2 rule_span(const int32_t* off, int32_t i, int32_t n_rules) {
+  const int32_t a = min(max(off[i], 0), n_rules);
+  return make_int2(a, min(max(off[i + 1], a), n_rules));
+}
 
 constexpr int kGU = 4;  // pods per thread per round of loads (all issued before use)
 
@@ -230,8 +239,9 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
     for (int u = 0; u < kGU; ++u) {
       const int32_t pc = min(tid + u * kGroupTpb, g.P - 1);
       r[u] = prio ? g.prio[pc] : pas_rule{-1, 0, 0};
-      r0[u] = filt ? g.rule_off[pc] : 0;
-      r1[u] = filt ? g.rule_off[pc + 1] : 0;
+      const int2 sp = filt ? rule_span(g.rule_off, pc, g.n_rules) : make_int2(0, 0);
+      r0[u] = sp.x;
+      r1[u] = sp.y;
     }
     if (tid < g.M) cnt[tid] = g.cnt[tid];
     __syncthreads();
@@ -305,8 +315,9 @@ __device__ void group_body(const GroupParams& g, int32_t* sh) {
     for (int u = 0; u < kGU; ++u) {
       const int32_t p = min(p0 + u * kGroupTpb, g.P - 1);
       kc[u] = g.keys[p];
-      r0[u] = filt ? g.rule_off[p] : 0;
-      r1[u] = filt ? g.rule_off[p + 1] : 0;
+      const int2 sp = filt ? rule_span(g.rule_off, p, g.n_rules) : make_int2(0, 0);
+      r0[u] = sp.x;
+      r1[u] = sp.y;
     }
 #pragma unroll
     for (int u = 0; u < kGU; ++u) {
@@ -682,7 +693,8 @@ struct PlanOut {
 
 template <int kRun, bool kPlan = false>
 __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
-    int32_t N, int32_t M, int32_t W64, int32_t n_strat, const int32_t* __restrict__ rule_off,
+    int32_t N, int32_t M, int32_t W64, int32_t n_strat, int32_t n_rules,
+    const int32_t* __restrict__ rule_off,
     const pas_rule* __restrict__ rules, const int64_t* __restrict__ vals,
     const uint64_t* __restrict__ present, const int64_t* __restrict__ scale_tab,
     uint64_t* __restrict__ viol_out, PlanOut plan) {
@@ -701,9 +713,12 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     return;
   }
   const int32_t pw_lane = min(gw0 + lane, W64 - 1);
-  const int32_t r_begin = rule_off[0], r_end = rule_off[n_strat];
+  // the offsets clamped into [0, n_rules] and non-decreasing (rule_span): strategy s ends at
+  // or before r_end, so the walk below never passes strategy n_strat - 1
+  const int32_t r_begin = min(max(rule_off[0], 0), n_rules);
+  const int32_t r_end = min(max(rule_off[n_strat], r_begin), n_rules);
   int32_t s = 0;
-  int32_t s_end = n_strat > 0 ? rule_off[1] : 0;
+  int32_t s_end = n_strat > 0 ? min(max(rule_off[1], r_begin), r_end) : 0;
   uint64_t acc = 0;  // lane k: word gw0 + k
   int64_t violated = 0;
   if constexpr (kPlan) {  // lane t: strategy t's carried-label words of this wave's run
@@ -745,7 +760,7 @@ __global__ __launch_bounds__(kTpb) void tas_violations_run_kernel(
     while (r >= s_end) {  // the list has passed strategy s: its words are complete
       flush();
       ++s;
-      s_end = rule_off[s + 1];
+      s_end = min(max(rule_off[s + 1], s_end), r_end);
     }
     const pas_rule ru2 = rules[min(r + 2, r_end - 1)];
     int64_t nv[kRun];
@@ -913,7 +928,8 @@ int tas_eval_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas_rul
   const int32_t range_rules = (flags & PAS_TAS_FILTER) ? n_rules : 0;
   RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges,
                   t.scale_tab};
-  GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, tune.no_group};
+  GroupParams gp{n_pods, M,      flags,  d_prio,        d_rule_off,
+                 t.cnt,  d_keys, d_desc, tune.no_group, std::max(n_rules, 0)};
   const size_t group_lds = sizeof(int32_t) * ((size_t)G + 1 + (size_t)M);  // hist | cnt
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_prep_kernel),
@@ -979,7 +995,8 @@ int tas_group_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_prio,
   const int32_t range_rules = d_ranges ? n_rules : 0;
   RangesParams rp{range_rules, M, t.row, d_rules, t.cnt, t.sorted, t.f1k, t.f32, d_ranges,
                   t.scale_tab};
-  GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, 0};
+  GroupParams gp{n_pods, M, flags, d_prio, d_rule_off, t.cnt, d_keys, d_desc, 0,
+                 std::max(n_rules, 0)};
   const size_t group_lds = sizeof(int32_t) * ((size_t)3 * M + 1 + (size_t)M);
   if (group_lds > 64 * 1024)
     PAS_HIP(ctx, hipFuncSetAttribute(reinterpret_cast<const void*>(&tas_prep_kernel),
@@ -991,8 +1008,9 @@ int tas_group_launch(pas_ctx* ctx, int32_t n_pods, const pas_rule* d_prio,
   return PAS_OK;
 }
 
-int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
-                          const int32_t* d_rule_off, uint64_t* d_viol, hipStream_t s) {
+int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, int32_t n_rules,
+                          const pas_rule* d_rules, const int32_t* d_rule_off, uint64_t* d_viol,
+                          hipStream_t s) {
   const TasSnapshot& t = ctx->tas;
   const int32_t W64 = (int32_t)w64(t.n_nodes);
   if (W64 == 0) return PAS_OK;
@@ -1007,15 +1025,16 @@ int tas_violations_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   const int32_t per = (run == 2 || run == 4 || run == 16) ? run : 8;
   const int32_t rwaves = (W64 + per - 1) / per;
   rfn<<<(rwaves + kWaves - 1) / kWaves, kTpb, 0, s>>>(
-      t.n_nodes, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, t.scale_tab,
-      d_viol, PlanOut{NamePlan{}, nullptr, nullptr, nullptr, nullptr});
+      t.n_nodes, t.n_metrics, W64, n_strat, std::max(n_rules, 0), d_rule_off, d_rules, t.vals,
+      t.present, t.scale_tab, d_viol, PlanOut{NamePlan{}, nullptr, nullptr, nullptr, nullptr});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return PAS_OK;
 }
 
-int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules,
-                          const int32_t* d_rule_off, uint64_t* d_viol, const NamePlan& names,
+int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, int32_t n_rules,
+                          const pas_rule* d_rules, const int32_t* d_rule_off, uint64_t* d_viol,
+                          const NamePlan& names,
                           const uint64_t* d_labels, uint64_t* d_add, uint64_t* d_rem,
                           int64_t* d_total, hipStream_t s) {
   const TasSnapshot& t = ctx->tas;
@@ -1040,8 +1059,8 @@ int tas_deschedule_launch(pas_ctx* ctx, int32_t n_strat, const pas_rule* d_rules
   TimedLaunch tl;
   timing_begin(ctx, s, PAS_K_TAS_VIOLATIONS, &tl);
   tas_violations_run_kernel<kRun, true><<<blocks, kTpb, 0, s>>>(
-      N, t.n_metrics, W64, n_strat, d_rule_off, d_rules, t.vals, t.present, t.scale_tab, d_viol,
-      PlanOut{names, d_labels, d_add, d_rem, part});
+      N, t.n_metrics, W64, n_strat, std::max(n_rules, 0), d_rule_off, d_rules, t.vals, t.present,
+      t.scale_tab, d_viol, PlanOut{names, d_labels, d_add, d_rem, part});
   timing_end(ctx, s, &tl);
   PAS_HIP(ctx, hipGetLastError());
   return label_total_launch(ctx, blocks, (int64_t)N * __builtin_popcountll(names.canon), part,

@@ -45,6 +45,7 @@ struct LazyTopkParams {
   int32_t n_pods, N, M, R, W64, k, node_base;
   const pas_rule* rules;
   const int32_t* rule_off;
+  int32_t n_rules;  // bounds rule_off: a pod's span is clamped into [0, n_rules]
   const pas_rule* prio;
   const uint64_t* cand;  // [P][W64] or null (every node a candidate)
   const int32_t* perm;   // [3][M][R] snapshot orders
@@ -131,7 +132,7 @@ __device__ bool lane_fit(const LazyTopkParams& a, int32_t p, int32_t n) {
   for (int k = 0; k < KMAX; ++k)
 #pragma unroll
     for (int q = 0; q < QW; ++q) w[k][q] = k < ncard ? w[k][q] : 0;
-  const int32_t nct = a.ncont[p];
+  const int32_t nct = min(max(a.ncont[p], 0), a.C);  // (as gas_prep_kernel: within the rows)
   for (int32_t c = 0; c < nct; ++c) {
     const int64_t b = (int64_t)p * a.C + c;
     const uint32_t m = a.mask[b];
@@ -287,7 +288,10 @@ void tas_gas_topk_kernel(LazyTopkParams a) {
                    : q.op == PAS_OP_LESS_THAN  ? kOrderAsc
                                                : kOrderIndex;
     d0 = make_int4(pos, cq > 0 ? oq * a.M + q.metric : -1, cq, 0);
-    d1 = make_int4(a.rule_off[pos], a.rule_off[pos + 1], 0, 0);
+    // (clamped into [0, n_rules] and non-decreasing: a device rule_off that is not a CSR
+    // never indexes past the rules, as the eval prep's rule_span)
+    const int32_t r0 = min(max(a.rule_off[pos], 0), a.n_rules);
+    d1 = make_int4(r0, min(max(a.rule_off[pos + 1], r0), a.n_rules), 0, 0);
   }
   const int32_t p = d0.x;
   const int32_t k = a.k;
@@ -546,6 +550,7 @@ int tas_gas_topk_launch(pas_ctx* ctx, int32_t n_pods, int32_t n_rules, const pas
   a.node_base = node_base;
   a.rules = d_rules;
   a.rule_off = d_rule_off;
+  a.n_rules = std::max(n_rules, 0);
   a.prio = d_prio;
   a.cand = d_cand;
   a.perm = t.perm;
