@@ -347,7 +347,8 @@ typedef struct pas_gas_selection {
  *                                       (sort.Strings, :216-224) order of card name;
  *                                       cards in the usage map but not in the label are
  *                                       left out (skipped at :230-234)
- * max_cards <= PAS_GAS_MAX_CARDS (64), n_res <= PAS_GAS_MAX_RES. */
+ * max_cards <= PAS_GAS_MAX_CARDS (64), n_res <= PAS_GAS_MAX_RES.  The host form rejects
+ * n_cards[n] > max_cards (PAS_EINVAL); the _device form stores such a count as max_cards. */
 int pas_gas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
                          int32_t n_res, const int32_t* n_cards, const int64_t* cap_per_gpu,
                          const int64_t* used);

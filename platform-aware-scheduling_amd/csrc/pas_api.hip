@@ -740,6 +740,14 @@ int pas_gas_snapshot_set(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t ma
   return PAS_OK;
 }
 
+// The device snapshot's card counts, which the host cannot check: a count past max_cards is
+// read as max_cards (pas_gas_snapshot_set rejects it), so every node has its result written
+// by the fit kernels that cover its cards.
+__global__ void clamp_cards_kernel(int32_t* __restrict__ n_cards, int32_t n, int32_t max_cards) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) n_cards[i] = min(n_cards[i], max_cards);
+}
+
 int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int32_t max_cards,
                                 int32_t n_res, const int32_t* d_n_cards,
                                 const int64_t* d_cap_per_gpu, const int64_t* d_used,
@@ -761,6 +769,9 @@ int pas_gas_snapshot_set_device(pas_ctx* ctx, uint64_t gen, int32_t n_nodes, int
     PAS_HIP(ctx, hipMemcpyAsync(g.used, d_used,
                                 sizeof(int64_t) * (size_t)n_nodes * max_cards * n_res,
                                 hipMemcpyDeviceToDevice, s));
+    clamp_cards_kernel<<<(unsigned)((n_nodes + 255) / 256), 256, 0, s>>>(g.n_cards, n_nodes,
+                                                                         max_cards);
+    PAS_HIP(ctx, hipGetLastError());
   }
   g.gen = gen;
   ++g.epoch;

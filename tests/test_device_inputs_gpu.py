@@ -173,3 +173,20 @@ def test_c5_device_malformed_inputs(ctx, oracle):
                             cand, gas, 0, k, 0)
     for g, w in zip((key, node, ln), want):
         np.testing.assert_array_equal(g.cpu().numpy(), w)
+
+
+def test_gas_snapshot_device_card_count_past_max(ctx, oracle):
+    """A device n_cards past max_cards is stored as max_cards (the host form's PAS_EINVAL case):
+    every node's word is the oracle's on the clamped count."""
+    from test_gas_gpu import random_gas
+    rng = np.random.default_rng(0xBAD4)
+    for k in (3, 8, 12):
+        n_cards, cap, used, req, mask, ncont = random_gas(rng, 700, k, 3, 60, 4, i915=0)
+        bad = n_cards.copy()
+        bad[::9] = k + 5
+        bad[4::17] = 2**31 - 1
+        ctx.gas_snapshot_set_device(82 + k, len(bad), k, 3, dev(bad), dev(cap), dev(used))
+        ctx.synchronize()
+        got = ctx.gas_fit(82 + k, req, mask, ncont, 0)
+        want = oracle.gas_fit(np.minimum(bad, k).astype(np.int32), cap, used, req, mask, ncont, 0)
+        np.testing.assert_array_equal(got, want)
